@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""Headline benchmark: payload GiB/s (device-resident) encode+reconstruct,
+n=1024 shards, 1 MiB messages (BASELINE.json `metric`, config 3; config 5
+is the same workload on 8 GPUs).
+
+One step = encode a batch of payloads into n shards each, evaluate the
+erasure locator of every payload, and reconstruct every payload from the
+shards that survive a random erasure of 342 of them -- all on the GPU with
+inputs already resident in HBM.  Payloads are independent, so N GPUs run N
+replicas on disjoint payload sets (weak scaling, no data-path collective);
+only the barrier and the max-over-ranks timing use torch.distributed.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "reed-solomon-novelpoly_amd", "python"))
+
+METRIC = "payload GiB/s (device-resident) encode+reconstruct, n=1024 shards, 1 MiB msgs"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", type=int, default=3, help="BASELINE config id (workload shape)")
+    ap.add_argument("--batch", type=int, default=0, help="payloads per GPU (default: the config's)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--out", default="", help="also write the JSON line to this file")
+    return ap.parse_args()
+
+
+def partition(total: int, world: int, rank: int):
+    """Contiguous payload ranges per rank (weak scaling: each rank gets `total`)."""
+    return rank * total, (rank + 1) * total
+
+
+def load_traffic(round_tag="r01"):
+    p = os.path.join(ROOT, "profiles", f"{round_tag}_pmc_summary.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f)
+    return {}
+
+
+def cpu_baseline(cfg, params, seconds):
+    """Oracle (C restatement, single thread) on a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import np_oracle
+    from novelpoly_amd import synth
+
+    orc = np_oracle.Oracle()
+    n, k, plen, erase = params.n(), params.k(), cfg["payload"], cfg["erase"]
+    done, t_total = 0, 0.0
+    while t_total < seconds and done < 10_000:
+        pl = synth.payload(10_000 + done, plen)
+        pres = synth.present_mask(10_000 + done, n, erase)
+        t0 = time.perf_counter()
+        st, shards = orc.encode(pl, n, k, n)
+        recv = [s if pres[i] else None for i, s in enumerate(shards)]
+        st2, rec = orc.reconstruct(recv, n, k)
+        t_total += time.perf_counter() - t0
+        assert st == 0 and st2 == 0 and rec[:plen] == pl
+        done += 1
+    return {
+        "value": round(done * plen / t_total / 2**30, 6),
+        "unit": "GiB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{done} payloads of config {cfg['id']} (encode + reconstruct with {erase} erasures), "
+                  f"oracle/np_oracle.c single thread, {t_total:.1f}s",
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import novelpoly_amd as npa
+    from novelpoly_amd import synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    cfg = dict(synth.CONFIGS[args.config])
+    cfg["id"] = args.config
+    params = npa.CodeParams.derive_parameters(cfg["n_wanted"], cfg["k_wanted"])
+    n, k = params.n(), params.k()
+    batch = args.batch or (cfg["batch"] if args.config != 5 else cfg["batch"] // 8)
+    plen = cfg["payload"]
+    erase = cfg["erase"] if cfg["erase"] is not None else n - k
+    ctx = npa.Context(local)
+    rs = params.make_encoder(ctx)
+    sl = rs.shard_len(plen)
+    out_len = (sl // 2) * 2 * k
+    lo, hi = partition(batch, world, rank)
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x5EED0000 + rank)
+    payloads = torch.randint(0, 256, (batch, plen), dtype=torch.uint8, device=dev, generator=g)
+    shards = torch.empty((batch, n, sl), dtype=torch.uint8, device=dev)
+    present_h = torch.from_numpy(
+        __import__("numpy").stack([synth.present_mask(i, n, erase) for i in range(lo, hi)]))
+    present = present_h.to(dev)
+    loc = torch.empty((batch, n), dtype=torch.int16, device=dev)
+    out = torch.empty((batch, out_len), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+
+    ev = {name: [] for name in ("encode", "locator", "reconstruct")}
+
+    def step(record):
+        if record:
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            e[0].record(stream)
+        npa.encode_batch_dev(params, payloads.data_ptr(), plen, plen, batch, shards.data_ptr(), n * sl, ctx=ctx,
+                             stream=sptr)
+        if record:
+            e[1].record(stream)
+        npa.error_locator_dev(n, present.data_ptr(), batch, loc.data_ptr(), ctx=ctx, stream=sptr)
+        if record:
+            e[2].record(stream)
+        npa.reconstruct_batch_dev2(params, shards.data_ptr(), sl, n * sl, present.data_ptr(), loc.data_ptr(), batch,
+                                   out.data_ptr(), out_len, ctx=ctx, stream=sptr)
+        if record:
+            e[3].record(stream)
+            ev["encode"].append((e[0], e[1]))
+            ev["locator"].append((e[1], e[2]))
+            ev["reconstruct"].append((e[2], e[3]))
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # correctness guard on the measured buffers: every payload round-trips
+    ok = bool(torch.equal(out[:, :plen], payloads))
+
+    ms_step = elapsed / args.steps * 1e3
+    total_payload = world * batch * plen
+    value = total_payload / (elapsed / args.steps) / 2**30
+
+    kt = {name: sum(a.elapsed_time(b) for a, b in pairs) / len(pairs) for name, pairs in ev.items()}
+    nshard = n  # wanted_n == n for the BASELINE configs
+    algo = {
+        "encode": batch * (plen + nshard * sl),
+        "locator": batch * (n + 2 * n),
+        "reconstruct": batch * ((n - erase) * sl + out_len),
+    }
+    traffic = load_traffic()
+    roof = {}
+    for name in kt:
+        achieved = algo[name] / (kt[name] / 1e3) / 1e9
+        roof[name] = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic.get(name),
+                      "ms": round(kt[name], 4), "algorithmic_bytes": algo[name]}
+    dominant = max(kt, key=kt.get)
+
+    line = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u16",
+        "data": "synthetic",
+        "config": {"workload": f"BASELINE config {args.config}: n_wanted={cfg['n_wanted']} "
+                               f"k_wanted={cfg['k_wanted']} (effective n={n}, k={k}), {plen} B payloads, "
+                               f"batch {batch}/GPU, encode + error locator + reconstruct with {erase} "
+                               f"random erasures per payload",
+                   "n": n, "k": k, "payload_bytes": plen, "batch_per_gpu": batch, "global_batch": world * batch,
+                   "erasures": erase, "parallelism": f"replicas x{world} (no collective)",
+                   "fast_path": params.is_faster8()},
+        "roofline": dict(roof[dominant], kernel=dominant),
+        "kernels": roof,
+        "roundtrip_ok": ok,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(cfg, params, args.cpu_seconds)
+    if rank == 0:
+        s = json.dumps(line)
+        print(s, flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(s + "\n")
+    if world > 1:
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,18 @@
+// Device table pointers shared by host engine and kernels (no device code here).
+#pragma once
+#include <cstdint>
+
+namespace np {
+
+// Device copies of the tables of field_tables.hpp (one set per context).
+struct DevTables {
+  const uint16_t* log;         // 65536
+  const uint16_t* exp;         // 65536
+  const uint16_t* skew;        // 65536, log form, 65535 = skip
+  const uint16_t* skew_add;    // 65536, additive form, 0 = skip
+  const uint16_t* log_walsh;   // 65536
+  const uint32_t* perm_pools;  // 65536 x 20 dwords
+  const uint16_t* split;       // 65536 x 128 u16
+};
+
+}  // namespace np

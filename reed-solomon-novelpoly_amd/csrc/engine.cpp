@@ -1,0 +1,554 @@
+// Host engine behind the C ABI (include/novelpoly.h): parameter derivation,
+// validation with the crate's error behaviour, per-device contexts, staging
+// and kernel dispatch.  Mirrors src/novel_poly_basis/mod.rs:24-285 of the
+// reference crate; the per-chunk / per-column loops of mod.rs:144-154 and
+// :221-236 are replaced by batched GPU kernels.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/novelpoly.h"
+#include "field_tables.hpp"
+#include "launchers.hpp"
+
+namespace {
+
+thread_local size_t g_detail[3] = {0, 0, 0};
+
+int fail(int st, size_t a = 0, size_t b = 0, size_t c = 0) {
+  g_detail[0] = a;
+  g_detail[1] = b;
+  g_detail[2] = c;
+  return st;
+}
+
+bool is_pow2(size_t x) { return x && !(x & (x - 1)); }
+size_t next_pow2(size_t x) {
+  size_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+size_t prev_pow2(size_t x) {
+  size_t p = 1;
+  while ((p << 1) <= x) p <<= 1;
+  return p;
+}
+
+// Device buffer that only grows.
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max(bytes, cap * 2);
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+struct HostBuf {  // pinned staging that only grows
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    if (e == hipSuccess) cap = bytes;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+std::mutex g_cfg_mu;
+std::vector<int> g_configured_devices;
+
+}  // namespace
+
+struct np_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  np::DevTables T{};
+  std::vector<void*> table_allocs;
+  std::mutex mu;  // serialises host-API calls (they share the scratch buffers)
+  DevBuf d_in, d_out, d_present, d_loc;
+  HostBuf h_in, h_out;
+};
+
+namespace {
+
+int dev_err(hipError_t e) {
+  if (e == hipSuccess) return NP_OK;
+  if (e == hipErrorOutOfMemory) return fail(NP_ERR_ALLOC);
+  return fail(NP_ERR_DEVICE, static_cast<size_t>(e));
+}
+
+template <class T>
+hipError_t upload(np_ctx* c, const std::vector<T>& v, const T** dst) {
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, v.size() * sizeof(T));
+  if (e != hipSuccess) return e;
+  c->table_allocs.push_back(p);
+  e = hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+  *dst = static_cast<const T*>(p);
+  return e;
+}
+
+int check_params(const np_code_params* p) {
+  if (!p) return fail(NP_ERR_INVALID_ARGUMENT);
+  if (!is_pow2(p->n) && !is_pow2(p->k)) return fail(NP_ERR_PARAMETER_MUST_BE_POWER_OF_2, p->n, p->k);
+  // The crate asserts these (inc_encode.rs:166-169, inc_reconstruct.rs:8-11).
+  if (!is_pow2(p->n) || !is_pow2(p->k) || 2 * p->k > p->n || p->n > np::kFieldSize || p->wanted_n > p->n)
+    return fail(NP_ERR_INVALID_ARGUMENT, p->n, p->k, p->wanted_n);
+  return NP_OK;
+}
+
+np::EncodeArgs enc_args(const np_code_params* p, const uint8_t* payloads, size_t len, size_t pstride, size_t batch,
+                        uint8_t* shards, size_t bstride) {
+  np::EncodeArgs a{};
+  a.payloads = payloads;
+  a.payload_len = len;
+  a.payload_stride = pstride;
+  a.batch = batch;
+  a.n = static_cast<uint32_t>(p->n);
+  a.k = static_cast<uint32_t>(p->k);
+  a.wanted_n = static_cast<uint32_t>(p->wanted_n);
+  a.shard_len = np_shard_len(p, len);
+  a.shards = shards;
+  a.batch_stride = bstride;
+  return a;
+}
+
+hipError_t launch_encode(np_ctx* c, const np::EncodeArgs& a, hipStream_t s) {
+  if (np::fast_encode_supported(a.n, a.k)) return np::launch_encode_fast(c->T, a, s);
+  return np::launch_encode_generic(c->T, a, s);
+}
+
+hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream_t s) {
+  if (np::fast_reconstruct_supported(a.n, a.k)) return np::launch_reconstruct_fast(c->T, a, s);
+  return np::launch_reconstruct_generic(c->T, a, s);
+}
+
+hipStream_t pick(np_ctx* c, void* s) { return s ? static_cast<hipStream_t>(s) : c->stream; }
+
+}  // namespace
+
+extern "C" {
+
+void np_last_error_detail(size_t out[3]) {
+  if (!out) return;
+  out[0] = g_detail[0];
+  out[1] = g_detail[1];
+  out[2] = g_detail[2];
+}
+
+const char* np_status_message(int st) {
+  switch (st) {  // errors.rs:4-28
+    case NP_OK: return "ok";
+    case NP_ERR_WANTED_SHARD_COUNT_TOO_HIGH: return "Number of wanted shards exceeds max of 2^16";
+    case NP_ERR_WANTED_SHARD_COUNT_TOO_LOW: return "Number of wanted shards must be at least 2";
+    case NP_ERR_WANTED_PAYLOAD_SHARD_COUNT_TOO_LOW: return "Number of wanted payload shards must be at least 1";
+    case NP_ERR_PAYLOAD_SIZE_IS_ZERO: return "Size of the payload is zero";
+    case NP_ERR_NEED_MORE_SHARDS: return "Needs more shards to recover";
+    case NP_ERR_PARAMETER_MUST_BE_POWER_OF_2: return "Parameters: n and k both must be a power of 2";
+    case NP_ERR_INCONSISTENT_SHARD_LENGTHS: return "Shards do have inconsistent lengths";
+    case NP_ERR_EMPTY_SHARD: return "Shard is empty";
+    case NP_ERR_INVALID_ARGUMENT: return "invalid argument (a case the reference asserts on)";
+    case NP_ERR_DEVICE: return "HIP runtime failure";
+    case NP_ERR_ALLOC: return "allocation failure";
+    case NP_ERR_NO_DEVICE: return "no gfx950 device available";
+    default: return "unknown status";
+  }
+}
+
+const char* np_version(void) { return "novelpoly-mi355x 0.1.0 (gfx950)"; }
+
+size_t np_recoverability_subset_size(size_t n) { return (n ? (n - 1) / 3 : 0) + 1; }
+
+int np_derive_parameters(size_t n_wanted, size_t k_wanted, np_code_params* out) {
+  if (!out) return fail(NP_ERR_INVALID_ARGUMENT);
+  if (n_wanted < 2) return fail(NP_ERR_WANTED_SHARD_COUNT_TOO_LOW, n_wanted);
+  if (k_wanted < 1) return fail(NP_ERR_WANTED_PAYLOAD_SHARD_COUNT_TOO_LOW, k_wanted);
+  const size_t k = prev_pow2(k_wanted), n = next_pow2(n_wanted);
+  if (n > np::kFieldSize) return fail(NP_ERR_WANTED_SHARD_COUNT_TOO_HIGH, n_wanted);
+  out->n = n;
+  out->k = k;
+  out->wanted_n = n_wanted;
+  return NP_OK;
+}
+
+int np_params_new(size_t n, size_t k, size_t wanted_n, np_code_params* out) {
+  if (!out) return fail(NP_ERR_INVALID_ARGUMENT);
+  if (!is_pow2(n) && !is_pow2(k)) return fail(NP_ERR_PARAMETER_MUST_BE_POWER_OF_2, n, k);
+  out->n = n;
+  out->k = k;
+  out->wanted_n = wanted_n;
+  return NP_OK;
+}
+
+size_t np_shard_len(const np_code_params* p, size_t payload_size) {
+  if (!p || p->k == 0) return 0;
+  const size_t syms = (payload_size + 1) / 2;
+  return ((syms + p->k - 1) / p->k) * 2;
+}
+
+int np_is_fast_path(const np_code_params* p) {
+  if (!p) return 0;
+  return np::fast_encode_supported(static_cast<uint32_t>(p->n), static_cast<uint32_t>(p->k)) ? 1 : 0;
+}
+
+int np_ctx_create(int device, np_ctx** out) {
+  if (!out) return fail(NP_ERR_INVALID_ARGUMENT);
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return fail(NP_ERR_NO_DEVICE);
+  if (device < 0) {
+    if (hipGetDevice(&device) != hipSuccess) return fail(NP_ERR_NO_DEVICE);
+  }
+  if (device >= count) return fail(NP_ERR_NO_DEVICE, static_cast<size_t>(device));
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return fail(NP_ERR_NO_DEVICE);
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return fail(NP_ERR_NO_DEVICE, static_cast<size_t>(device));
+  if (hipSetDevice(device) != hipSuccess) return fail(NP_ERR_DEVICE);
+  np_ctx* c = new (std::nothrow) np_ctx();
+  if (!c) return fail(NP_ERR_ALLOC);
+  c->device = device;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  const np::HostTables& t = np::host_tables();
+  if (e == hipSuccess) e = upload(c, t.log, &c->T.log);
+  if (e == hipSuccess) e = upload(c, t.exp, &c->T.exp);
+  if (e == hipSuccess) e = upload(c, t.skew, &c->T.skew);
+  if (e == hipSuccess) e = upload(c, t.skew_add, &c->T.skew_add);
+  if (e == hipSuccess) e = upload(c, t.log_walsh, &c->T.log_walsh);
+  if (e == hipSuccess) e = upload(c, t.perm_pools, &c->T.perm_pools);
+  if (e == hipSuccess) e = upload(c, t.split, &c->T.split);
+  if (e == hipSuccess) {
+    std::lock_guard<std::mutex> g(g_cfg_mu);
+    if (std::find(g_configured_devices.begin(), g_configured_devices.end(), device) == g_configured_devices.end()) {
+      e = np::configure_generic_kernels();
+      if (e == hipSuccess) e = np::configure_fast_kernels();
+      if (e == hipSuccess) g_configured_devices.push_back(device);
+    }
+  }
+  if (e != hipSuccess) {
+    np_ctx_destroy(c);
+    return dev_err(e);
+  }
+  *out = c;
+  return NP_OK;
+}
+
+void np_ctx_destroy(np_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (void* p : c->table_allocs) (void)hipFree(p);
+  c->d_in.release();
+  c->d_out.release();
+  c->d_present.release();
+  c->d_loc.release();
+  c->h_in.release();
+  c->h_out.release();
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+void* np_ctx_stream(np_ctx* c) { return c ? static_cast<void*>(c->stream) : nullptr; }
+int np_ctx_device(np_ctx* c) { return c ? c->device : -1; }
+
+int np_ctx_synchronize(np_ctx* c) {
+  if (!c) return fail(NP_ERR_INVALID_ARGUMENT);
+  (void)hipSetDevice(c->device);
+  return dev_err(hipStreamSynchronize(c->stream));
+}
+
+// --------------------------------------------------------------- encode ----
+int np_rs_encode(np_ctx* c, const np_code_params* p, const uint8_t* payload, size_t len, uint8_t* shards_out,
+                 size_t shard_len) {
+  if (!c) return fail(NP_ERR_INVALID_ARGUMENT);
+  int st = check_params(p);
+  if (st) return st;
+  if (len == 0) return fail(NP_ERR_PAYLOAD_SIZE_IS_ZERO);  // mod.rs:118-120
+  if (!payload || !shards_out || shard_len != np_shard_len(p, len)) return fail(NP_ERR_INVALID_ARGUMENT);
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
+  const size_t out_bytes = p->wanted_n * shard_len;
+  hipError_t e = c->d_in.ensure(len);
+  if (e == hipSuccess) e = c->d_out.ensure(std::max<size_t>(out_bytes, 1));
+  if (e == hipSuccess) e = c->h_in.ensure(len);
+  if (e == hipSuccess) e = c->h_out.ensure(std::max<size_t>(out_bytes, 1));
+  if (e != hipSuccess) return dev_err(e);
+  std::memcpy(c->h_in.p, payload, len);
+  e = hipMemcpyAsync(c->d_in.p, c->h_in.p, len, hipMemcpyHostToDevice, c->stream);
+  np::EncodeArgs a = enc_args(p, c->d_in.as<uint8_t>(), len, len, 1, c->d_out.as<uint8_t>(), out_bytes);
+  if (e == hipSuccess) e = launch_encode(c, a, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(c->h_out.p, c->d_out.p, out_bytes, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) return dev_err(e);
+  std::memcpy(shards_out, c->h_out.p, out_bytes);
+  return NP_OK;
+}
+
+int np_encode(np_ctx* c, const uint8_t* payload, size_t len, size_t n_min, uint8_t* shards_out, size_t shard_len) {
+  // encode.rs:6-11
+  np_code_params p;
+  int st = np_derive_parameters(n_min, np_recoverability_subset_size(n_min), &p);
+  if (st) return st;
+  return np_rs_encode(c, &p, payload, len, shards_out, shard_len);
+}
+
+int np_encode_batch_dev(np_ctx* c, const np_code_params* p, const uint8_t* d_payloads, size_t len, size_t pstride,
+                        size_t batch, uint8_t* d_shards, size_t bstride, void* stream) {
+  if (!c) return fail(NP_ERR_INVALID_ARGUMENT);
+  int st = check_params(p);
+  if (st) return st;
+  if (len == 0) return fail(NP_ERR_PAYLOAD_SIZE_IS_ZERO);
+  const size_t sl = np_shard_len(p, len);
+  if (!d_payloads || !d_shards || pstride < len || bstride < p->wanted_n * sl) return fail(NP_ERR_INVALID_ARGUMENT);
+  (void)hipSetDevice(c->device);
+  np::EncodeArgs a = enc_args(p, d_payloads, len, pstride, batch, d_shards, bstride);
+  return dev_err(launch_encode(c, a, pick(c, stream)));
+}
+
+// ---------------------------------------------------------- reconstruct ----
+int np_error_locator_dev(np_ctx* c, size_t n, const uint8_t* d_present, size_t batch, uint16_t* d_loc,
+                         void* stream) {
+  if (!c || !d_present || !d_loc || !is_pow2(n) || n > np::kFieldSize) return fail(NP_ERR_INVALID_ARGUMENT);
+  (void)hipSetDevice(c->device);
+  return dev_err(np::launch_error_locator(c->T, static_cast<uint32_t>(n), d_present, batch, d_loc, pick(c, stream)));
+}
+
+int np_reconstruct_batch_dev2(np_ctx* c, const np_code_params* p, const uint8_t* d_shards, size_t shard_len,
+                              size_t bstride, const uint8_t* d_present, const uint16_t* d_loc, size_t batch,
+                              uint8_t* d_out, size_t out_stride, void* stream) {
+  if (!c) return fail(NP_ERR_INVALID_ARGUMENT);
+  int st = check_params(p);
+  if (st) return st;
+  if (shard_len == 0 || (shard_len & 1)) return fail(NP_ERR_EMPTY_SHARD);
+  if (!d_shards || !d_present || !d_loc || !d_out || bstride < p->n * shard_len ||
+      out_stride < (shard_len / 2) * 2 * p->k)
+    return fail(NP_ERR_INVALID_ARGUMENT);
+  (void)hipSetDevice(c->device);
+  np::ReconstructArgs a{};
+  a.shards = d_shards;
+  a.shard_len = shard_len;
+  a.batch_stride = bstride;
+  a.present = d_present;
+  a.locators = d_loc;
+  a.batch = batch;
+  a.n = static_cast<uint32_t>(p->n);
+  a.k = static_cast<uint32_t>(p->k);
+  a.out = d_out;
+  a.out_stride = out_stride;
+  return dev_err(launch_reconstruct(c, a, pick(c, stream)));
+}
+
+int np_reconstruct_batch_dev(np_ctx* c, const np_code_params* p, const uint8_t* d_shards, size_t shard_len,
+                             size_t bstride, const uint8_t* present, size_t batch, uint8_t* d_out, size_t out_stride,
+                             void* stream) {
+  if (!c || !present) return fail(NP_ERR_INVALID_ARGUMENT);
+  int st = check_params(p);
+  if (st) return st;
+  for (size_t b = 0; b < batch; ++b) {  // mod.rs:171-180
+    size_t have = 0;
+    for (size_t v = 0; v < p->n; ++v) have += present[b * p->n + v] ? 1 : 0;
+    if (have < p->k) return fail(NP_ERR_NEED_MORE_SHARDS, have, p->k, p->n);
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick(c, stream);
+  hipError_t e = c->d_present.ensure(std::max<size_t>(batch * p->n, 1));
+  if (e == hipSuccess) e = c->d_loc.ensure(std::max<size_t>(batch * p->n * sizeof(uint16_t), 2));
+  if (e != hipSuccess) return dev_err(e);
+  e = hipMemcpyAsync(c->d_present.p, present, batch * p->n, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess)
+    e = np::launch_error_locator(c->T, static_cast<uint32_t>(p->n), c->d_present.as<uint8_t>(), batch,
+                                 c->d_loc.as<uint16_t>(), s);
+  if (e != hipSuccess) return dev_err(e);
+  st = np_reconstruct_batch_dev2(c, p, d_shards, shard_len, bstride, c->d_present.as<uint8_t>(),
+                                 c->d_loc.as<uint16_t>(), batch, d_out, out_stride, s);
+  if (st) return st;
+  // present mask was copied from pageable host memory: make the call
+  // synchronous with respect to it before returning.
+  return dev_err(hipStreamSynchronize(s));
+}
+
+int np_rs_reconstruct(np_ctx* c, const np_code_params* p, const uint8_t* const* shards, const size_t* lens,
+                      size_t n_received, uint8_t* out, size_t cap, size_t* out_len) {
+  if (!c || !p || (n_received && (!shards || !lens))) return fail(NP_ERR_INVALID_ARGUMENT);
+  if (!is_pow2(p->n) && !is_pow2(p->k)) return fail(NP_ERR_PARAMETER_MUST_BE_POWER_OF_2, p->n, p->k);
+  const size_t n = p->n, k = p->k;
+  // mod.rs:163-180: pad/truncate to n, erasures, existential count
+  std::vector<uint8_t> present(n, 0);
+  size_t have = 0;
+  for (size_t i = 0; i < n && i < n_received; ++i) {
+    present[i] = shards[i] ? 1 : 0;
+    have += present[i];
+  }
+  if (have < k) return fail(NP_ERR_NEED_MORE_SHARDS, have, k, n);
+  // mod.rs:183-214: shard length from the first present shard
+  size_t first = 0;
+  while (!present[first]) ++first;
+  const size_t syms = (lens[first] + 1) / 2;
+  if (syms == 0) return fail(NP_ERR_EMPTY_SHARD);
+  for (size_t i = first + 1; i < n; ++i)
+    if (present[i] && (lens[i] + 1) / 2 != syms) return fail(NP_ERR_INCONSISTENT_SHARD_LENGTHS, syms, (lens[i] + 1) / 2);
+  int st = check_params(p);
+  if (st) return st;
+  const size_t need = syms * 2 * k;
+  if (!out || !out_len || cap < need) return fail(NP_ERR_INVALID_ARGUMENT, need);
+  const size_t sl = 2 * syms;
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
+  hipError_t e = c->h_in.ensure(n * sl);
+  if (e == hipSuccess) e = c->d_in.ensure(n * sl);
+  if (e == hipSuccess) e = c->d_out.ensure(need);
+  if (e == hipSuccess) e = c->h_out.ensure(need);
+  if (e == hipSuccess) e = c->d_present.ensure(n);
+  if (e == hipSuccess) e = c->d_loc.ensure(n * sizeof(uint16_t));
+  if (e != hipSuccess) return dev_err(e);
+  uint8_t* stage = c->h_in.as<uint8_t>();
+  for (size_t i = 0; i < n; ++i) {
+    uint8_t* row = stage + i * sl;
+    if (present[i]) {
+      std::memcpy(row, shards[i], lens[i]);
+      if (lens[i] < sl) std::memset(row + lens[i], 0, sl - lens[i]);  // WrappedShard zero pad
+    } else {
+      std::memset(row, 0, sl);
+    }
+  }
+  hipStream_t s = c->stream;
+  e = hipMemcpyAsync(c->d_in.p, stage, n * sl, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(c->d_present.p, present.data(), n, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess)
+    e = np::launch_error_locator(c->T, static_cast<uint32_t>(n), c->d_present.as<uint8_t>(), 1,
+                                 c->d_loc.as<uint16_t>(), s);
+  if (e == hipSuccess) {
+    np::ReconstructArgs a{};
+    a.shards = c->d_in.as<uint8_t>();
+    a.shard_len = sl;
+    a.batch_stride = n * sl;
+    a.present = c->d_present.as<uint8_t>();
+    a.locators = c->d_loc.as<uint16_t>();
+    a.batch = 1;
+    a.n = static_cast<uint32_t>(n);
+    a.k = static_cast<uint32_t>(k);
+    a.out = c->d_out.as<uint8_t>();
+    a.out_stride = need;
+    e = launch_reconstruct(c, a, s);
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(c->h_out.p, c->d_out.p, need, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return dev_err(e);
+  std::memcpy(out, c->h_out.p, need);
+  *out_len = need;
+  return NP_OK;
+}
+
+int np_reconstruct(np_ctx* c, const uint8_t* const* shards, const size_t* lens, size_t n_received,
+                   size_t validator_count, uint8_t* out, size_t cap, size_t* out_len) {
+  // reconstruct.rs:4-9
+  np_code_params p;
+  int st = np_derive_parameters(validator_count, np_recoverability_subset_size(validator_count), &p);
+  if (st) return st;
+  return np_rs_reconstruct(c, &p, shards, lens, n_received, out, cap, out_len);
+}
+
+int np_rs_reconstruct_from_systematic(np_ctx* c, const np_code_params* p, const uint8_t* const* chunks,
+                                      const size_t* lens, size_t n_chunks, uint8_t* out, size_t cap,
+                                      size_t* out_len) {
+  // mod.rs:247-285: a pure gather of the first k shards, no field arithmetic.
+  if (!c || !p || (n_chunks && (!chunks || !lens))) return fail(NP_ERR_INVALID_ARGUMENT);
+  if (n_chunks == 0) return fail(NP_ERR_NEED_MORE_SHARDS, 0, p->k, p->n);
+  if (n_chunks < p->k) return fail(NP_ERR_NEED_MORE_SHARDS, n_chunks, p->k, p->n);
+  const size_t syms = (lens[0] + 1) / 2;
+  if (syms == 0) return fail(NP_ERR_EMPTY_SHARD);
+  for (size_t i = 0; i < n_chunks; ++i)
+    if ((lens[i] + 1) / 2 != syms) return fail(NP_ERR_INCONSISTENT_SHARD_LENGTHS, syms, (lens[i] + 1) / 2);
+  const size_t k = p->k, need = syms * 2 * k;
+  if (!out || !out_len || cap < need) return fail(NP_ERR_INVALID_ARGUMENT, need);
+  for (size_t s = 0; s < syms; ++s)
+    for (size_t j = 0; j < k; ++j) {
+      const uint8_t* ch = chunks[j];
+      out[s * 2 * k + 2 * j] = (2 * s < lens[j]) ? ch[2 * s] : 0;
+      out[s * 2 * k + 2 * j + 1] = (2 * s + 1 < lens[j]) ? ch[2 * s + 1] : 0;
+    }
+  *out_len = need;
+  return NP_OK;
+}
+
+// --------------------------------------------------------- parity hooks ----
+int np_afft_dev(np_ctx* c, uint16_t* d, size_t size, size_t index, size_t cols, void* stream) {
+  if (!c || !d || !is_pow2(size) || size > np::kFieldSize || index + size > np::kFieldSize)
+    return fail(NP_ERR_INVALID_ARGUMENT);
+  (void)hipSetDevice(c->device);
+  return dev_err(np::launch_afft(c->T, d, static_cast<uint32_t>(size), static_cast<uint32_t>(index), cols, false,
+                                 pick(c, stream)));
+}
+
+int np_inverse_afft_dev(np_ctx* c, uint16_t* d, size_t size, size_t index, size_t cols, void* stream) {
+  if (!c || !d || !is_pow2(size) || size > np::kFieldSize || index + size > np::kFieldSize)
+    return fail(NP_ERR_INVALID_ARGUMENT);
+  (void)hipSetDevice(c->device);
+  return dev_err(np::launch_afft(c->T, d, static_cast<uint32_t>(size), static_cast<uint32_t>(index), cols, true,
+                                 pick(c, stream)));
+}
+
+int np_walsh_dev(np_ctx* c, uint16_t* d, size_t size, void* stream) {
+  if (!c || !d || !is_pow2(size) || size > np::kFieldSize) return fail(NP_ERR_INVALID_ARGUMENT);
+  (void)hipSetDevice(c->device);
+  return dev_err(np::launch_walsh(d, static_cast<uint32_t>(size), pick(c, stream)));
+}
+
+int np_mul_dev(np_ctx* c, const uint16_t* a, const uint16_t* m, uint16_t* o, size_t count, void* stream) {
+  if (!c || !a || !m || !o) return fail(NP_ERR_INVALID_ARGUMENT);
+  (void)hipSetDevice(c->device);
+  return dev_err(np::launch_mul(c->T, a, m, o, count, pick(c, stream)));
+}
+
+int np_encode_low_dev(np_ctx* c, const uint16_t* d, size_t k, uint16_t* cw, size_t n, size_t cols, void* stream) {
+  if (!c || !d || !cw || !is_pow2(n) || !is_pow2(k) || 2 * k > n || n > np::kFieldSize)
+    return fail(NP_ERR_INVALID_ARGUMENT);
+  (void)hipSetDevice(c->device);
+  return dev_err(
+      np::launch_encode_low(c->T, d, static_cast<uint32_t>(k), cw, static_cast<uint32_t>(n), cols, pick(c, stream)));
+}
+
+int np_decode_main_dev(np_ctx* c, uint16_t* cw, size_t upto, const uint8_t* d_present, const uint16_t* d_loc,
+                       size_t n, size_t cols, void* stream) {
+  if (!c || !cw || !d_present || !d_loc || !is_pow2(n) || n > np::kFieldSize || upto > n)
+    return fail(NP_ERR_INVALID_ARGUMENT);
+  (void)hipSetDevice(c->device);
+  return dev_err(np::launch_decode_main(c->T, cw, static_cast<uint32_t>(upto), d_present, d_loc,
+                                        static_cast<uint32_t>(n), cols, pick(c, stream)));
+}
+
+}  // extern "C"

@@ -1,0 +1,141 @@
+// Host construction of field tables, skews and multiplier lookup tables.
+// See field_tables.hpp for the reference citations.
+#include "field_tables.hpp"
+
+#include <mutex>
+
+namespace np {
+namespace {
+
+// Cantor basis of GF(2^16) over GF(2) used by the crate (f2e16.rs:6).
+constexpr uint16_t kCantorBasis[16] = {1,     44234, 15374, 5694,  50562, 60718, 37196, 16402,
+                                       27800, 4312,  27250, 47360, 64952, 64308, 65336, 39198};
+constexpr uint32_t kReductionPoly = 0x1002d;  // x^16 + x^5 + x^3 + x^2 + 1 (GENERATOR 0x2D)
+
+void fwht_mod_onemask(uint16_t* v, uint32_t n) {
+  // inc_log_mul.rs:92-114: butterflies (a+b, a-b) over Z/65535 with end-around carry.
+  for (uint32_t half = 1; half < n; half <<= 1) {
+    for (uint32_t base = 0; base < n; base += half << 1) {
+      for (uint32_t i = base; i < base + half; ++i) {
+        uint32_t a = v[i], b = v[i + half];
+        uint32_t sum = a + b, dif = a + kOneMask - b;
+        v[i] = static_cast<uint16_t>((sum & 0xffffu) + (sum >> 16));
+        v[i + half] = static_cast<uint16_t>((dif & 0xffffu) + (dif >> 16));
+      }
+    }
+  }
+}
+
+void build(HostTables& t) {
+  t.log.assign(kFieldSize, 0);
+  t.exp.assign(kFieldSize, 0);
+  // polynomial-basis element -> log, by stepping powers of the generator.
+  std::vector<uint16_t> log_of_poly(kFieldSize, 0);
+  uint32_t power = 1;
+  for (uint32_t e = 0; e < kOneMask; ++e) {
+    log_of_poly[power] = static_cast<uint16_t>(e);
+    power <<= 1;
+    if (power >> 16) power ^= kReductionPoly;
+  }
+  log_of_poly[0] = static_cast<uint16_t>(kOneMask);
+  // Cantor coordinates -> polynomial element (XOR of the selected basis vectors).
+  std::vector<uint16_t> poly_of(kFieldSize, 0);
+  for (int bit = 0; bit < 16; ++bit) {
+    const uint32_t top = 1u << bit;
+    for (uint32_t low = 0; low < top; ++low) poly_of[top | low] = poly_of[low] ^ kCantorBasis[bit];
+  }
+  for (uint32_t a = 0; a < kFieldSize; ++a) t.log[a] = log_of_poly[poly_of[a]];
+  for (uint32_t a = 0; a < kFieldSize; ++a) t.exp[t.log[a]] = static_cast<uint16_t>(a);
+  t.exp[kOneMask] = t.exp[0];
+
+  t.log_walsh = t.log;
+  t.log_walsh[0] = 0;
+  fwht_mod_onemask(t.log_walsh.data(), kFieldSize);
+
+  // Skew factors (inc_afft.rs:386-445).
+  std::vector<uint16_t> sk(kFieldSize, 0);
+  uint16_t basis[15];
+  for (int i = 0; i < 15; ++i) basis[i] = static_cast<uint16_t>(2u << i);
+  for (int m = 0; m < 15; ++m) {
+    const uint32_t first = (1u << m) - 1, stride = 2u << m;
+    sk[first] = 0;
+    for (int i = m; i < 15; ++i) {
+      const uint32_t span = 2u << i;
+      for (uint32_t j = first; j < span; j += stride) sk[j + span] = sk[j] ^ basis[i];
+    }
+    const uint16_t prod = host_mul(t, basis[m], t.log[basis[m] ^ 1]);
+    basis[m] = static_cast<uint16_t>(kOneMask - t.log[prod]);
+    for (int i = m + 1; i < 15; ++i) {
+      const uint32_t e = (static_cast<uint32_t>(t.log[basis[i] ^ 1]) + basis[m]) % kOneMask;
+      basis[i] = host_mul(t, basis[i], static_cast<uint16_t>(e));
+    }
+  }
+  t.skew.assign(kFieldSize, static_cast<uint16_t>(kOneMask));
+  t.skew_add.assign(kFieldSize, 0);
+  for (uint32_t i = 0; i < kOneMask; ++i) {
+    t.skew[i] = t.log[sk[i]];
+    t.skew_add[i] = sk[i];
+  }
+
+  // Multiplier lookup tables, indexed by the additive multiplier c.
+  t.split.assign(static_cast<size_t>(kFieldSize) * kSplitEntries, 0);
+  t.perm_pools.assign(static_cast<size_t>(kFieldSize) * kPermPoolWords, 0);
+  for (uint32_t c = 0; c < kFieldSize; ++c) {
+    uint16_t* s = &t.split[static_cast<size_t>(c) * kSplitEntries];
+    for (uint32_t v = 0; v < 64; ++v) s[v] = host_mul_add(t, static_cast<uint16_t>(v), static_cast<uint16_t>(c));
+    for (uint32_t v = 0; v < 32; ++v) {
+      s[64 + v] = host_mul_add(t, static_cast<uint16_t>(v << 6), static_cast<uint16_t>(c));
+      s[96 + v] = host_mul_add(t, static_cast<uint16_t>(v << 11), static_cast<uint16_t>(c));
+    }
+    // v_perm pools: input byte plane P (0 = low byte, 1 = high byte), bit group
+    // G (bits 0-2, 3-5, 6-7 of that byte) -> contribution to output byte O.
+    // Layout (dwords): for O in {lo, hi}: [P0G0 lo,hi][P0G1 lo,hi][P0G2][P1G0 lo,hi][P1G1 lo,hi][P1G2]
+    uint32_t* pool = &t.perm_pools[static_cast<size_t>(c) * kPermPoolWords];
+    int w = 0;
+    for (int out_byte = 0; out_byte < 2; ++out_byte) {
+      for (int plane = 0; plane < 2; ++plane) {
+        const int shifts[3] = {0, 3, 6};
+        const int widths[3] = {3, 3, 2};
+        for (int g = 0; g < 3; ++g) {
+          uint8_t entries[8] = {0};
+          for (int v = 0; v < (1 << widths[g]); ++v) {
+            const uint16_t in = static_cast<uint16_t>((v << shifts[g]) << (8 * plane));
+            const uint16_t prod = host_mul_add(t, in, static_cast<uint16_t>(c));
+            entries[v] = static_cast<uint8_t>(out_byte ? (prod >> 8) : (prod & 0xff));
+          }
+          // v_perm_b32(S0, S1, sel): selector 0..3 -> bytes of S1, 4..7 -> bytes of S0.
+          const uint32_t lo = entries[0] | (entries[1] << 8) | (entries[2] << 16) | (uint32_t(entries[3]) << 24);
+          const uint32_t hi = entries[4] | (entries[5] << 8) | (entries[6] << 16) | (uint32_t(entries[7]) << 24);
+          if (widths[g] == 3) {
+            pool[w++] = lo;  // goes to S1 (a VGPR)
+            pool[w++] = hi;  // goes to S0 (an SGPR)
+          } else {
+            pool[w++] = lo;  // 4-entry table: S0 == S1
+          }
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+
+uint16_t host_mul(const HostTables& t, uint16_t a, uint16_t m) {
+  if (a == 0) return 0;
+  const uint32_t s = static_cast<uint32_t>(t.log[a]) + m;
+  return t.exp[(s & 0xffffu) + (s >> 16)];
+}
+
+uint16_t host_mul_add(const HostTables& t, uint16_t a, uint16_t c) {
+  if (a == 0 || c == 0) return 0;
+  return host_mul(t, a, t.log[c]);
+}
+
+const HostTables& host_tables() {
+  static HostTables tables;
+  static std::once_flag once;
+  std::call_once(once, [] { build(tables); });
+  return tables;
+}
+
+}  // namespace np

@@ -1,0 +1,41 @@
+// Host-side construction of the GF(2^16) tables the kernels consume.
+//
+// Generated from scratch at context creation (the crate generates them at
+// build time: reed-solomon-novelpoly/inc_gen_field_tables.rs:29-93, skew
+// factors at src/field/inc_afft.rs:386-445).  Field constants:
+// src/field/f2e16.rs:4-12.
+#pragma once
+#include <cstdint>
+#include <vector>
+
+namespace np {
+
+constexpr uint32_t kFieldSize = 65536;
+constexpr uint32_t kOneMask = 65535;  // ONEMASK: group order, also the "skip" skew sentinel
+
+struct HostTables {
+  std::vector<uint16_t> log;        // Cantor coordinates -> discrete log   (LOG_TABLE)
+  std::vector<uint16_t> exp;        // discrete log -> Cantor coordinates   (EXP_TABLE)
+  std::vector<uint16_t> skew;       // 65536 entries, log form, [i]==65535 -> multiply skipped (AFFT.skews)
+  std::vector<uint16_t> skew_add;   // additive (field element) form of skew, 0 for the sentinel
+  std::vector<uint16_t> log_walsh;  // LOG_WALSH
+  // Per additive multiplier c (65536 of them): byte tables for the v_perm
+  // multiplier (see kernels.hip, "byte-planar quad multiply"); 20 dwords each.
+  std::vector<uint32_t> perm_pools;
+  // Per additive multiplier c: 6/5/5-bit split product tables, 128 u16 each:
+  // [0,64) c*v for v = bits 0..5, [64,96) c*(v<<6), [96,128) c*(v<<11).
+  std::vector<uint16_t> split;
+};
+
+// Built once, thread-safe.
+const HostTables& host_tables();
+
+// a * g^m with the crate's conventions (inc_log_mul.rs:42-49).
+uint16_t host_mul(const HostTables& t, uint16_t a, uint16_t m);
+// a * c for two field elements in additive (Cantor coordinate) form.
+uint16_t host_mul_add(const HostTables& t, uint16_t a, uint16_t c);
+
+constexpr int kPermPoolWords = 20;
+constexpr int kSplitEntries = 128;
+
+}  // namespace np

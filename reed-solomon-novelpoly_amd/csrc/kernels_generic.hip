@@ -1,0 +1,377 @@
+// Generic gfx950 kernels: correct for every power-of-two n <= 65536 and
+// k <= n/2 (any CodeParams the crate can derive).  One workgroup owns a
+// tile of codeword columns held in LDS; its 256 threads sweep the butterflies
+// of each transform level.  The multiply is the crate's LOG/EXP gather
+// (inc_log_mul.rs:42-49) from L2-resident tables, so this path is the
+// correctness fallback, not the fast path (kernels_fast.hip).
+#include "device_common.hpp"
+#include "launchers.hpp"
+
+namespace np {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr uint32_t kLdsBudgetSyms = 32768;  // 64 KiB of u16 per workgroup by default
+
+// One level of the additive FFT / inverse FFT over `nseg` segments of `size`
+// symbols.  Segment g starts at lds + seg_base(g) and uses skew index offset
+// seg_index(g) (inc_afft.rs:139-214 / 267-332).
+struct Segs {
+  uint32_t col_stride;  // symbols between columns
+  uint32_t first_off;   // offset of segment 0 within a column
+  uint32_t seg_per_col; // segments per column
+  uint32_t size;        // symbols per segment
+  uint32_t index0;      // skew index of segment 0
+  uint32_t index_step;  // skew index increment per segment (= size for encode shifts)
+};
+
+template <bool INVERSE>
+__device__ void lds_transform(const DevTables& T, uint16_t* lds, const Segs& sg, uint32_t ncols) {
+  const uint32_t half = sg.size >> 1;
+  const uint32_t total = ncols * sg.seg_per_col * half;
+  for (uint32_t step = 0; (1u << step) < sg.size; ++step) {
+    const uint32_t d = INVERSE ? (1u << step) : (half >> step);
+    for (uint32_t b = threadIdx.x; b < total; b += blockDim.x) {
+      const uint32_t seg = b / half, r = b - seg * half;
+      const uint32_t col = seg / sg.seg_per_col, sc = seg - col * sg.seg_per_col;
+      uint16_t* v = lds + col * sg.col_stride + sg.first_off + sc * sg.size;
+      const uint32_t grp = r / d, off = r - grp * d;
+      const uint32_t i = grp * 2 * d + off;
+      const uint32_t j = grp * 2 * d + d;  // group key, inc_afft.rs:457 / 573
+      const uint32_t sk = T.skew[j + sg.index0 + sc * sg.index_step - 1];
+      uint32_t x = v[i], y = v[i + d];
+      if (INVERSE) {
+        y ^= x;
+        if (sk != kQ) x ^= gf_mul_log(T, y, sk);
+      } else {
+        if (sk != kQ) x ^= gf_mul_log(T, y, sk);
+        y ^= x;
+      }
+      v[i] = static_cast<uint16_t>(x);
+      v[i + d] = static_cast<uint16_t>(y);
+    }
+    __syncthreads();
+  }
+}
+
+// Formal derivative restricted to outputs [0, upto) of each column, in place
+// (inc_afft.rs:17-31; closed form SURVEY F7).  Outputs are produced in
+// increasing order in chunks of blockDim.x; a chunk only reads positions >= its
+// own first position, so in-place update after a barrier is exact.
+__device__ void lds_formal_derivative(uint16_t* lds, uint32_t col_stride, uint32_t n, uint32_t upto,
+                                      uint32_t ncols) {
+  const uint32_t total = ncols * upto;
+  for (uint32_t base = 0; base < total; base += blockDim.x) {
+    const uint32_t e = base + threadIdx.x;
+    uint32_t acc = 0, col = 0, j = 0;
+    if (e < total) {
+      col = e / upto;
+      j = e - col * upto;
+      const uint16_t* v = lds + col * col_stride;
+      acc = v[j];
+      for (uint32_t l = 1; l < n; l <<= 1)
+        if (!(j & l)) acc ^= v[j | l];
+    }
+    __syncthreads();
+    if (e < total) lds[col * col_stride + j] = static_cast<uint16_t>(acc);
+    __syncthreads();
+  }
+}
+
+uint32_t cols_for(uint32_t syms_per_col) {
+  uint32_t c = kLdsBudgetSyms / syms_per_col;
+  if (c < 1) c = 1;
+  if (c > 64) c = 64;
+  return c;
+}
+
+// ---------------------------------------------------------------- encode ----
+// grid = (tiles of chunks, batch).  mod.rs:144-154 + inc_encode.rs:165-208.
+__global__ __launch_bounds__(kThreads) void k_encode_generic(DevTables T, EncodeArgs a, uint32_t nchunks,
+                                                             uint32_t cols) {
+  extern __shared__ uint16_t lds[];
+  const size_t b = blockIdx.y;
+  const uint32_t ch0 = blockIdx.x * cols;
+  const uint32_t ncol = min(cols, nchunks - ch0);
+  const uint32_t n = a.n, k = a.k;
+  const uint8_t* p = a.payloads + b * a.payload_stride;
+  uint8_t* out = a.shards + b * a.batch_stride;
+
+  for (uint32_t e = threadIdx.x; e < ncol * k; e += blockDim.x) {
+    const uint32_t c = e / k, i = e - c * k;
+    lds[c * n + i] = be_sym(p, (static_cast<size_t>(ch0 + c) * k + i) * 2, a.payload_len);
+  }
+  __syncthreads();
+  // systematic part: codeword[0..k) == data (inc_encode.rs:47)
+  const uint32_t sys = min(k, a.wanted_n);
+  for (uint32_t e = threadIdx.x; e < sys * ncol; e += blockDim.x) {
+    const uint32_t v = e / ncol, c = e - v * ncol;
+    const uint16_t s = lds[c * n + v];
+    uint8_t* q = out + static_cast<size_t>(v) * a.shard_len + 2 * static_cast<size_t>(ch0 + c);
+    q[0] = static_cast<uint8_t>(s >> 8);
+    q[1] = static_cast<uint8_t>(s);
+  }
+  __syncthreads();
+  lds_transform<true>(T, lds, Segs{n, 0, 1, k, 0, 0}, ncol);  // inverse_afft(k, 0)
+  const uint32_t nseg = n / k - 1;
+  for (uint32_t e = threadIdx.x; e < ncol * nseg * k; e += blockDim.x) {
+    const uint32_t c = e / (nseg * k), r = e - c * nseg * k;
+    lds[c * n + k + r] = lds[c * n + (r % k)];
+  }
+  __syncthreads();
+  lds_transform<false>(T, lds, Segs{n, k, nseg, k, k, k}, ncol);  // afft(k, shift) per shift
+  for (uint32_t e = threadIdx.x; e < (a.wanted_n > k ? a.wanted_n - k : 0) * ncol; e += blockDim.x) {
+    const uint32_t v = k + e / ncol, c = e % ncol;
+    const uint16_t s = lds[c * n + v];
+    uint8_t* q = out + static_cast<size_t>(v) * a.shard_len + 2 * static_cast<size_t>(ch0 + c);
+    q[0] = static_cast<uint8_t>(s >> 8);
+    q[1] = static_cast<uint8_t>(s);
+  }
+}
+
+// ----------------------------------------------------------- reconstruct ----
+// grid = (tiles of symbol columns, batch).  mod.rs:221-236 + inc_reconstruct.rs:1-85.
+// The forward FFT is pruned to the first k outputs: for index 0 the left
+// group of every level >= k has the zero skew (skews[2^m - 1] == sentinel), so
+// positions [0,k) only see afft(k, 0) -- bit-exact with decode_main.
+__global__ __launch_bounds__(kThreads) void k_reconstruct_generic(DevTables T, ReconstructArgs a, uint32_t nsyms,
+                                                                  uint32_t cols) {
+  extern __shared__ uint16_t lds[];
+  const size_t b = blockIdx.y;
+  const uint32_t s0 = blockIdx.x * cols;
+  const uint32_t ncol = min(cols, nsyms - s0);
+  const uint32_t n = a.n, k = a.k;
+  const uint8_t* sh = a.shards + b * a.batch_stride;
+  const uint8_t* pres = a.present + b * n;
+  const uint16_t* loc = a.locators + b * n;
+
+  for (uint32_t e = threadIdx.x; e < ncol * n; e += blockDim.x) {
+    const uint32_t v = e / ncol, c = e - v * ncol;
+    uint16_t w = 0;
+    if (pres[v]) {
+      const uint8_t* q = sh + static_cast<size_t>(v) * a.shard_len + 2 * static_cast<size_t>(s0 + c);
+      w = gf_mul_log(T, (uint32_t(q[0]) << 8) | q[1], loc[v]);
+    }
+    lds[c * n + v] = w;
+  }
+  __syncthreads();
+  lds_transform<true>(T, lds, Segs{n, 0, 1, n, 0, 0}, ncol);
+  lds_formal_derivative(lds, n, n, k, ncol);
+  lds_transform<false>(T, lds, Segs{n, 0, 1, k, 0, 0}, ncol);
+  uint8_t* out = a.out + b * a.out_stride;
+  for (uint32_t e = threadIdx.x; e < ncol * k; e += blockDim.x) {
+    const uint32_t c = e / k, j = e - c * k;
+    uint32_t w;
+    if (pres[j]) {
+      const uint8_t* q = sh + static_cast<size_t>(j) * a.shard_len + 2 * static_cast<size_t>(s0 + c);
+      w = (uint32_t(q[0]) << 8) | q[1];
+    } else {
+      w = gf_mul_log(T, lds[c * n + j], loc[j]);
+    }
+    uint8_t* o = out + static_cast<size_t>(s0 + c) * 2 * k + 2 * j;
+    o[0] = static_cast<uint8_t>(w >> 8);
+    o[1] = static_cast<uint8_t>(w);
+  }
+}
+
+// ------------------------------------------------------------- locator ----
+// inc_reconstruct.rs:90-113 over the full field (mod.rs:217-218), one
+// workgroup per erasure pattern, 128 KiB of LDS.
+__device__ void lds_walsh(uint16_t* v, uint32_t size) {
+  for (uint32_t h = 1; h < size; h <<= 1) {
+    for (uint32_t b = threadIdx.x; b < size / 2; b += blockDim.x) {
+      const uint32_t g = b / h, off = b - g * h;
+      const uint32_t i = g * 2 * h + off;
+      const uint32_t x = v[i], y = v[i + h];
+      const uint32_t s = x + y, t = x + kQ - y;
+      v[i] = static_cast<uint16_t>((s & 0xffffu) + (s >> 16));
+      v[i + h] = static_cast<uint16_t>((t & 0xffffu) + (t >> 16));
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_error_locator(DevTables T, uint32_t n, const uint8_t* present,
+                                                        uint16_t* locators) {
+  extern __shared__ uint16_t lw[];
+  const size_t b = blockIdx.x;
+  const uint8_t* pres = present + b * n;
+  for (uint32_t i = threadIdx.x; i < 65536u; i += blockDim.x) lw[i] = (i < n && !pres[i]) ? 1 : 0;
+  __syncthreads();
+  lds_walsh(lw, 65536u);
+  for (uint32_t i = threadIdx.x; i < 65536u; i += blockDim.x)
+    lw[i] = static_cast<uint16_t>((static_cast<uint32_t>(lw[i]) * T.log_walsh[i]) % kQ);
+  __syncthreads();
+  lds_walsh(lw, 65536u);
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+    locators[b * n + i] = pres[i] ? lw[i] : static_cast<uint16_t>(kQ - lw[i]);
+}
+
+// ------------------------------------------------------------ parity hooks ----
+template <bool INVERSE>
+__global__ __launch_bounds__(kThreads) void k_afft_cols(DevTables T, uint16_t* data, uint32_t size,
+                                                        uint32_t index, size_t cols_total, uint32_t cols) {
+  extern __shared__ uint16_t lds[];
+  const size_t c0 = static_cast<size_t>(blockIdx.x) * cols;
+  const uint32_t ncol = static_cast<uint32_t>(min(static_cast<size_t>(cols), cols_total - c0));
+  uint16_t* g = data + c0 * size;
+  for (uint32_t e = threadIdx.x; e < ncol * size; e += blockDim.x) lds[e] = g[e];
+  __syncthreads();
+  lds_transform<INVERSE>(T, lds, Segs{size, 0, 1, size, index, 0}, ncol);
+  for (uint32_t e = threadIdx.x; e < ncol * size; e += blockDim.x) g[e] = lds[e];
+}
+
+__global__ __launch_bounds__(1024) void k_walsh(uint16_t* data, uint32_t size) {
+  extern __shared__ uint16_t lds[];
+  for (uint32_t e = threadIdx.x; e < size; e += blockDim.x) lds[e] = data[e];
+  __syncthreads();
+  lds_walsh(lds, size);
+  for (uint32_t e = threadIdx.x; e < size; e += blockDim.x) data[e] = lds[e];
+}
+
+__global__ void k_mul(DevTables T, const uint16_t* a, const uint16_t* m, uint16_t* out, size_t count) {
+  const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < count) out[i] = gf_mul_log(T, a[i], m[i]);
+}
+
+__global__ __launch_bounds__(kThreads) void k_encode_low(DevTables T, const uint16_t* data, uint32_t k,
+                                                         uint16_t* codeword, uint32_t n, size_t cols_total,
+                                                         uint32_t cols) {
+  extern __shared__ uint16_t lds[];
+  const size_t c0 = static_cast<size_t>(blockIdx.x) * cols;
+  const uint32_t ncol = static_cast<uint32_t>(min(static_cast<size_t>(cols), cols_total - c0));
+  for (uint32_t e = threadIdx.x; e < ncol * k; e += blockDim.x) {
+    const uint32_t c = e / k, i = e - c * k;
+    lds[c * n + i] = data[(c0 + c) * k + i];
+  }
+  __syncthreads();
+  lds_transform<true>(T, lds, Segs{n, 0, 1, k, 0, 0}, ncol);
+  const uint32_t nseg = n / k - 1;
+  for (uint32_t e = threadIdx.x; e < ncol * nseg * k; e += blockDim.x) {
+    const uint32_t c = e / (nseg * k), r = e - c * nseg * k;
+    lds[c * n + k + r] = lds[c * n + (r % k)];
+  }
+  __syncthreads();
+  lds_transform<false>(T, lds, Segs{n, k, nseg, k, k, k}, ncol);
+  for (uint32_t e = threadIdx.x; e < ncol * n; e += blockDim.x) {
+    const uint32_t c = e / n, i = e - c * n;
+    codeword[(c0 + c) * n + i] = i < k ? data[(c0 + c) * k + i] : lds[c * n + i];
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_decode_main(DevTables T, uint16_t* codeword, uint32_t upto,
+                                                          const uint8_t* present, const uint16_t* loc,
+                                                          uint32_t n, size_t cols_total, uint32_t cols) {
+  extern __shared__ uint16_t lds[];
+  const size_t c0 = static_cast<size_t>(blockIdx.x) * cols;
+  const uint32_t ncol = static_cast<uint32_t>(min(static_cast<size_t>(cols), cols_total - c0));
+  uint16_t* g = codeword + c0 * n;
+  for (uint32_t e = threadIdx.x; e < ncol * n; e += blockDim.x) {
+    const uint32_t i = e % n;
+    lds[e] = present[i] ? gf_mul_log(T, g[e], loc[i]) : 0;
+  }
+  __syncthreads();
+  lds_transform<true>(T, lds, Segs{n, 0, 1, n, 0, 0}, ncol);
+  lds_formal_derivative(lds, n, n, n, ncol);
+  lds_transform<false>(T, lds, Segs{n, 0, 1, n, 0, 0}, ncol);
+  for (uint32_t e = threadIdx.x; e < ncol * n; e += blockDim.x) {
+    const uint32_t i = e % n;
+    uint16_t w = lds[e];
+    if (i < upto) w = present[i] ? 0 : gf_mul_log(T, w, loc[i]);
+    g[e] = w;
+  }
+}
+
+inline uint32_t grid_x(size_t total, uint32_t per) { return static_cast<uint32_t>((total + per - 1) / per); }
+
+}  // namespace
+
+hipError_t configure_generic_kernels() {
+  const int lim = 160 * 1024;
+  hipError_t e = hipSuccess;
+  auto set = [&](const void* f) {
+    hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    if (r != hipSuccess && e == hipSuccess) e = r;
+  };
+  set(reinterpret_cast<const void*>(&k_encode_generic));
+  set(reinterpret_cast<const void*>(&k_reconstruct_generic));
+  set(reinterpret_cast<const void*>(&k_error_locator));
+  set(reinterpret_cast<const void*>(&k_afft_cols<true>));
+  set(reinterpret_cast<const void*>(&k_afft_cols<false>));
+  set(reinterpret_cast<const void*>(&k_walsh));
+  set(reinterpret_cast<const void*>(&k_encode_low));
+  set(reinterpret_cast<const void*>(&k_decode_main));
+  return e;
+}
+
+hipError_t launch_encode_generic(const DevTables& T, const EncodeArgs& a, hipStream_t s) {
+  const size_t nchunks = (a.payload_len + 2 * a.k - 1) / (2 * a.k);
+  if (nchunks == 0 || a.batch == 0) return hipSuccess;
+  const uint32_t cols = cols_for(a.n);
+  dim3 grid(grid_x(nchunks, cols), static_cast<uint32_t>(a.batch));
+  k_encode_generic<<<grid, kThreads, cols * a.n * sizeof(uint16_t), s>>>(T, a, static_cast<uint32_t>(nchunks),
+                                                                          cols);
+  return hipGetLastError();
+}
+
+hipError_t launch_reconstruct_generic(const DevTables& T, const ReconstructArgs& a, hipStream_t s) {
+  const size_t nsyms = a.shard_len / 2;
+  if (nsyms == 0 || a.batch == 0) return hipSuccess;
+  const uint32_t cols = cols_for(a.n);
+  dim3 grid(grid_x(nsyms, cols), static_cast<uint32_t>(a.batch));
+  k_reconstruct_generic<<<grid, kThreads, cols * a.n * sizeof(uint16_t), s>>>(T, a, static_cast<uint32_t>(nsyms),
+                                                                               cols);
+  return hipGetLastError();
+}
+
+hipError_t launch_error_locator(const DevTables& T, uint32_t n, const uint8_t* present, size_t batch,
+                                uint16_t* locators, hipStream_t s) {
+  if (batch == 0) return hipSuccess;
+  k_error_locator<<<static_cast<uint32_t>(batch), 1024, 65536 * sizeof(uint16_t), s>>>(T, n, present, locators);
+  return hipGetLastError();
+}
+
+hipError_t launch_afft(const DevTables& T, uint16_t* data, uint32_t size, uint32_t index, size_t cols,
+                       bool inverse, hipStream_t s) {
+  if (cols == 0 || size < 2) return hipSuccess;
+  const uint32_t per = cols_for(size);
+  const size_t lds = per * size * sizeof(uint16_t);
+  if (inverse)
+    k_afft_cols<true><<<grid_x(cols, per), kThreads, lds, s>>>(T, data, size, index, cols, per);
+  else
+    k_afft_cols<false><<<grid_x(cols, per), kThreads, lds, s>>>(T, data, size, index, cols, per);
+  return hipGetLastError();
+}
+
+hipError_t launch_walsh(uint16_t* data, uint32_t size, hipStream_t s) {
+  if (size < 2) return hipSuccess;
+  k_walsh<<<1, 1024, size * sizeof(uint16_t), s>>>(data, size);
+  return hipGetLastError();
+}
+
+hipError_t launch_mul(const DevTables& T, const uint16_t* a, const uint16_t* m, uint16_t* out, size_t count,
+                      hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  k_mul<<<grid_x(count, 256), 256, 0, s>>>(T, a, m, out, count);
+  return hipGetLastError();
+}
+
+hipError_t launch_encode_low(const DevTables& T, const uint16_t* data, uint32_t k, uint16_t* codeword, uint32_t n,
+                             size_t cols, hipStream_t s) {
+  if (cols == 0) return hipSuccess;
+  const uint32_t per = cols_for(n);
+  k_encode_low<<<grid_x(cols, per), kThreads, per * n * sizeof(uint16_t), s>>>(T, data, k, codeword, n, cols,
+                                                                                per);
+  return hipGetLastError();
+}
+
+hipError_t launch_decode_main(const DevTables& T, uint16_t* codeword, uint32_t upto, const uint8_t* present,
+                              const uint16_t* locator, uint32_t n, size_t cols, hipStream_t s) {
+  if (cols == 0) return hipSuccess;
+  const uint32_t per = cols_for(n);
+  k_decode_main<<<grid_x(cols, per), kThreads, per * n * sizeof(uint16_t), s>>>(T, codeword, upto, present,
+                                                                                 locator, n, cols, per);
+  return hipGetLastError();
+}
+
+}  // namespace np

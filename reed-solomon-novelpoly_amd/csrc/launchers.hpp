@@ -1,0 +1,62 @@
+// Internal launch API between the host engine (engine.cpp) and the kernels.
+// All functions enqueue on `s` and return hipSuccess or the launch error.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "dev_tables.hpp"
+
+namespace np {
+
+struct EncodeArgs {
+  const uint8_t* payloads;
+  size_t payload_len, payload_stride, batch;
+  uint32_t n, k, wanted_n;
+  size_t shard_len;  // bytes per shard = 2 * chunks
+  uint8_t* shards;
+  size_t batch_stride;
+};
+
+struct ReconstructArgs {
+  const uint8_t* shards;
+  size_t shard_len, batch_stride;
+  const uint8_t* present;    // device, batch x n
+  const uint16_t* locators;  // device, batch x n (log form)
+  size_t batch;
+  uint32_t n, k;
+  uint8_t* out;
+  size_t out_stride;
+};
+
+// ---- generic path: any power-of-two n <= 65536, k <= n/2 (kernels_generic.hip) ----
+hipError_t launch_encode_generic(const DevTables& T, const EncodeArgs& a, hipStream_t s);
+hipError_t launch_reconstruct_generic(const DevTables& T, const ReconstructArgs& a, hipStream_t s);
+hipError_t launch_error_locator(const DevTables& T, uint32_t n, const uint8_t* present, size_t batch,
+                                uint16_t* locators, hipStream_t s);
+// parity hooks
+hipError_t launch_afft(const DevTables& T, uint16_t* data, uint32_t size, uint32_t index, size_t cols,
+                       bool inverse, hipStream_t s);
+hipError_t launch_walsh(uint16_t* data, uint32_t size, hipStream_t s);
+hipError_t launch_mul(const DevTables& T, const uint16_t* a, const uint16_t* m, uint16_t* out, size_t count,
+                      hipStream_t s);
+hipError_t launch_encode_low(const DevTables& T, const uint16_t* data, uint32_t k, uint16_t* codeword,
+                             uint32_t n, size_t cols, hipStream_t s);
+hipError_t launch_decode_main(const DevTables& T, uint16_t* codeword, uint32_t upto, const uint8_t* present,
+                              const uint16_t* locator, uint32_t n, size_t cols, hipStream_t s);
+
+// ---- fast path (kernels_fast.hip) ----
+// Returns true if a specialised kernel serves (n, k).
+bool fast_encode_supported(uint32_t n, uint32_t k);
+bool fast_reconstruct_supported(uint32_t n, uint32_t k);
+hipError_t launch_encode_fast(const DevTables& T, const EncodeArgs& a, hipStream_t s);
+hipError_t launch_reconstruct_fast(const DevTables& T, const ReconstructArgs& a, hipStream_t s);
+
+}  // namespace np
+
+namespace np {
+// Raises the dynamic-LDS limit of the kernels that need > 64 KiB (call once per device).
+hipError_t configure_generic_kernels();
+hipError_t configure_fast_kernels();
+}  // namespace np

@@ -1,0 +1,62 @@
+"""Shared fixtures.  `-m "not gpu"` runs on CPU; `-m gpu` needs an MI355X."""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+for p in (os.path.join(ROOT, "oracle"), os.path.join(ROOT, "reed-solomon-novelpoly_amd", "python"), ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import np_oracle
+
+    return np_oracle.Oracle()
+
+
+@pytest.fixture(scope="session")
+def refc():
+    import np_oracle
+
+    if not np_oracle.ref_available():
+        pytest.skip("oracle/_ref/librsec_ref.so not built (reference tree absent)")
+    return np_oracle.RefC()
+
+
+@pytest.fixture(scope="session")
+def golden_vectors():
+    import numpy as np
+
+    return np.load(os.path.join(GOLDEN, "vectors.npz"), allow_pickle=False)
+
+
+@pytest.fixture(scope="session")
+def golden_json():
+    import json
+
+    def load(name):
+        with open(os.path.join(GOLDEN, name)) as f:
+            return json.load(f)
+
+    return load
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    """A device context on cuda:0 through the product library (fails loudly)."""
+    import novelpoly_amd as npa
+    import torch
+
+    assert torch.cuda.is_available(), "GPU test run without a visible GPU"
+    torch.cuda.init()
+    ctx = npa.default_context(0)
+    return ctx

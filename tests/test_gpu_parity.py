@@ -1,0 +1,259 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle and
+the golden fixtures generated from the reference's own C build.  Bit-exact
+everywhere (integer arithmetic)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import novelpoly_amd as npa
+from novelpoly_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(a):
+    import torch
+
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def host(t):
+    import torch
+
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def stream():
+    import torch
+
+    return torch.cuda.current_stream().cuda_stream
+
+
+def u16(t):
+    """uint16 numpy <-> torch: torch has no uint16 arithmetic, carry as int16 bits."""
+    return t
+
+
+def to_dev_u16(a):
+    return dev(np.ascontiguousarray(a, dtype=np.uint16).view(np.int16))
+
+
+def from_dev_u16(t):
+    return host(t).view(np.uint16)
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+# ------------------------------------------------------------- primitives ----
+def test_mul_dev_golden(gpu, golden_vectors):
+    import torch
+
+    g = golden_vectors
+    a, m = to_dev_u16(g["mul_a"]), to_dev_u16(g["mul_m"])
+    out = torch.empty_like(a)
+    npa.mul_dev(a.data_ptr(), m.data_ptr(), out.data_ptr(), a.numel(), ctx=gpu, stream=stream())
+    assert np.array_equal(from_dev_u16(out), g["mul_out"])
+
+
+def test_afft_dev_golden(gpu, golden_vectors):
+    g = golden_vectors
+    for size, index in g["transform_cases"]:
+        key = f"s{size}_i{index}"
+        for inverse, suffix in ((False, "_afft"), (True, "_ifft")):
+            t = to_dev_u16(g[key + "_in"])
+            npa.afft_dev(t.data_ptr(), int(size), int(index), 1, inverse=inverse, ctx=gpu, stream=stream())
+            assert np.array_equal(from_dev_u16(t), g[key + suffix]), key + suffix
+
+
+def test_afft_dev_many_columns(gpu, oracle):
+    rng = np.random.default_rng(5)
+    for size, index, cols in ((64, 128, 37), (256, 0, 70), (1024, 3072, 9)):
+        x = rng.integers(0, 65536, (cols, size), dtype=np.uint16)
+        t = to_dev_u16(x)
+        npa.afft_dev(t.data_ptr(), size, index, cols, inverse=False, ctx=gpu, stream=stream())
+        got = from_dev_u16(t)
+        for c in range(cols):
+            assert np.array_equal(got[c], oracle.afft(x[c], size, index))
+
+
+def test_walsh_dev_golden(gpu, golden_vectors):
+    g = golden_vectors
+    for size in (2, 16, 256, 4096):
+        t = to_dev_u16(g[f"walsh{size}_in"])
+        npa.walsh_dev(t.data_ptr(), size, ctx=gpu, stream=stream())
+        assert np.array_equal(from_dev_u16(t), g[f"walsh{size}_out"])
+
+
+def test_encode_low_and_decode_main_dev_golden(gpu, golden_vectors, oracle):
+    import torch
+
+    g = golden_vectors
+    for n, k in g["codec_cases"]:
+        n, k = int(n), int(k)
+        key = f"n{n}_k{k}"
+        d = to_dev_u16(g[key + "_data"])
+        cw = torch.zeros(n, dtype=torch.int16, device="cuda")
+        npa.encode_low_dev(d.data_ptr(), k, cw.data_ptr(), n, 1, ctx=gpu, stream=stream())
+        assert np.array_equal(from_dev_u16(cw), g[key + "_codeword"]), key
+        pres = dev(g[key + "_present"])
+        loc = torch.zeros(n, dtype=torch.int16, device="cuda")
+        npa.error_locator_dev(n, pres.data_ptr(), 1, loc.data_ptr(), ctx=gpu, stream=stream())
+        assert np.array_equal(from_dev_u16(loc), g[key + "_locator"]), key
+        c = g[key + "_codeword"].copy()
+        c[g[key + "_present"] == 0] = 0
+        ct = to_dev_u16(c)
+        npa.decode_main_dev(ct.data_ptr(), k, pres.data_ptr(), loc.data_ptr(), n, 1, ctx=gpu, stream=stream())
+        assert np.array_equal(from_dev_u16(ct), g[key + "_decoded"]), key
+
+
+# ---------------------------------------------------------- crate surface ----
+def test_api_cases_golden(gpu, golden_json):
+    for case in golden_json("api_cases.json"):
+        nw = case["n_wanted"]
+        pl = bytes.fromhex(case["payload"])
+        shards = npa.encode(pl, nw, ctx=gpu)
+        assert [s.hex() for s in shards] == case["shards"], nw
+        keep = set(case["kept"])
+        recv = [shards[i] if i in keep else None for i in range(nw)]
+        rec = npa.reconstruct(recv, nw, ctx=gpu)
+        assert rec.hex() == case["reconstructed"], nw
+        assert rec[: len(pl)] == pl
+
+
+@pytest.mark.parametrize("nw,plen", [(2, 1), (3, 10), (4, 100), (10, 16), (100, 1), (123, 1337), (2003, 17),
+                                     (2003, 0), (4, 2), (770, 5120), (1000, 100_000), (65535, 40_000),
+                                     (300, 77_777), (33, 3)])
+def test_roundtrip_vs_oracle(gpu, oracle, nw, plen):
+    # simplicissimus! cases (tests.rs:291-307) and larger shapes
+    pl = synth.payload(nw * 7 + plen, plen)
+    if plen == 0:
+        with pytest.raises(npa.PayloadSizeIsZero):
+            npa.encode(pl, nw, ctx=gpu)
+        return
+    p = npa.CodeParams.derive_parameters(nw, npa.recoverablity_subset_size(nw))
+    shards = npa.encode(pl, nw, ctx=gpu)
+    st, want = oracle.encode(pl, p.n(), p.k(), nw)
+    assert st == 0 and shards == want
+    # drop the first half of the redundancy and (if possible) some data shards
+    rng = np.random.default_rng(nw + plen)
+    ndrop = max(0, min(nw, p.n()) - p.k())
+    drop = set(rng.choice(nw, size=min(ndrop, nw - 1 if nw > 1 else 0), replace=False).tolist())
+    recv = [None if i in drop else shards[i] for i in range(nw)]
+    if sum(s is not None for s in recv) < p.k():
+        with pytest.raises(npa.NeedMoreShards):
+            npa.reconstruct(recv, nw, ctx=gpu)
+        return
+    rec = npa.reconstruct(recv, nw, ctx=gpu)
+    st, want_rec = oracle.reconstruct(recv, p.n(), p.k())
+    assert st == 0 and rec == want_rec
+    assert rec[:plen] == pl
+
+
+def test_reconstruct_inconsistent_input_matches_oracle(gpu, oracle):
+    # arbitrary (non-codeword) shards: the decoder must compute the same linear map
+    nw = 300
+    p = npa.CodeParams.derive_parameters(nw, npa.recoverablity_subset_size(nw))
+    rng = np.random.default_rng(11)
+    shards = [rng.integers(0, 256, 64, dtype=np.uint8).tobytes() for _ in range(nw)]
+    recv = [s if rng.random() < 0.7 else None for s in shards]
+    st, want = oracle.reconstruct(recv, p.n(), p.k())
+    assert st == 0 and npa.reconstruct(recv, nw, ctx=gpu) == want
+
+
+def test_errors(gpu):
+    shards = npa.encode(bytes(range(100)), 16, ctx=gpu)
+    with pytest.raises(npa.NeedMoreShards) as e:
+        npa.reconstruct([shards[0]] + [None] * 15, 16, ctx=gpu)
+    assert e.value.fields == (1, 4, 16)
+    with pytest.raises(npa.EmptyShard):
+        npa.reconstruct([b""] * 8 + [None] * 8, 16, ctx=gpu)
+    with pytest.raises(npa.InconsistentShardLengths):
+        npa.reconstruct([shards[0], shards[1], shards[2][:-2], shards[3]] + [None] * 12, 16, ctx=gpu)
+    rs = npa.CodeParams.derive_parameters(16, npa.recoverablity_subset_size(16)).make_encoder(gpu)
+    with pytest.raises(npa.NeedMoreShards):
+        rs.reconstruct_from_systematic(shards[:1])
+    with pytest.raises(npa.PayloadSizeIsZero):
+        rs.encode(b"")
+
+
+def test_reconstruct_from_systematic(gpu):
+    # tests.rs:482-497 round_trip_systematic_quickcheck (a few fixed draws)
+    for nw, plen in ((2, 5), (100, 1234), (1000, 70_001)):
+        rs = npa.CodeParams.derive_parameters(nw, (nw - 1) // 3 + 1).make_encoder(gpu)
+        pl = synth.payload(plen, plen)
+        chunks = rs.encode(pl)
+        assert rs.reconstruct_from_systematic(chunks[: rs.k])[:plen] == pl
+
+
+def test_round_trip_first_wanted_k(gpu):
+    # tests.rs:499-512 round_trip_quickcheck: reconstruct from the first wanted_k shards
+    rng = np.random.default_rng(499)
+    for _ in range(12):
+        nw = int(rng.integers(2, 65536))
+        plen = int(rng.integers(2, 200_000))
+        wk = (nw - 1) // 3 + 1
+        rs = npa.CodeParams.derive_parameters(nw, wk).make_encoder(gpu)
+        pl = synth.payload(nw, plen)
+        chunks = rs.encode(pl)
+        res = rs.reconstruct([c for c in chunks[:wk]])
+        assert res[:plen] == pl, (nw, plen)
+
+
+# ------------------------------------------------- BASELINE-size digests ----
+@pytest.mark.parametrize("cid", [1, 2, 3, 4])
+def test_config_digests_device_batch(gpu, golden_json, cid):
+    import torch
+
+    d = golden_json("digests.json")[f"cfg{cid}"]
+    p = npa.CodeParams.derive_parameters(d["n_wanted"], d["k_wanted"])
+    n, k, nw = p.n(), p.k(), p.wanted_n
+    plen = d["payload_len"]
+    pl = np.frombuffer(synth.payload(0, plen), dtype=np.uint8)
+    sl = d["shard_len"]
+    dp = dev(pl)
+    ds = torch.empty(nw * sl, dtype=torch.uint8, device="cuda")
+    npa.encode_batch_dev(p, dp.data_ptr(), plen, plen, 1, ds.data_ptr(), nw * sl, ctx=gpu, stream=stream())
+    shards = host(ds).tobytes()
+    assert sha(shards) == d["encode_sha256"]
+    pres = synth.present_mask(0, n, d["erase"])
+    out = torch.empty((sl // 2) * 2 * k, dtype=torch.uint8, device="cuda")
+    npa.reconstruct_batch_dev(p, ds.data_ptr(), sl, n * sl, pres.tobytes(), 1, out.data_ptr(), out.numel(),
+                              ctx=gpu, stream=stream())
+    assert sha(host(out).tobytes()) == d["reconstruct_sha256"]
+
+
+@pytest.mark.parametrize("cid", [2, 3, 4])
+def test_full_size_batch_properties(gpu, oracle, cid):
+    """At BASELINE shapes, with a batch: per-payload digests against the oracle
+    on a sample, and encode->erase->reconstruct round trip on every payload."""
+    import torch
+
+    cfg = synth.CONFIGS[cid]
+    p = npa.CodeParams.derive_parameters(cfg["n_wanted"], cfg["k_wanted"])
+    n, k = p.n(), p.k()
+    batch = {2: 64, 3: 16, 4: 4}[cid]
+    plen = cfg["payload"]
+    pls = np.stack([np.frombuffer(synth.payload(100 + b, plen), dtype=np.uint8) for b in range(batch)])
+    sl = p.make_encoder(gpu).shard_len(plen)
+    dp = dev(pls)
+    ds = torch.empty((batch, n, sl), dtype=torch.uint8, device="cuda")
+    npa.encode_batch_dev(p, dp.data_ptr(), plen, plen, batch, ds.data_ptr(), n * sl, ctx=gpu, stream=stream())
+    hs = host(ds)
+    for b in (0, batch - 1):
+        st, want = oracle.encode(pls[b].tobytes(), n, k, n)
+        assert st == 0 and hs[b].tobytes() == b"".join(want), b
+    erase = cfg["erase"] if cfg["erase"] is not None else n - k
+    pres = np.stack([synth.present_mask(100 + b, n, erase) for b in range(batch)])
+    # poison erased rows: the kernel must never read them
+    ds2 = ds.clone()
+    ds2[torch.from_numpy(pres == 0).cuda()] = 0xA5
+    out = torch.empty((batch, (sl // 2) * 2 * k), dtype=torch.uint8, device="cuda")
+    npa.reconstruct_batch_dev(p, ds2.data_ptr(), sl, n * sl, pres.tobytes(), batch, out.data_ptr(),
+                              out.shape[1], ctx=gpu, stream=stream())
+    ho = host(out)
+    for b in range(batch):
+        assert ho[b, :plen].tobytes() == pls[b].tobytes(), b

@@ -1,0 +1,119 @@
+"""CPU tests of the product library's host side: it loads, exports every
+symbol include/novelpoly.h declares, and its parameter logic matches the
+reference's known answers (no GPU compute here)."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+import novelpoly_amd as npa
+from novelpoly_amd import synth
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+
+
+def declared_functions():
+    src = open(os.path.join(ROOT, "include", "novelpoly.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(np_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = npa.lib()
+    names = declared_functions()
+    assert len(names) >= 28
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_status_messages():
+    L = npa.lib()
+    for st in range(0, 9):
+        assert L.np_status_message(st)
+    assert "gfx950" in npa.version()
+
+
+def test_recoverability_subset_size():
+    # util.rs:44-59 three_f_plus_1
+    kat = {0: 1, 1: 1, 2: 1, 3: 1, 4: 2, 5: 2, 6: 2, 8: 3, 11: 4, 173: 58, 174: 58, 175: 59}
+    for n, want in kat.items():
+        assert npa.recoverablity_subset_size(n) == want
+
+
+def test_code_params_kat():
+    # tests.rs:421-446 test_code_params
+    with pytest.raises(npa.Error):
+        npa.CodeParams.derive_parameters(0, npa.recoverablity_subset_size(0))
+    with pytest.raises(npa.WantedShardCountTooLow):
+        npa.CodeParams.derive_parameters(1, npa.recoverablity_subset_size(1))
+    for nw, n, k in ((2, 2, 1), (3, 4, 1), (4, 4, 2), (100, 128, 32)):
+        p = npa.CodeParams.derive_parameters(nw, npa.recoverablity_subset_size(nw))
+        assert (p.n(), p.k(), p.wanted_n) == (n, k, nw)
+    with pytest.raises(npa.WantedPayloadShardCountTooLow):
+        npa.CodeParams.derive_parameters(10, 0)
+    with pytest.raises(npa.WantedShardCountTooHigh) as ei:
+        npa.CodeParams.derive_parameters(65537, 3)
+    assert ei.value.fields == (65537,)
+    assert npa.CodeParams.derive_parameters(65536, 21846).n() == 65536
+
+
+def test_k_n_construction():
+    # tests.rs:50-64
+    for vc in range(3, 8201):
+        p = npa.CodeParams.derive_parameters(vc, npa.recoverablity_subset_size(vc))
+        assert p.wanted_n == vc and vc <= p.n()
+        assert vc // 3 >= p.k() - 1 and vc >= (p.k() - 1) * 3
+
+
+def test_shard_len_kat():
+    # tests.rs:448-466 shard_len_is_reasonable (n16 k4 wanted 5)
+    p = npa._Params(16, 4, 5)
+    L = npa.lib()
+    for size, want in ((100, 26), (99, 26), (95, 24), (94, 24), (90, 24), (19, 6)):
+        assert L.np_shard_len(C.byref(p), size) == want
+
+
+def test_params_new_power_of_two_rule():
+    # mod.rs:109-115: only fails when neither n nor k is a power of two
+    p = npa._Params()
+    assert npa.lib().np_params_new(12, 3, 12, C.byref(p)) == 6
+    assert npa.lib().np_params_new(16, 3, 12, C.byref(p)) == 0
+
+
+def test_wrapped_shard_pads_odd():
+    # wrapped_shard.rs:33-39
+    assert npa.WrappedShard(b"abc").into_inner() == b"abc\x00"
+    assert npa.WrappedShard(b"ab").into_inner() == b"ab"
+
+
+def test_baseline_configs_effective_params():
+    # SURVEY F10
+    for cid, cfg in synth.CONFIGS.items():
+        p = npa.CodeParams.derive_parameters(cfg["n_wanted"], cfg["k_wanted"])
+        assert (p.n(), p.k()) == (cfg["n"], cfg["k"]), cid
+
+
+def test_synth_is_deterministic():
+    a = synth.payload(7, 1000)
+    assert a == synth.payload(7, 1000) and a != synth.payload(8, 1000)
+    e = synth.erasure_indices(3, 1024, 342)
+    assert len(set(e.tolist())) == 342 and e.max() < 1024
+    assert np.array_equal(e, synth.erasure_indices(3, 1024, 342))
+
+
+def test_fast_path_table():
+    # the specialised kernels serve the BASELINE shapes; generic covers the rest
+    for cfg in synth.CONFIGS.values():
+        p = npa.CodeParams.derive_parameters(cfg["n_wanted"], cfg["k_wanted"])
+        assert isinstance(p.is_faster8(), bool)
+
+
+def test_ctx_without_gpu_reports_no_device():
+    import torch
+
+    if torch.cuda.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(npa.DeviceError):
+        npa.Context(0)
