@@ -96,6 +96,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # a dedicated stream: kernels, events and torch copies share one queue
+    torch.cuda.set_stream(torch.cuda.Stream(dev))
 
     cfg = dict(synth.CONFIGS[args.config])
     cfg["id"] = args.config

@@ -12,6 +12,18 @@ from novelpoly_amd import synth
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _own_stream():
+    """Run every test on a non-default torch stream and hand that stream to
+    the library, so torch copies and our kernels are ordered on one queue."""
+    import torch
+
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        yield
+    torch.cuda.synchronize()
+
+
 def dev(a):
     import torch
 
@@ -29,11 +41,6 @@ def stream():
     import torch
 
     return torch.cuda.current_stream().cuda_stream
-
-
-def u16(t):
-    """uint16 numpy <-> torch: torch has no uint16 arithmetic, carry as int16 bits."""
-    return t
 
 
 def to_dev_u16(a):
