@@ -37,67 +37,55 @@ __device__ __forceinline__ uint32_t vperm(uint32_t s0, uint32_t s1, uint32_t sel
   return __builtin_amdgcn_perm(s0, s1, sel);
 }
 
+// Byte-table selectors of four byte-planar symbols: bits 0-2, 3-5, 6-7 of
+// every byte of the low plane (s[0..2]) and of the high plane (s[3..5]).
+// Written as one asm block so that the compiler cannot hoist the selector
+// extraction of a whole transform level ahead of its use (that hoisting cost
+// 6 live VGPRs per pending butterfly and blew the register budget).
+__device__ __forceinline__ void selectors(uint32_t yl, uint32_t yh, uint32_t (&s)[6]) {
+  asm volatile(
+      "v_and_b32 %0, 0x07070707, %6\n\t"
+      "v_lshrrev_b32 %1, 3, %6\n\t"
+      "v_lshrrev_b32 %2, 6, %6\n\t"
+      "v_and_b32 %3, 0x07070707, %7\n\t"
+      "v_lshrrev_b32 %4, 3, %7\n\t"
+      "v_lshrrev_b32 %5, 6, %7\n\t"
+      "v_and_b32 %1, 0x07070707, %1\n\t"
+      "v_and_b32 %2, 0x03030303, %2\n\t"
+      "v_and_b32 %4, 0x07070707, %4\n\t"
+      "v_and_b32 %5, 0x03030303, %5"
+      : "=&v"(s[0]), "=&v"(s[1]), "=&v"(s[2]), "=&v"(s[3]), "=&v"(s[4]), "=&v"(s[5])
+      : "v"(yl), "v"(yh));
+}
+
 // x ^= c*y on four byte-planar symbols.  Pool layout: field_tables.cpp.
 __device__ __forceinline__ void qmul(uint32_t& xl, uint32_t& xh, uint32_t yl, uint32_t yh, const uint32_t (&p)[20]) {
-  asm volatile("" : "+v"(yl), "+v"(yh));  // keep selector extraction next to its use (register pressure)
-  const uint32_t a0 = yl & 0x07070707u, a1 = (yl >> 3) & 0x07070707u, a2 = (yl >> 6) & 0x03030303u;
-  const uint32_t b0 = yh & 0x07070707u, b1 = (yh >> 3) & 0x07070707u, b2 = (yh >> 6) & 0x03030303u;
-  uint32_t lo = xor3(vperm(p[1], p[0], a0), vperm(p[3], p[2], a1), vperm(p[4], p[4], a2));
-  lo = xor3(lo, vperm(p[6], p[5], b0), vperm(p[8], p[7], b1));
-  xl = xor3(xl, lo, vperm(p[9], p[9], b2));
-  uint32_t hi = xor3(vperm(p[11], p[10], a0), vperm(p[13], p[12], a1), vperm(p[14], p[14], a2));
-  hi = xor3(hi, vperm(p[16], p[15], b0), vperm(p[18], p[17], b1));
-  xh = xor3(xh, hi, vperm(p[19], p[19], b2));
+  uint32_t s[6];
+  selectors(yl, yh, s);
+  uint32_t lo = xor3(vperm(p[1], p[0], s[0]), vperm(p[3], p[2], s[1]), vperm(p[4], p[4], s[2]));
+  lo = xor3(lo, vperm(p[6], p[5], s[3]), vperm(p[8], p[7], s[4]));
+  xl = xor3(xl, lo, vperm(p[9], p[9], s[5]));
+  uint32_t hi = xor3(vperm(p[11], p[10], s[0]), vperm(p[13], p[12], s[1]), vperm(p[14], p[14], s[2]));
+  hi = xor3(hi, vperm(p[16], p[15], s[3]), vperm(p[18], p[17], s[4]));
+  xh = xor3(xh, hi, vperm(p[19], p[19], s[5]));
 }
 
-__device__ __forceinline__ void load_pool(const uint32_t* pools, int slot, uint32_t (&p)[20]) {
-  // Opaque offset: stops the compiler from hoisting every group's table load
-  // to the top of a transform (20 live VGPRs per hoisted group).
-  uint32_t off = static_cast<uint32_t>(slot) * kPoolWords;
-  asm volatile("" : "+v"(off));
-  const uint4* q = reinterpret_cast<const uint4*>(pools + off);
+typedef const __attribute__((address_space(4))) uint32_t* cpool_t;
+
+// Multiplier tables of the additive element c, read through the scalar cache
+// (wave-uniform address -> s_load).
+__device__ __forceinline__ void pool_of(const DevTables& T, uint32_t c, uint32_t (&p)[20]) {
+  const cpool_t q = (cpool_t)(T.perm_pools) + c * kPoolWords;
 #pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    const uint4 v = q[i];
-    p[4 * i] = v.x;
-    p[4 * i + 1] = v.y;
-    p[4 * i + 2] = v.z;
-    p[4 * i + 3] = v.w;
-  }
+  for (int i = 0; i < 20; ++i) p[i] = q[i];
 }
 
-// Global table of the multiplier with additive value c.
-__device__ __forceinline__ void global_pool(const DevTables& T, uint32_t c, uint32_t (&p)[20]) {
-  const uint4* q = reinterpret_cast<const uint4*>(T.perm_pools + static_cast<size_t>(c) * kPoolWords);
-#pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    const uint4 v = q[i];
-    p[4 * i] = v.x;
-    p[4 * i + 1] = v.y;
-    p[4 * i + 2] = v.z;
-    p[4 * i + 3] = v.w;
-  }
-}
-
-// Slot of (level b, group t) in a size-K transform's pool array: K - (K>>b) + t.
-template <int K>
-__device__ __forceinline__ constexpr int pslot(int b, int t) {
-  return K - (K >> b) + t;
-}
-
-// Stage the K-1 multiplier tables of a size-K transform at index I into LDS.
-template <int K>
-__device__ void stage_pools(const DevTables& T, uint32_t* pools, uint32_t index) {
-  for (int s = threadIdx.x; s < K - 1; s += blockDim.x) {
-    int b = 0;
-    while (s >= K - (K >> (b + 1))) ++b;
-    const int t = s - (K - (K >> b));
-    const uint32_t c = T.skew_add[((2u * t + 1u) << b) + index - 1u];
-    const uint4* src = reinterpret_cast<const uint4*>(T.perm_pools + static_cast<size_t>(c) * kPoolWords);
-    uint4* dst = reinterpret_cast<uint4*>(pools + s * kPoolWords);
-#pragma unroll
-    for (int i = 0; i < 5; ++i) dst[i] = src[i];
-  }
+// Additive skew of group t at level b of a transform at index I (a multiple
+// of the transform size): skews[(2t+1)2^b + I - 1] is the field element with
+// Cantor coordinates 2(t + I/2^(b+1)) = 2t + (I >> b)  (tests/test_oracle.py::
+// test_skews_are_cantor_points pins this on the reference tables).
+__device__ __forceinline__ uint32_t skew_c(int b, int t, uint32_t index) {
+  return 2u * static_cast<uint32_t>(t) + (index >> b);
 }
 
 // --------------------------------------------------------------- LDS tile ----
@@ -177,7 +165,7 @@ __device__ __forceinline__ void store_row4(uint8_t* rowp, uint2 v, uint32_t col0
 
 // ------------------------------------------------------ register transforms ----
 template <int K, bool INDEX0>
-__device__ __forceinline__ void ifft_reg(const uint32_t* pools, uint32_t (&L)[K / 4], uint32_t (&H)[K / 4]) {
+__device__ __forceinline__ void ifft_reg(const DevTables& T, uint32_t index, uint32_t (&L)[K / 4], uint32_t (&H)[K / 4]) {
 #pragma unroll
   for (int b = 2; (1 << b) < K; ++b) {
     const int D = 1 << (b - 2), G = K >> (b + 1);
@@ -192,16 +180,14 @@ __device__ __forceinline__ void ifft_reg(const uint32_t* pools, uint32_t (&L)[K 
         continue;
       }
       uint32_t p[20];
-      load_pool(pools, pslot<K>(b, t), p);
+      pool_of(T, skew_c(b, t, index), p);
 #pragma unroll
       for (int u = 0; u < D; ++u) {
         const int qx = t * 2 * D + u, qy = qx + D;
         L[qy] ^= L[qx];
         H[qy] ^= H[qx];
         qmul(L[qx], H[qx], L[qy], H[qy], p);
-        if ((u % 2) == 1) __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);  // keep one group's tables live at a time
     }
   }
 }
@@ -214,7 +200,7 @@ constexpr int log2k() {
 }
 
 template <int K, bool INDEX0>
-__device__ __forceinline__ void fft_reg(const uint32_t* pools, uint32_t (&L)[K / 4], uint32_t (&H)[K / 4]) {
+__device__ __forceinline__ void fft_reg(const DevTables& T, uint32_t index, uint32_t (&L)[K / 4], uint32_t (&H)[K / 4]) {
 #pragma unroll
   for (int lv = log2k<K>() - 1; lv >= 2; --lv) {  // top level first
     const int D = 1 << (lv - 2), G = K >> (lv + 1);
@@ -229,55 +215,54 @@ __device__ __forceinline__ void fft_reg(const uint32_t* pools, uint32_t (&L)[K /
         continue;
       }
       uint32_t p[20];
-      load_pool(pools, pslot<K>(lv, t), p);
+      pool_of(T, skew_c(lv, t, index), p);
 #pragma unroll
       for (int u = 0; u < D; ++u) {
         const int qx = t * 2 * D + u, qy = qx + D;
         qmul(L[qx], H[qx], L[qy], H[qy], p);
         L[qy] ^= L[qx];
         H[qy] ^= H[qx];
-        if ((u % 2) == 1) __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
     }
   }
 }
 
 // Chunk-quad levels 0 and 1 for block m (positions 4m..4m+3) of 4 rows.
 template <int K, bool INVERSE, bool INDEX0>
-__device__ __forceinline__ void cq_levels(const uint32_t* pools, uint32_t m, uint32_t (&cl)[4], uint32_t (&ch)[4]) {
+__device__ __forceinline__ void cq_levels(const DevTables& T, uint32_t index, uint32_t m, uint32_t (&cl)[4],
+                                          uint32_t (&ch)[4]) {
   const bool skip = INDEX0 && m == 0;  // group t == 0 at index 0 has the zero skew
   uint32_t p[20];
   if (INVERSE) {
     cl[1] ^= cl[0]; ch[1] ^= ch[0];
     cl[3] ^= cl[2]; ch[3] ^= ch[2];
     if (!skip) {
-      load_pool(pools, pslot<K>(0, 2 * m), p);
+      pool_of(T, skew_c(0, 2 * m, index), p);
       qmul(cl[0], ch[0], cl[1], ch[1], p);
     }
-    load_pool(pools, pslot<K>(0, 2 * m + 1), p);
+    pool_of(T, skew_c(0, 2 * m + 1, index), p);
     qmul(cl[2], ch[2], cl[3], ch[3], p);
     cl[2] ^= cl[0]; ch[2] ^= ch[0];
     cl[3] ^= cl[1]; ch[3] ^= ch[1];
     if (!skip) {
-      load_pool(pools, pslot<K>(1, m), p);
+      pool_of(T, skew_c(1, m, index), p);
       qmul(cl[0], ch[0], cl[2], ch[2], p);
       qmul(cl[1], ch[1], cl[3], ch[3], p);
     }
   } else {
     if (!skip) {
-      load_pool(pools, pslot<K>(1, m), p);
+      pool_of(T, skew_c(1, m, index), p);
       qmul(cl[0], ch[0], cl[2], ch[2], p);
       qmul(cl[1], ch[1], cl[3], ch[3], p);
     }
     cl[2] ^= cl[0]; ch[2] ^= ch[0];
     cl[3] ^= cl[1]; ch[3] ^= ch[1];
     if (!skip) {
-      load_pool(pools, pslot<K>(0, 2 * m), p);
+      pool_of(T, skew_c(0, 2 * m, index), p);
       qmul(cl[0], ch[0], cl[1], ch[1], p);
     }
     cl[1] ^= cl[0]; ch[1] ^= ch[0];
-    load_pool(pools, pslot<K>(0, 2 * m + 1), p);
+    pool_of(T, skew_c(0, 2 * m + 1, index), p);
     qmul(cl[2], ch[2], cl[3], ch[3], p);
     cl[3] ^= cl[2]; ch[3] ^= ch[2];
   }
@@ -307,7 +292,6 @@ __global__ __launch_bounds__(256, 1) void k_encode_fast(DevTables T, EncodeArgs 
                                                         uint32_t tiles) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
-  uint32_t* pools = reinterpret_cast<uint32_t*>(smem + kTile * 2 * K);
   const uint32_t pb = blockIdx.x / tiles, tl = blockIdx.x - pb * tiles;
   const uint32_t ch0 = tl * kTile;
   const uint32_t ncols = min(static_cast<uint32_t>(kTile), nchunks - ch0);
@@ -316,7 +300,6 @@ __global__ __launch_bounds__(256, 1) void k_encode_fast(DevTables T, EncodeArgs 
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const bool al8 = (a.shard_len & 7u) == 0;
 
-  stage_pools<K>(T, pools, 0);
   // ---- load the tile: 256 chunks x 2K bytes, contiguous in the payload
   {
     const size_t base = static_cast<size_t>(ch0) * 2 * K;
@@ -349,10 +332,10 @@ __global__ __launch_bounds__(256, 1) void k_encode_fast(DevTables T, EncodeArgs 
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const uint32_t row = 4 * m + p;
-      if (row < a.wanted_n) store_row4(out + static_cast<size_t>(row) * a.shard_len, cq_row(cl[p], ch[p]), 4 * lane,
+      if (row < a.wanted_n) store_row4(out + static_cast<size_t>(row) * a.shard_len + 2 * static_cast<size_t>(ch0), cq_row(cl[p], ch[p]), 4 * lane,
                                        ncols, al8);
     }
-    cq_levels<K, true, true>(pools, m, cl, ch);
+    cq_levels<K, true, true>(T, 0, m, cl, ch);
     cq_to_blks(cl, ch, d);
 #pragma unroll
     for (int i = 0; i < 4; ++i) *reinterpret_cast<uint2*>(tile + tile_off<K>(4 * lane + i, m)) = d[i];
@@ -360,7 +343,7 @@ __global__ __launch_bounds__(256, 1) void k_encode_fast(DevTables T, EncodeArgs 
   __syncthreads();
   uint32_t WL[K / 4], WH[K / 4], ML[K / 4], MH[K / 4];
   read_row<K>(tile, tid, WL, WH);
-  ifft_reg<K, true>(pools, WL, WH);
+  ifft_reg<K, true>(T, 0, WL, WH);
 #pragma unroll
   for (int q = 0; q < K / 4; ++q) {
     ML[q] = WL[q];
@@ -370,15 +353,13 @@ __global__ __launch_bounds__(256, 1) void k_encode_fast(DevTables T, EncodeArgs 
   const uint32_t nshift = a.n / K;
   for (uint32_t sh = 1; sh < nshift; ++sh) {
     if (sh * K >= a.wanted_n) break;
-    __syncthreads();  // previous users of pools / tile are done
-    stage_pools<K>(T, pools, sh * K);
-    __syncthreads();
+    __syncthreads();  // the previous chunk-quad pass is done with the tile
 #pragma unroll
     for (int q = 0; q < K / 4; ++q) {
       WL[q] = ML[q];
       WH[q] = MH[q];
     }
-    fft_reg<K, false>(pools, WL, WH);
+    fft_reg<K, false>(T, sh * K, WL, WH);
     write_row<K>(tile, tid, WL, WH);
     __syncthreads();
     for (uint32_t m = wave; m < K / 4; m += 4) {
@@ -387,12 +368,12 @@ __global__ __launch_bounds__(256, 1) void k_encode_fast(DevTables T, EncodeArgs 
       for (int i = 0; i < 4; ++i) d[i] = *reinterpret_cast<const uint2*>(tile + tile_off<K>(4 * lane + i, m));
       uint32_t cl[4], ch[4];
       blks_to_cq(d, cl, ch);
-      cq_levels<K, false, false>(pools, m, cl, ch);
+      cq_levels<K, false, false>(T, sh * K, m, cl, ch);
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         const uint32_t row = sh * K + 4 * m + p;
         if (row < a.wanted_n)
-          store_row4(out + static_cast<size_t>(row) * a.shard_len, cq_row(cl[p], ch[p]), 4 * lane, ncols, al8);
+          store_row4(out + static_cast<size_t>(row) * a.shard_len + 2 * static_cast<size_t>(ch0), cq_row(cl[p], ch[p]), 4 * lane, ncols, al8);
       }
     }
   }
@@ -400,7 +381,7 @@ __global__ __launch_bounds__(256, 1) void k_encode_fast(DevTables T, EncodeArgs 
 
 template <int K>
 size_t encode_lds_bytes() {
-  return static_cast<size_t>(kTile) * 2 * K + static_cast<size_t>(K - 1) * kPoolWords * 4;
+  return static_cast<size_t>(kTile) * 2 * K;
 }
 
 template <int K>

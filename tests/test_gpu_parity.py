@@ -264,3 +264,20 @@ def test_full_size_batch_properties(gpu, oracle, cid):
     ho = host(out)
     for b in range(batch):
         assert ho[b, :plen].tobytes() == pls[b].tobytes(), b
+
+
+@pytest.mark.parametrize("nw,kw,plen", [(256, 86, 128 * 256), (256, 86, 128 * 300 + 5), (256, 86, 1280),
+                                        (512, 100, 128 * 700), (1024, 342, 512 * 256), (1024, 342, 5121),
+                                        (1024, 342, 512 * 512 + 77), (300, 100, 77777), (512, 128, 256 * 600),
+                                        (600, 256, 512 * 300), (2048, 300, 512 * 260)])
+def test_fast_encode_shapes(gpu, oracle, nw, kw, plen):
+    """Specialised encode kernel (k in {64,128,256}): single/multi/partial tiles,
+    odd payload tails, wanted_n < n and n/k in {2,4,8}."""
+    p = npa.CodeParams.derive_parameters(nw, kw)
+    assert p.is_faster8()
+    pl = synth.payload(nw + plen, plen)
+    got = p.make_encoder(gpu).encode(pl)
+    st, want = oracle.encode(pl, p.n(), p.k(), nw)
+    assert st == 0
+    bad = [v for v in range(nw) if got[v] != want[v]]
+    assert not bad, f"{len(bad)} shards differ, first {bad[:5]}"
