@@ -1,8 +1,11 @@
 // Device table pointers shared by host engine and kernels (no device code here).
 #pragma once
+#include <cstddef>
 #include <cstdint>
 
 namespace np {
+
+constexpr size_t kZeroPageBytes = 4096;
 
 // Device copies of the tables of field_tables.hpp (one set per context).
 struct DevTables {
@@ -13,6 +16,7 @@ struct DevTables {
   const uint16_t* log_walsh;   // 65536
   const uint32_t* perm_pools;  // 65536 x 20 dwords
   const uint16_t* split;       // 65536 x 128 u16
+  const uint8_t* zeros;        // kZeroPageBytes of zeros (stand-in source for absent rows)
 };
 
 }  // namespace np

@@ -281,3 +281,30 @@ def test_fast_encode_shapes(gpu, oracle, nw, kw, plen):
     assert st == 0
     bad = [v for v in range(nw) if got[v] != want[v]]
     assert not bad, f"{len(bad)} shards differ, first {bad[:5]}"
+
+
+@pytest.mark.parametrize("nw,kw,plen,erase", [(256, 86, 128 * 256, 170), (256, 86, 128 * 300 + 5, 100),
+                                              (128, 64, 128 * 256, 64), (128, 64, 999, 1),
+                                              (512, 128, 256 * 300, 300), (256, 128, 256 * 256 + 3, 128),
+                                              (1024, 342, 512 * 256, 342), (1024, 342, 512 * 300 + 1, 768),
+                                              (512, 256, 512 * 257, 256), (1000, 256, 4097, 0),
+                                              (1024, 342, 512 * 256, -1)])
+def test_fast_reconstruct_shapes(gpu, oracle, nw, kw, plen, erase):
+    """Specialised reconstruct kernel (k in {64,128,256}, n in {2k,4k}): full and
+    partial column tiles, random and worst-case erasure sets (erase = -1: every
+    systematic shard lost), bit-exact against the oracle."""
+    p = npa.CodeParams.derive_parameters(nw, kw)
+    n, k = p.n(), p.k()
+    assert n in (2 * k, 4 * k) and k in (64, 128, 256)
+    pl = synth.payload(7 * nw + plen, plen)
+    shards = p.make_encoder(gpu).encode(pl)
+    if erase == -1:
+        gone = set(range(k))
+    else:
+        gone = set(synth.erasure_indices(plen + erase, n, min(erase, n - k)).tolist())
+    recv = [None if i in gone else s for i, s in enumerate(shards[:nw])]
+    assert sum(r is not None for r in recv) >= k
+    got = p.make_encoder(gpu).reconstruct(recv)
+    st, want = oracle.reconstruct(recv, n, k)
+    assert st == 0 and got == want
+    assert got[:plen] == pl
