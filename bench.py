@@ -45,11 +45,15 @@ def partition(total: int, world: int, rank: int):
 
 
 def load_traffic(round_tag="r01"):
+    """Per-launch HBM bytes (FETCH_SIZE + WRITE_SIZE, calibrated) of each kernel
+    from the committed PMC summary of this round (tools/profile_round.sh +
+    tools/pmc_summary.py, measured on this same bench command)."""
     p = os.path.join(ROOT, "profiles", f"{round_tag}_pmc_summary.json")
-    if os.path.exists(p):
-        with open(p) as f:
-            return json.load(f)
-    return {}
+    if not os.path.exists(p):
+        return {}
+    with open(p) as f:
+        summary = json.load(f)
+    return {k: v.get("traffic_bytes") for k, v in summary.get("kernels", {}).items()}
 
 
 def cpu_baseline(cfg, params, seconds):

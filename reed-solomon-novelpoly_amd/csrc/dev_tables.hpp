@@ -15,7 +15,6 @@ struct DevTables {
   const uint16_t* skew_add;    // 65536, additive form, 0 = skip
   const uint16_t* log_walsh;   // 65536
   const uint32_t* perm_pools;  // 65536 x 20 dwords
-  const uint16_t* split;       // 65536 x 128 u16
   const uint8_t* zeros;        // kZeroPageBytes of zeros (stand-in source for absent rows)
 };
 

@@ -249,7 +249,6 @@ int np_ctx_create(int device, np_ctx** out) {
   if (e == hipSuccess) e = upload(c, t.skew_add, &c->T.skew_add);
   if (e == hipSuccess) e = upload(c, t.log_walsh, &c->T.log_walsh);
   if (e == hipSuccess) e = upload(c, t.perm_pools, &c->T.perm_pools);
-  if (e == hipSuccess) e = upload(c, t.split, &c->T.split);
   if (e == hipSuccess) e = upload(c, std::vector<uint8_t>(np::kZeroPageBytes, 0), &c->T.zeros);
   if (e == hipSuccess) {
     std::lock_guard<std::mutex> g(g_cfg_mu);

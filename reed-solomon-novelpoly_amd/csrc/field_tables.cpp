@@ -78,15 +78,8 @@ void build(HostTables& t) {
   }
 
   // Multiplier lookup tables, indexed by the additive multiplier c.
-  t.split.assign(static_cast<size_t>(kFieldSize) * kSplitEntries, 0);
   t.perm_pools.assign(static_cast<size_t>(kFieldSize) * kPermPoolWords, 0);
   for (uint32_t c = 0; c < kFieldSize; ++c) {
-    uint16_t* s = &t.split[static_cast<size_t>(c) * kSplitEntries];
-    for (uint32_t v = 0; v < 64; ++v) s[v] = host_mul_add(t, static_cast<uint16_t>(v), static_cast<uint16_t>(c));
-    for (uint32_t v = 0; v < 32; ++v) {
-      s[64 + v] = host_mul_add(t, static_cast<uint16_t>(v << 6), static_cast<uint16_t>(c));
-      s[96 + v] = host_mul_add(t, static_cast<uint16_t>(v << 11), static_cast<uint16_t>(c));
-    }
     // v_perm pools: input byte plane P (0 = low byte, 1 = high byte), bit group
     // G (bits 0-2, 3-5, 6-7 of that byte) -> contribution to output byte O.
     // Layout (dwords): for O in {lo, hi}: [P0G0 lo,hi][P0G1 lo,hi][P0G2][P1G0 lo,hi][P1G1 lo,hi][P1G2]

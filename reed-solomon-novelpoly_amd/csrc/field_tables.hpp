@@ -20,11 +20,8 @@ struct HostTables {
   std::vector<uint16_t> skew_add;   // additive (field element) form of skew, 0 for the sentinel
   std::vector<uint16_t> log_walsh;  // LOG_WALSH
   // Per additive multiplier c (65536 of them): byte tables for the v_perm
-  // multiplier (see kernels.hip, "byte-planar quad multiply"); 20 dwords each.
+  // multiplier (kernels_fast.hip, "GF multiply"); 20 dwords each.
   std::vector<uint32_t> perm_pools;
-  // Per additive multiplier c: 6/5/5-bit split product tables, 128 u16 each:
-  // [0,64) c*v for v = bits 0..5, [64,96) c*(v<<6), [96,128) c*(v<<11).
-  std::vector<uint16_t> split;
 };
 
 // Built once, thread-safe.
@@ -36,6 +33,5 @@ uint16_t host_mul(const HostTables& t, uint16_t a, uint16_t m);
 uint16_t host_mul_add(const HostTables& t, uint16_t a, uint16_t c);
 
 constexpr int kPermPoolWords = 20;
-constexpr int kSplitEntries = 128;
 
 }  // namespace np
