@@ -145,19 +145,41 @@ __device__ __forceinline__ void qplane(uint32_t& acc, const uint32_t (&s)[6], ui
         [sd] "s"(sd), [se] "s"(se), [sf] "s"(sf));
 }
 
+// A multiplier ready for use: its 20 table dwords in SGPRs plus VGPR copies of
+// the 8 dwords that v_perm must read from a VGPR.  The copies are made by an
+// asm block where the butterfly group starts, so that they are neither hoisted
+// next to the s_load of a prefetched table nor repeated per butterfly.
+struct Mult {
+  uint32_t s[20];
+  uint32_t v[8];
+};
+
+__device__ __forceinline__ Mult make_mult(const uint32_t (&p)[20]) {
+  Mult m;
+#pragma unroll
+  for (int i = 0; i < 20; ++i) m.s[i] = p[i];
+  asm volatile(
+      "v_mov_b32 %0, %8\n\tv_mov_b32 %1, %9\n\tv_mov_b32 %2, %10\n\tv_mov_b32 %3, %11\n\t"
+      "v_mov_b32 %4, %12\n\tv_mov_b32 %5, %13\n\tv_mov_b32 %6, %14\n\tv_mov_b32 %7, %15"
+      : "=v"(m.v[0]), "=v"(m.v[1]), "=v"(m.v[2]), "=v"(m.v[3]), "=v"(m.v[4]), "=v"(m.v[5]), "=v"(m.v[6]),
+        "=v"(m.v[7])
+      : "s"(p[0]), "s"(p[2]), "s"(p[5]), "s"(p[7]), "s"(p[10]), "s"(p[12]), "s"(p[15]), "s"(p[17]));
+  return m;
+}
+
 // x ^= c*y on four byte-planar symbols (pool layout: field_tables.cpp).
-__device__ __forceinline__ void qmul(uint32_t& xl, uint32_t& xh, uint32_t yl, uint32_t yh, const uint32_t (&p)[20]) {
+__device__ __forceinline__ void qmul(uint32_t& xl, uint32_t& xh, uint32_t yl, uint32_t yh, const Mult& m) {
   uint32_t s[6];
   selectors(yl, yh, s);
-  qplane(xl, s, p[0], p[2], p[5], p[7], p[1], p[3], p[4], p[6], p[8], p[9]);
-  qplane(xh, s, p[10], p[12], p[15], p[17], p[11], p[13], p[14], p[16], p[18], p[19]);
+  qplane(xl, s, m.v[0], m.v[1], m.v[2], m.v[3], m.s[1], m.s[3], m.s[4], m.s[6], m.s[8], m.s[9]);
+  qplane(xh, s, m.v[4], m.v[5], m.v[6], m.v[7], m.s[11], m.s[13], m.s[14], m.s[16], m.s[18], m.s[19]);
 }
 
 // (ol, oh) = c*y.
-__device__ __forceinline__ void qmul_set(uint32_t& ol, uint32_t& oh, uint32_t yl, uint32_t yh, const uint32_t (&p)[20]) {
+__device__ __forceinline__ void qmul_set(uint32_t& ol, uint32_t& oh, uint32_t yl, uint32_t yh, const Mult& m) {
   ol = 0;
   oh = 0;
-  qmul(ol, oh, yl, yh, p);
+  qmul(ol, oh, yl, yh, m);
 }
 
 typedef const __attribute__((address_space(4))) uint32_t* cpool_t;
@@ -165,6 +187,9 @@ typedef const __attribute__((address_space(4))) uint32_t* cpool_t;
 // Multiplier tables of the additive element c via the scalar cache (c is
 // wave-uniform, so this is s_load).
 __device__ __forceinline__ void pool_of(const DevTables& T, uint32_t c, uint32_t (&p)[20]) {
+  // opaque index: two fetches of the same table (e.g. beta, or the index-0
+  // skews shared by an IFFT and an FFT) must not be merged into one long-lived value
+  asm volatile("" : "+s"(c));
   const cpool_t q = (cpool_t)(T.perm_pools) + c * kPoolWords;
 #pragma unroll
   for (int i = 0; i < 20; ++i) p[i] = q[i];
@@ -312,7 +337,7 @@ __device__ __forceinline__ void pipe_step(const DevTables& T, CF& cval, GF& grou
   if constexpr (F < NG) {
     if constexpr (F + 1 < NG) pool_of(T, cval(Int<F + 1>{}), nxt);
     __builtin_amdgcn_sched_barrier(0);
-    group(Int<F>{}, cur);
+    group(Int<F>{}, make_mult(cur));
     __builtin_amdgcn_sched_barrier(0);
     pipe_step<F + 1, NG>(T, cval, group, nxt, cur);
   }
@@ -369,7 +394,7 @@ __device__ __forceinline__ void cq_levels(const DevTables& T, uint32_t index, ui
     constexpr GroupRef r = cq_group<INVERSE>(decltype(fc)::value);
     return 2u * (g * (8u >> r.b) + r.t) + (index >> r.b);
   };
-  auto group = [&](auto fc, const uint32_t (&p)[20]) __attribute__((always_inline)) {
+  auto group = [&](auto fc, const Mult& p) __attribute__((always_inline)) {
     constexpr GroupRef r = cq_group<INVERSE>(decltype(fc)::value);
     constexpr int d = 1 << r.b;
     const bool live = !INDEX0 || r.t != 0 || g != 0;  // c == 0: the skew sentinel, no product
@@ -399,7 +424,7 @@ __device__ __forceinline__ void hi_levels(const DevTables& T, uint32_t index, ui
     constexpr GroupRef r = hi_group<K, INVERSE>(decltype(fc)::value);
     return 2u * r.t + (index >> r.b);
   };
-  auto group = [&](auto fc, const uint32_t (&p)[20]) __attribute__((always_inline)) {
+  auto group = [&](auto fc, const Mult& p) __attribute__((always_inline)) {
     constexpr GroupRef r = hi_group<K, INVERSE>(decltype(fc)::value);
     constexpr int dj = 1 << (r.b - 2 - logR);
     constexpr bool live = !INDEX0 || r.t != 0;
@@ -439,7 +464,8 @@ __device__ __forceinline__ void add_derivative(uint32_t (&A)[16], uint32_t (&X)[
     for (int jb = 0; jb < 4; ++jb)
       if (!(j & (1 << jb))) v ^= X[j | (1 << jb)];
     A[j] ^= v;
-    X[j] = 0;  // dead from here on
+    asm volatile("" : "+v"(A[j]));  // finish position j here (bounded temporaries)
+    X[j] = 0;                       // dead from here on
   }
 }
 
@@ -484,7 +510,7 @@ __device__ __forceinline__ void hi_write(uint8_t* tile, uint32_t base, const uin
 // ----------------------------------------------------------------- encode ----
 // One workgroup: 256 chunks of one payload.  mod.rs:144-154 / inc_encode.rs:15-48.
 template <int K>
-__global__ __launch_bounds__(4 * K) void k_encode_fast(DevTables T, EncodeArgs a, uint32_t nchunks, uint32_t tiles) {
+__global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_fast(DevTables T, EncodeArgs a, uint32_t nchunks, uint32_t tiles) {
   using G = Geo<K>;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
@@ -596,7 +622,7 @@ __device__ __forceinline__ void rec_segment(const RecCtx& c, uint32_t (&AL)[16],
     load_rows<8>(raw, sh, shard_len, PR, index + 16 * g + 8 * half, T.zeros, c.lane, c.ncols, c.full);
     pipelined<8>(
         T, [&](auto pc) __attribute__((always_inline)) { return uniform(E[index + 16 * g + 8 * half + decltype(pc)::value]); },
-        [&](auto pc, const uint32_t (&pool)[20]) __attribute__((always_inline)) {
+        [&](auto pc, const Mult& pool) __attribute__((always_inline)) {
           constexpr int p = decltype(pc)::value;
           const int x = 8 * half + p;
           uint32_t l, h;
@@ -628,8 +654,9 @@ __device__ __forceinline__ void rec_segment(const RecCtx& c, uint32_t (&AL)[16],
     add_derivative<K>(AL, XL, c.tid % Geo<K>::R);
     add_derivative<K>(AH, XH, c.tid % Geo<K>::R);
   } else if constexpr (NQ == 4 && q == 3) {
-    uint32_t pool[20];
-    pool_of(T, 2u, pool);  // beta = Cantor(2), the t = 1 skew of level logK at index 0
+    uint32_t beta[20];
+    pool_of(T, 2u, beta);  // beta = Cantor(2), the t = 1 skew of level logK at index 0
+    const Mult pool = make_mult(beta);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       XL[j] ^= AL[j];
@@ -657,7 +684,7 @@ __device__ __forceinline__ void rec_segment(const RecCtx& c, uint32_t (&AL)[16],
 // derivative of size K; then out = FFT(K, 0)(d) (the size-n forward transform
 // restricted to its first K outputs is FFT(K, 0): its t = 0 skews are 0).
 template <int K, int NQ>
-__global__ __launch_bounds__(4 * K) void k_reconstruct_fast(DevTables T, ReconstructArgs a, uint32_t nsyms,
+__global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void k_reconstruct_fast(DevTables T, ReconstructArgs a, uint32_t nsyms,
                                                             uint32_t tiles) {
   using G = Geo<K>;
   constexpr int N = NQ * K;
@@ -709,7 +736,7 @@ __global__ __launch_bounds__(4 * K) void k_reconstruct_fast(DevTables T, Reconst
       load_rows<8>(raw, sh, a.shard_len, PR, 16 * g + 8 * half, T.zeros, lane, ncols, full);
       pipelined<8>(
           T, [&](auto pc) __attribute__((always_inline)) { return uniform(E[16 * g + 8 * half + decltype(pc)::value]); },
-          [&](auto pc, const uint32_t (&pool)[20]) __attribute__((always_inline)) {
+          [&](auto pc, const Mult& pool) __attribute__((always_inline)) {
             constexpr int p = decltype(pc)::value;
             const int x = 8 * half + p;
             // present: the received symbol (mod.rs:225-235); erased: the
