@@ -127,9 +127,11 @@ int np_encode_batch_dev(np_ctx* ctx, const np_code_params* params, const uint8_t
 int np_reconstruct_batch_dev(np_ctx* ctx, const np_code_params* params, const uint8_t* d_shards,
                              size_t shard_len, size_t batch_stride, const uint8_t* present, size_t batch,
                              uint8_t* d_out, size_t out_stride, void* stream);
-/* Same as np_reconstruct_batch_dev with the erasure locators already computed
- * (d_locators: batch rows of n uint16, see np_error_locator_dev) and the present
- * mask on the device (d_present: batch rows of n bytes). */
+/* Same as np_reconstruct_batch_dev with the present mask on the device
+ * (d_present: batch rows of n bytes) and optionally the erasure locators already
+ * computed (d_locators: batch rows of n uint16, see np_error_locator_dev).
+ * d_locators == NULL: the locators are computed on the device (fused into the
+ * reconstruct kernel on the fast path).  No host-side NeedMoreShards check. */
 int np_reconstruct_batch_dev2(np_ctx* ctx, const np_code_params* params, const uint8_t* d_shards,
                               size_t shard_len, size_t batch_stride, const uint8_t* d_present,
                               const uint16_t* d_locators, size_t batch, uint8_t* d_out, size_t out_stride,

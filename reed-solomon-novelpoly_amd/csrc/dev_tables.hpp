@@ -14,6 +14,7 @@ struct DevTables {
   const uint16_t* skew;        // 65536, log form, 65535 = skip
   const uint16_t* skew_add;    // 65536, additive form, 0 = skip
   const uint16_t* log_walsh;   // 65536
+  const uint16_t* lw_fold;     // 2 x 65536, F_n at [n, 2n) (field_tables.hpp)
   const uint32_t* perm_pools;  // 65536 x 20 dwords
   const uint8_t* zeros;        // kZeroPageBytes of zeros (stand-in source for absent rows)
 };

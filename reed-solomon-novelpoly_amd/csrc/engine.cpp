@@ -152,9 +152,18 @@ hipError_t launch_encode(np_ctx* c, const np::EncodeArgs& a, hipStream_t s) {
   return np::launch_encode_generic(c->T, a, s);
 }
 
+// a.locators == nullptr: the locators are computed on the device (fused into
+// the fast kernel; a locator launch into the context scratch otherwise, which
+// needs the context lock held by the caller).
 hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream_t s) {
   if (np::fast_reconstruct_supported(a.n, a.k)) return np::launch_reconstruct_fast(c->T, a, s);
-  return np::launch_reconstruct_generic(c->T, a, s);
+  if (a.locators) return np::launch_reconstruct_generic(c->T, a, s);
+  np::ReconstructArgs b = a;
+  hipError_t e = c->d_loc.ensure(std::max<size_t>(a.batch * a.n * sizeof(uint16_t), 2));
+  if (e == hipSuccess) e = np::launch_error_locator(c->T, a.n, a.present, a.batch, c->d_loc.as<uint16_t>(), s);
+  if (e != hipSuccess) return e;
+  b.locators = c->d_loc.as<uint16_t>();
+  return np::launch_reconstruct_generic(c->T, b, s);
 }
 
 hipStream_t pick(np_ctx* c, void* s) { return s ? static_cast<hipStream_t>(s) : c->stream; }
@@ -248,6 +257,7 @@ int np_ctx_create(int device, np_ctx** out) {
   if (e == hipSuccess) e = upload(c, t.skew, &c->T.skew);
   if (e == hipSuccess) e = upload(c, t.skew_add, &c->T.skew_add);
   if (e == hipSuccess) e = upload(c, t.log_walsh, &c->T.log_walsh);
+  if (e == hipSuccess) e = upload(c, t.lw_fold, &c->T.lw_fold);
   if (e == hipSuccess) e = upload(c, t.perm_pools, &c->T.perm_pools);
   if (e == hipSuccess) e = upload(c, std::vector<uint8_t>(np::kZeroPageBytes, 0), &c->T.zeros);
   if (e == hipSuccess) {
@@ -353,9 +363,11 @@ int np_reconstruct_batch_dev2(np_ctx* c, const np_code_params* p, const uint8_t*
   int st = check_params(p);
   if (st) return st;
   if (shard_len == 0 || (shard_len & 1)) return fail(NP_ERR_EMPTY_SHARD);
-  if (!d_shards || !d_present || !d_loc || !d_out || bstride < p->n * shard_len ||
-      out_stride < (shard_len / 2) * 2 * p->k)
+  if (!d_shards || !d_present || !d_out || bstride < p->n * shard_len || out_stride < (shard_len / 2) * 2 * p->k)
     return fail(NP_ERR_INVALID_ARGUMENT);
+  std::unique_lock<std::mutex> g(c->mu, std::defer_lock);
+  if (!d_loc && !np::fast_reconstruct_supported(static_cast<uint32_t>(p->n), static_cast<uint32_t>(p->k)))
+    g.lock();  // generic path: locators go to the context scratch
   (void)hipSetDevice(c->device);
   np::ReconstructArgs a{};
   a.shards = d_shards;
@@ -385,17 +397,26 @@ int np_reconstruct_batch_dev(np_ctx* c, const np_code_params* p, const uint8_t* 
   std::lock_guard<std::mutex> g(c->mu);
   (void)hipSetDevice(c->device);
   hipStream_t s = pick(c, stream);
+  if (shard_len == 0 || (shard_len & 1)) return fail(NP_ERR_EMPTY_SHARD);
+  if (!d_shards || !d_out || bstride < p->n * shard_len || out_stride < (shard_len / 2) * 2 * p->k)
+    return fail(NP_ERR_INVALID_ARGUMENT);
   hipError_t e = c->d_present.ensure(std::max<size_t>(batch * p->n, 1));
-  if (e == hipSuccess) e = c->d_loc.ensure(std::max<size_t>(batch * p->n * sizeof(uint16_t), 2));
   if (e != hipSuccess) return dev_err(e);
   e = hipMemcpyAsync(c->d_present.p, present, batch * p->n, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess)
-    e = np::launch_error_locator(c->T, static_cast<uint32_t>(p->n), c->d_present.as<uint8_t>(), batch,
-                                 c->d_loc.as<uint16_t>(), s);
   if (e != hipSuccess) return dev_err(e);
-  st = np_reconstruct_batch_dev2(c, p, d_shards, shard_len, bstride, c->d_present.as<uint8_t>(),
-                                 c->d_loc.as<uint16_t>(), batch, d_out, out_stride, s);
-  if (st) return st;
+  np::ReconstructArgs a{};
+  a.shards = d_shards;
+  a.shard_len = shard_len;
+  a.batch_stride = bstride;
+  a.present = c->d_present.as<uint8_t>();
+  a.locators = nullptr;  // computed on the device
+  a.batch = batch;
+  a.n = static_cast<uint32_t>(p->n);
+  a.k = static_cast<uint32_t>(p->k);
+  a.out = d_out;
+  a.out_stride = out_stride;
+  e = launch_reconstruct(c, a, s);
+  if (e != hipSuccess) return dev_err(e);
   // present mask was copied from pageable host memory: make the call
   // synchronous with respect to it before returning.
   return dev_err(hipStreamSynchronize(s));
@@ -433,7 +454,6 @@ int np_rs_reconstruct(np_ctx* c, const np_code_params* p, const uint8_t* const* 
   if (e == hipSuccess) e = c->d_out.ensure(need);
   if (e == hipSuccess) e = c->h_out.ensure(need);
   if (e == hipSuccess) e = c->d_present.ensure(n);
-  if (e == hipSuccess) e = c->d_loc.ensure(n * sizeof(uint16_t));
   if (e != hipSuccess) return dev_err(e);
   uint8_t* stage = c->h_in.as<uint8_t>();
   for (size_t i = 0; i < n; ++i) {
@@ -448,16 +468,13 @@ int np_rs_reconstruct(np_ctx* c, const np_code_params* p, const uint8_t* const* 
   hipStream_t s = c->stream;
   e = hipMemcpyAsync(c->d_in.p, stage, n * sl, hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipMemcpyAsync(c->d_present.p, present.data(), n, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess)
-    e = np::launch_error_locator(c->T, static_cast<uint32_t>(n), c->d_present.as<uint8_t>(), 1,
-                                 c->d_loc.as<uint16_t>(), s);
   if (e == hipSuccess) {
     np::ReconstructArgs a{};
     a.shards = c->d_in.as<uint8_t>();
     a.shard_len = sl;
     a.batch_stride = n * sl;
     a.present = c->d_present.as<uint8_t>();
-    a.locators = c->d_loc.as<uint16_t>();
+    a.locators = nullptr;  // computed on the device
     a.batch = 1;
     a.n = static_cast<uint32_t>(n);
     a.k = static_cast<uint32_t>(k);

@@ -51,6 +51,13 @@ void build(HostTables& t) {
   t.log_walsh = t.log;
   t.log_walsh[0] = 0;
   fwht_mod_onemask(t.log_walsh.data(), kFieldSize);
+  t.lw_fold.assign(2 * static_cast<size_t>(kFieldSize), 0);
+  for (uint32_t n = 1; n <= kFieldSize; n <<= 1)
+    for (uint32_t j = 0; j < n; ++j) {
+      uint64_t acc = 0;
+      for (uint32_t h = j; h < kFieldSize; h += n) acc += t.log_walsh[h];
+      t.lw_fold[n + j] = static_cast<uint16_t>(acc % kOneMask);
+    }
 
   // Skew factors (inc_afft.rs:386-445).
   std::vector<uint16_t> sk(kFieldSize, 0);

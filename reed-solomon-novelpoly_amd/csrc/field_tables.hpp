@@ -19,6 +19,11 @@ struct HostTables {
   std::vector<uint16_t> skew;       // 65536 entries, log form, [i]==65535 -> multiply skipped (AFFT.skews)
   std::vector<uint16_t> skew_add;   // additive (field element) form of skew, 0 for the sentinel
   std::vector<uint16_t> log_walsh;  // LOG_WALSH
+  // LOG_WALSH folded to n points for every power of two n: entries [n, 2n) hold
+  // F_n[j] = sum_h LOG_WALSH[j + n*h] mod 65535 (the 65536-point
+  // Walsh pair of eval_error_polynomial restricted to an erasure set inside
+  // [0, n) equals two n-point Walsh transforms around F_n, mod 65535).
+  std::vector<uint16_t> lw_fold;
   // Per additive multiplier c (65536 of them): byte tables for the v_perm
   // multiplier (kernels_fast.hip, "GF multiply"); 20 dwords each.
   std::vector<uint32_t> perm_pools;

@@ -588,6 +588,55 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
   }
 }
 
+// ---------------------------------------------------------------- locator ----
+// eval_error_polynomial (inc_reconstruct.rs:90-113, called over the whole field
+// by mod.rs:217-218) for an erasure set inside [0, N), folded to N points
+// (SURVEY F8): loc = WHT_N(WHT_N(e) * F_N mod 65535) mod 65535 with F_N the
+// folded LOG_WALSH (field_tables.hpp).  Equal to the reference mod 65535, which
+// is all a multiplier needs (EXP[65535] == EXP[0]).  Leaves E[v] = EXP[loc] for
+// present rows and EXP[65535 - loc] for erased rows (the postmultiplier,
+// inc_reconstruct.rs:108-112), and PR[v] = present flag.  W: N dwords of scratch.
+template <int N, int NT>
+__device__ __forceinline__ void fused_locator(const DevTables& T, const uint8_t* pres, uint32_t* W, uint16_t* E,
+                                              uint8_t* PR) {
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t v = tid; v < N; v += NT) {
+    const uint8_t p = pres[v];
+    PR[v] = p;
+    W[v] = p ? 0u : 1u;
+  }
+  __syncthreads();
+  for (uint32_t h = 1; h < N; h <<= 1) {  // integer WHT of the 0/1 erasure vector
+    for (uint32_t b = tid; b < N / 2; b += NT) {
+      const uint32_t i = (b / h) * 2 * h + (b % h), j = i + h;
+      const int32_t x = static_cast<int32_t>(W[i]), y = static_cast<int32_t>(W[j]);
+      W[i] = static_cast<uint32_t>(x + y);
+      W[j] = static_cast<uint32_t>(x - y);
+    }
+    __syncthreads();
+  }
+  const uint16_t* F = T.lw_fold + N;
+  for (uint32_t v = tid; v < N; v += NT) {
+    const int32_t x = static_cast<int32_t>(W[v]);  // |x| <= N
+    const uint32_t m = x < 0 ? static_cast<uint32_t>(x + 65535) : static_cast<uint32_t>(x);
+    W[v] = (m * static_cast<uint32_t>(F[v])) % 65535u;
+  }
+  __syncthreads();
+  for (uint32_t h = 1; h < N; h <<= 1) {  // WHT mod 65535
+    for (uint32_t b = tid; b < N / 2; b += NT) {
+      const uint32_t i = (b / h) * 2 * h + (b % h), j = i + h;
+      const uint32_t x = W[i], y = W[j];
+      uint32_t s = x + y, d = x + 65535u - y;
+      s -= s >= 65535u ? 65535u : 0u;
+      d -= d >= 65535u ? 65535u : 0u;
+      W[i] = s;
+      W[j] = d;
+    }
+    __syncthreads();
+  }
+  for (uint32_t v = tid; v < N; v += NT) E[v] = T.exp[PR[v] ? W[v] : 65535u - W[v]];
+}
+
 // ------------------------------------------------------------ reconstruct ----
 struct RecCtx {
   const DevTables& T;
@@ -625,9 +674,13 @@ __device__ __forceinline__ void rec_segment(const RecCtx& c, uint32_t (&AL)[16],
         [&](auto pc, const Mult& pool) __attribute__((always_inline)) {
           constexpr int p = decltype(pc)::value;
           const int x = 8 * half + p;
-          uint32_t l, h;
-          blk_to_quad(raw[p], l, h);  // absent rows read as zero
-          qmul_set(XL[x], XH[x], l, h, pool);
+          XL[x] = 0;  // absent rows contribute zero
+          XH[x] = 0;
+          if (uniform(PR[index + 16 * g + x])) {
+            uint32_t l, h;
+            blk_to_quad(raw[p], l, h);
+            qmul_set(XL[x], XH[x], l, h, pool);
+          }
         });
   }
   cq_levels<true, q == 0>(T, index, g, XL, XH);
@@ -702,9 +755,13 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
   const bool full =
       ncols == kTile && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
 
-  for (uint32_t v = tid; v < static_cast<uint32_t>(N); v += G::kThreads) {
-    E[v] = T.exp[loc[v]];  // mul(x, log m) == x * EXP[m] (inc_log_mul.rs:42-49)
-    PR[v] = pres[v];
+  if (loc) {
+    for (uint32_t v = tid; v < static_cast<uint32_t>(N); v += G::kThreads) {
+      E[v] = T.exp[loc[v]];  // mul(x, log m) == x * EXP[m] (inc_log_mul.rs:42-49)
+      PR[v] = pres[v];
+    }
+  } else {
+    fused_locator<N, G::kThreads>(T, pres, reinterpret_cast<uint32_t*>(tile), E, PR);
   }
   __syncthreads();
 
@@ -741,12 +798,12 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
             const int x = 8 * half + p;
             // present: the received symbol (mod.rs:225-235); erased: the
             // postmultiplied recovered symbol (inc_reconstruct.rs:76-84)
-            const bool present = uniform(PR[16 * g + x]) != 0;
-            uint32_t ml, mh, rl, rh;
-            qmul_set(ml, mh, XL[x], XH[x], pool);
-            blk_to_quad(raw[p], rl, rh);
-            XL[x] = present ? rl : ml;
-            XH[x] = present ? rh : mh;
+            if (uniform(PR[16 * g + x])) {
+              blk_to_quad(raw[p], XL[x], XH[x]);
+            } else {
+              const uint32_t l = XL[x], h = XH[x];
+              qmul_set(XL[x], XH[x], l, h, pool);
+            }
           });
     }
     __syncthreads();

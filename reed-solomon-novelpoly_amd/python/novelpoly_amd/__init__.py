@@ -408,7 +408,8 @@ def reconstruct_batch_dev2(params: CodeParams, d_shards: int, shard_len: int, ba
                            ctx: Optional[Context] = None, stream: int = 0) -> None:
     ctx = ctx or default_context()
     _raise(lib().np_reconstruct_batch_dev2(ctx.handle, C.byref(params._c()), d_shards, shard_len, batch_stride,
-                                           d_present, d_locators, batch, d_out, out_stride, stream or None))
+                                           d_present, d_locators or None, batch, d_out, out_stride,
+                                           stream or None))
 
 
 def reconstruct_batch_dev(params: CodeParams, d_shards: int, shard_len: int, batch_stride: int, present,

@@ -1,0 +1,82 @@
+"""World-size-2 gloo test of the multi-GPU bench logic on CPU: disjoint payload
+ranges per rank, barrier + max-over-ranks timing, whole-job aggregate, and the
+per-rank work itself (checked with the CPU oracle as the stand-in compute, since
+there is no GPU here).  The GPU run uses the same functions over RCCL."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "reed-solomon-novelpoly_amd", "python")]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, per_rank, q):
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    import np_oracle
+    from novelpoly_amd import synth
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = bench.partition(per_rank, world, rank)
+    orc = np_oracle.Oracle()
+    n, k, plen = 16, 8, 600
+    dist.barrier()
+    t0 = time.perf_counter()
+    ok = True
+    for i in range(lo, hi):
+        pl = synth.payload(i, plen)
+        st, shards = orc.encode(pl, n, k, n)
+        pres = synth.present_mask(i, n, 8)
+        st2, rec = orc.reconstruct([s if pres[j] else None for j, s in enumerate(shards)], n, k)
+        ok &= st == 0 and st2 == 0 and rec[:plen] == pl
+    time.sleep(0.05 * (rank + 1))  # make the ranks' clocks differ
+    mine = time.perf_counter() - t0
+    dist.barrier()
+    job = bench.max_over_ranks(mine, dist, torch.device("cpu"))
+    q.put((rank, lo, hi, mine, job, ok, bench.aggregate_gib_s(world, per_rank, plen, job, 1)))
+    dist.destroy_process_group()
+
+
+def test_two_rank_weak_scaling_logic():
+    world, per_rank = 2, 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, per_rank, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ranges = [(r[1], r[2]) for r in res]
+    assert ranges == [(0, 3), (3, 6)]  # disjoint, covering the global batch
+    assert all(r[5] for r in res)  # every rank's payloads round-trip
+    slowest = max(r[3] for r in res)
+    for r in res:
+        assert r[4] == pytest.approx(slowest)  # every rank reports the max
+        assert r[6] == pytest.approx(world * per_rank * 600 / slowest / 2**30)
+
+
+def test_partition_is_disjoint_and_complete():
+    import bench
+
+    for world in (1, 2, 4, 8):
+        got = [bench.partition(1024, world, r) for r in range(world)]
+        assert got[0][0] == 0 and got[-1][1] == 1024 * world
+        assert all(a[1] == b[0] for a, b in zip(got, got[1:]))

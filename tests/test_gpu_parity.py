@@ -308,3 +308,39 @@ def test_fast_reconstruct_shapes(gpu, oracle, nw, kw, plen, erase):
     st, want = oracle.reconstruct(recv, n, k)
     assert st == 0 and got == want
     assert got[:plen] == pl
+
+
+@pytest.mark.parametrize("nw,kw,plen,batch", [(1024, 342, 512 * 300, 5), (256, 86, 128 * 256 + 7, 9),
+                                              (512, 256, 512 * 256, 3), (2048, 512, 1024 * 40, 2)])
+def test_device_reconstruct_locator_modes(gpu, oracle, nw, kw, plen, batch):
+    """np_reconstruct_batch_dev2 with locators from np_error_locator_dev and with
+    d_locators = NULL (computed on the device: fused folded locator on the fast
+    path) give the oracle's bytes."""
+    import torch
+
+    p = npa.CodeParams.derive_parameters(nw, kw)
+    n, k = p.n(), p.k()
+    sl = p.make_encoder(gpu).shard_len(plen)
+    pls = np.stack([np.frombuffer(synth.payload(900 + b, plen), dtype=np.uint8) for b in range(batch)])
+    dp = dev(pls)
+    ds = torch.empty((batch, n, sl), dtype=torch.uint8, device="cuda")
+    npa.encode_batch_dev(p, dp.data_ptr(), plen, plen, batch, ds.data_ptr(), n * sl, ctx=gpu, stream=stream())
+    pres = np.stack([synth.present_mask(900 + b, n, (n - k) if b % 2 else (n - k) // 3) for b in range(batch)])
+    dpres = dev(pres)
+    loc = torch.empty((batch, n), dtype=torch.int16, device="cuda")
+    npa.error_locator_dev(n, dpres.data_ptr(), batch, loc.data_ptr(), ctx=gpu, stream=stream())
+    olen = (sl // 2) * 2 * k
+    outs = []
+    for lp in (loc.data_ptr(), 0):
+        out = torch.empty((batch, olen), dtype=torch.uint8, device="cuda")
+        npa.reconstruct_batch_dev2(p, ds.data_ptr(), sl, n * sl, dpres.data_ptr(), lp, batch, out.data_ptr(), olen,
+                                   ctx=gpu, stream=stream())
+        outs.append(host(out))
+    hs = host(ds)
+    for b in range(batch):
+        recv = [hs[b, i].tobytes() if pres[b, i] else None for i in range(n)]
+        st, want = oracle.reconstruct(recv, n, k)
+        assert st == 0
+        for o in outs:
+            assert o[b].tobytes() == want, b
+        assert want[:plen] == pls[b].tobytes()

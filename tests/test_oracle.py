@@ -232,3 +232,31 @@ def test_glue_errors(oracle):
     assert oracle.reconstruct(recv, 16, 4) == (7, (shards[0].__len__() // 2, len(shards[3]) // 2 - 1, 0))
     assert oracle.reconstruct_from_systematic([], 16, 4)[0] == 5
     assert oracle.reconstruct_from_systematic(shards[:3], 16, 4) == (5, (3, 4, 16))
+
+
+@pytest.mark.parametrize("n", [16, 256, 1024, 4096])
+def test_locator_fold_identity(oracle, n):
+    """SURVEY F8, used by the fused locator of the fast reconstruct kernel: for an
+    erasure set inside [0, n) the 65536-point Walsh pair of eval_error_polynomial
+    equals two n-point Walsh transforms around the folded LOG_WALSH, mod 65535."""
+    lw = oracle.log_walsh().astype(np.int64)
+    fold = lw.reshape(-1, n).sum(axis=0) % 65535
+
+    def wht(v):
+        v = v.copy()
+        h = 1
+        while h < len(v):
+            v = v.reshape(-1, 2, h)
+            a, b = v[:, 0, :].copy(), v[:, 1, :].copy()
+            v[:, 0, :], v[:, 1, :] = a + b, a - b
+            v = v.reshape(-1)
+            h *= 2
+        return v
+
+    rng = np.random.default_rng(n)
+    for trial in range(6):
+        erased = rng.random(n) < (0.05, 0.33, 0.67, 0.0, 0.9, 0.5)[trial]
+        want = oracle.eval_error_polynomial(erased.tolist())[:n].astype(np.int64)
+        loc = wht((wht(erased.astype(np.int64)) % 65535) * fold % 65535) % 65535
+        loc = np.where(erased, (65535 - loc) % 65535, loc)
+        assert np.array_equal(loc % 65535, want % 65535), trial
