@@ -101,6 +101,11 @@ struct np_ctx {
   std::mutex mu;  // serialises host-API calls (they share the scratch buffers)
   DevBuf d_in, d_out, d_present, d_loc;
   HostBuf h_in, h_out;
+  // Per-workgroup scratch of the k = 1024 kernels (kernels_big.hip).  Launches
+  // on different streams are ordered through big_done so they never share it.
+  DevBuf d_big;
+  hipEvent_t big_done = nullptr;
+  bool big_used = false;
 };
 
 namespace {
@@ -147,8 +152,41 @@ np::EncodeArgs enc_args(const np_code_params* p, const uint8_t* payloads, size_t
   return a;
 }
 
+constexpr size_t kBigScratchCap = size_t(1) << 30;  // bytes of k = 1024 scratch per context
+
+// Big-kernel scratch of `want` bytes (capped), ordered after every earlier
+// big launch of this context on any stream.  Caller holds the context lock.
+hipError_t big_scratch(np_ctx* c, size_t want, hipStream_t s, uint8_t** out, size_t* bytes) {
+  want = std::min(want, kBigScratchCap);
+  hipError_t e = hipSuccess;
+  if (!c->big_done) e = hipEventCreateWithFlags(&c->big_done, hipEventDisableTiming);
+  if (e == hipSuccess && c->big_used) {
+    if (want > c->d_big.cap) e = hipEventSynchronize(c->big_done);  // about to free the old buffer
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, c->big_done, 0);
+  }
+  if (e == hipSuccess) e = c->d_big.ensure(want);
+  *out = c->d_big.as<uint8_t>();
+  *bytes = c->d_big.cap;
+  return e;
+}
+
+hipError_t big_done(np_ctx* c, hipStream_t s, hipError_t e) {
+  if (e != hipSuccess) return e;
+  c->big_used = true;
+  return hipEventRecord(c->big_done, s);
+}
+
+// Caller holds the context lock.
 hipError_t launch_encode(np_ctx* c, const np::EncodeArgs& a, hipStream_t s) {
   if (np::fast_encode_supported(a.n, a.k)) return np::launch_encode_fast(c->T, a, s);
+  if (np::big_encode_supported(a.n, a.k)) {
+    const size_t tiles = ((a.payload_len + 2 * a.k - 1) / (2 * a.k) + 255) / 256;
+    uint8_t* scr = nullptr;
+    size_t bytes = 0;
+    hipError_t e = big_scratch(c, a.batch * tiles * np::big_encode_scratch_per_tile(), s, &scr, &bytes);
+    if (e == hipSuccess) e = np::launch_encode_big(c->T, a, scr, bytes, s);
+    return big_done(c, s, e);
+  }
   return np::launch_encode_generic(c->T, a, s);
 }
 
@@ -157,6 +195,14 @@ hipError_t launch_encode(np_ctx* c, const np::EncodeArgs& a, hipStream_t s) {
 // needs the context lock held by the caller).
 hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream_t s) {
   if (np::fast_reconstruct_supported(a.n, a.k)) return np::launch_reconstruct_fast(c->T, a, s);
+  if (np::big_reconstruct_supported(a.n, a.k)) {
+    const size_t tiles = (a.shard_len / 2 + 255) / 256;
+    uint8_t* scr = nullptr;
+    size_t bytes = 0;
+    hipError_t e = big_scratch(c, a.batch * tiles * np::big_reconstruct_scratch_per_tile(a.n), s, &scr, &bytes);
+    if (e == hipSuccess) e = np::launch_reconstruct_big(c->T, a, scr, bytes, s);
+    return big_done(c, s, e);
+  }
   if (a.locators) return np::launch_reconstruct_generic(c->T, a, s);
   np::ReconstructArgs b = a;
   hipError_t e = c->d_loc.ensure(std::max<size_t>(a.batch * a.n * sizeof(uint16_t), 2));
@@ -231,7 +277,8 @@ size_t np_shard_len(const np_code_params* p, size_t payload_size) {
 
 int np_is_fast_path(const np_code_params* p) {
   if (!p) return 0;
-  return np::fast_encode_supported(static_cast<uint32_t>(p->n), static_cast<uint32_t>(p->k)) ? 1 : 0;
+  const uint32_t n = static_cast<uint32_t>(p->n), k = static_cast<uint32_t>(p->k);
+  return (np::fast_encode_supported(n, k) || np::big_encode_supported(n, k)) ? 1 : 0;
 }
 
 int np_ctx_create(int device, np_ctx** out) {
@@ -265,6 +312,7 @@ int np_ctx_create(int device, np_ctx** out) {
     if (std::find(g_configured_devices.begin(), g_configured_devices.end(), device) == g_configured_devices.end()) {
       e = np::configure_generic_kernels();
       if (e == hipSuccess) e = np::configure_fast_kernels();
+      if (e == hipSuccess) e = np::configure_big_kernels();
       if (e == hipSuccess) g_configured_devices.push_back(device);
     }
   }
@@ -285,6 +333,8 @@ void np_ctx_destroy(np_ctx* c) {
   c->d_out.release();
   c->d_present.release();
   c->d_loc.release();
+  c->d_big.release();
+  if (c->big_done) (void)hipEventDestroy(c->big_done);
   c->h_in.release();
   c->h_out.release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -343,6 +393,7 @@ int np_encode_batch_dev(np_ctx* c, const np_code_params* p, const uint8_t* d_pay
   if (len == 0) return fail(NP_ERR_PAYLOAD_SIZE_IS_ZERO);
   const size_t sl = np_shard_len(p, len);
   if (!d_payloads || !d_shards || pstride < len || bstride < p->wanted_n * sl) return fail(NP_ERR_INVALID_ARGUMENT);
+  std::lock_guard<std::mutex> g(c->mu);
   (void)hipSetDevice(c->device);
   np::EncodeArgs a = enc_args(p, d_payloads, len, pstride, batch, d_shards, bstride);
   return dev_err(launch_encode(c, a, pick(c, stream)));
@@ -365,9 +416,7 @@ int np_reconstruct_batch_dev2(np_ctx* c, const np_code_params* p, const uint8_t*
   if (shard_len == 0 || (shard_len & 1)) return fail(NP_ERR_EMPTY_SHARD);
   if (!d_shards || !d_present || !d_out || bstride < p->n * shard_len || out_stride < (shard_len / 2) * 2 * p->k)
     return fail(NP_ERR_INVALID_ARGUMENT);
-  std::unique_lock<std::mutex> g(c->mu, std::defer_lock);
-  if (!d_loc && !np::fast_reconstruct_supported(static_cast<uint32_t>(p->n), static_cast<uint32_t>(p->k)))
-    g.lock();  // generic path: locators go to the context scratch
+  std::lock_guard<std::mutex> g(c->mu);  // scratch of the generic / k = 1024 paths
   (void)hipSetDevice(c->device);
   np::ReconstructArgs a{};
   a.shards = d_shards;

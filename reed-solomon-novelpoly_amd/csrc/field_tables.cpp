@@ -89,8 +89,11 @@ void build(HostTables& t) {
   for (uint32_t c = 0; c < kFieldSize; ++c) {
     // v_perm pools: input byte plane P (0 = low byte, 1 = high byte), bit group
     // G (bits 0-2, 3-5, 6-7 of that byte) -> contribution to output byte O.
-    // Layout (dwords): for O in {lo, hi}: [P0G0 lo,hi][P0G1 lo,hi][P0G2][P1G0 lo,hi][P1G1 lo,hi][P1G2]
-    uint32_t* pool = &t.perm_pools[static_cast<size_t>(c) * kPermPoolWords];
+    // Logical order: for O in {lo, hi}: [P0G0 a,b][P0G1 a,b][P0G2][P1G0 a,b][P1G1 a,b][P1G2]
+    // where a = entries 0-3 (v_perm S1, read from a VGPR) and b = entries 4-7
+    // (S0, an SGPR).  Stored as the 8 "a" dwords first (kPoolVWords, staged
+    // in LDS by the kernels) and then the 12 SGPR dwords.
+    uint32_t logical[kPermPoolWords];
     int w = 0;
     for (int out_byte = 0; out_byte < 2; ++out_byte) {
       for (int plane = 0; plane < 2; ++plane) {
@@ -106,15 +109,16 @@ void build(HostTables& t) {
           // v_perm_b32(S0, S1, sel): selector 0..3 -> bytes of S1, 4..7 -> bytes of S0.
           const uint32_t lo = entries[0] | (entries[1] << 8) | (entries[2] << 16) | (uint32_t(entries[3]) << 24);
           const uint32_t hi = entries[4] | (entries[5] << 8) | (entries[6] << 16) | (uint32_t(entries[7]) << 24);
-          if (widths[g] == 3) {
-            pool[w++] = lo;  // goes to S1 (a VGPR)
-            pool[w++] = hi;  // goes to S0 (an SGPR)
-          } else {
-            pool[w++] = lo;  // 4-entry table: S0 == S1
-          }
+          logical[w++] = lo;
+          if (widths[g] == 3) logical[w++] = hi;  // 4-entry tables use S0 == S1
         }
       }
     }
+    static constexpr int kV[8] = {0, 2, 5, 7, 10, 12, 15, 17};
+    static constexpr int kS[12] = {1, 3, 4, 6, 8, 9, 11, 13, 14, 16, 18, 19};
+    uint32_t* pool = &t.perm_pools[static_cast<size_t>(c) * kPermPoolWords];
+    for (int i = 0; i < 8; ++i) pool[i] = logical[kV[i]];
+    for (int i = 0; i < 12; ++i) pool[8 + i] = logical[kS[i]];
   }
 }
 

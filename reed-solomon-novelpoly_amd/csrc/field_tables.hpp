@@ -38,5 +38,6 @@ uint16_t host_mul(const HostTables& t, uint16_t a, uint16_t m);
 uint16_t host_mul_add(const HostTables& t, uint16_t a, uint16_t c);
 
 constexpr int kPermPoolWords = 20;
+constexpr int kPoolVWords = 8;  // VGPR half, stored first
 
 }  // namespace np

@@ -53,10 +53,21 @@ bool fast_reconstruct_supported(uint32_t n, uint32_t k);
 hipError_t launch_encode_fast(const DevTables& T, const EncodeArgs& a, hipStream_t s);
 hipError_t launch_reconstruct_fast(const DevTables& T, const ReconstructArgs& a, hipStream_t s);
 
+// ---- k = 1024 (kernels_big.hip): per-workgroup scratch, launches split to fit it ----
+bool big_encode_supported(uint32_t n, uint32_t k);
+bool big_reconstruct_supported(uint32_t n, uint32_t k);
+size_t big_encode_scratch_per_tile();
+size_t big_reconstruct_scratch_per_tile(uint32_t n);
+hipError_t launch_encode_big(const DevTables& T, const EncodeArgs& a, uint8_t* scratch, size_t scratch_bytes,
+                             hipStream_t s);
+hipError_t launch_reconstruct_big(const DevTables& T, const ReconstructArgs& a, uint8_t* scratch,
+                                  size_t scratch_bytes, hipStream_t s);
+
 }  // namespace np
 
 namespace np {
 // Raises the dynamic-LDS limit of the kernels that need > 64 KiB (call once per device).
 hipError_t configure_generic_kernels();
 hipError_t configure_fast_kernels();
+hipError_t configure_big_kernels();
 }  // namespace np

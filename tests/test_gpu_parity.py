@@ -269,7 +269,9 @@ def test_full_size_batch_properties(gpu, oracle, cid):
 @pytest.mark.parametrize("nw,kw,plen", [(256, 86, 128 * 256), (256, 86, 128 * 300 + 5), (256, 86, 1280),
                                         (512, 100, 128 * 700), (1024, 342, 512 * 256), (1024, 342, 5121),
                                         (1024, 342, 512 * 512 + 77), (300, 100, 77777), (512, 128, 256 * 600),
-                                        (600, 256, 512 * 300), (2048, 300, 512 * 260)])
+                                        (600, 256, 512 * 300), (2048, 300, 512 * 260),
+                                        (4096, 1366, 2048 * 256), (4096, 1366, 2048 * 300 + 3),
+                                        (2048, 1024, 2048 * 100), (3000, 1024, 5000)])
 def test_fast_encode_shapes(gpu, oracle, nw, kw, plen):
     """Specialised encode kernel (k in {64,128,256}): single/multi/partial tiles,
     odd payload tails, wanted_n < n and n/k in {2,4,8}."""
@@ -288,14 +290,16 @@ def test_fast_encode_shapes(gpu, oracle, nw, kw, plen):
                                               (512, 128, 256 * 300, 300), (256, 128, 256 * 256 + 3, 128),
                                               (1024, 342, 512 * 256, 342), (1024, 342, 512 * 300 + 1, 768),
                                               (512, 256, 512 * 257, 256), (1000, 256, 4097, 0),
-                                              (1024, 342, 512 * 256, -1)])
+                                              (1024, 342, 512 * 256, -1), (4096, 1366, 2048 * 256, 2730),
+                                              (4096, 1366, 2048 * 260 + 1, 3072), (2048, 1024, 2048 * 100, 1024),
+                                              (4096, 1366, 2048 * 256, -1), (3000, 1024, 7777, 1000)])
 def test_fast_reconstruct_shapes(gpu, oracle, nw, kw, plen, erase):
     """Specialised reconstruct kernel (k in {64,128,256}, n in {2k,4k}): full and
     partial column tiles, random and worst-case erasure sets (erase = -1: every
     systematic shard lost), bit-exact against the oracle."""
     p = npa.CodeParams.derive_parameters(nw, kw)
     n, k = p.n(), p.k()
-    assert n in (2 * k, 4 * k) and k in (64, 128, 256)
+    assert n in (2 * k, 4 * k) and k in (64, 128, 256, 1024)
     pl = synth.payload(7 * nw + plen, plen)
     shards = p.make_encoder(gpu).encode(pl)
     if erase == -1:
