@@ -441,12 +441,9 @@ size_t rec_big_lds() {
 
 }  // namespace
 
-#ifndef NP_BIG_KERNELS
-#define NP_BIG_KERNELS 0  // enabled once verified on the device
-#endif
-bool big_encode_supported(uint32_t n, uint32_t k) { return NP_BIG_KERNELS && k == kKB && n >= 2 * k && n <= 65536; }
+bool big_encode_supported(uint32_t n, uint32_t k) { return k == kKB && n >= 2 * k && n <= 65536; }
 bool big_reconstruct_supported(uint32_t n, uint32_t k) {
-  return NP_BIG_KERNELS && k == kKB && (n == 2 * k || n == 4 * k);
+  return k == kKB && (n == 2 * k || n == 4 * k);
 }
 size_t big_encode_scratch_per_tile() { return kEncScratch; }
 size_t big_reconstruct_scratch_per_tile(uint32_t n) { return (4u * (n / kKB) + 4u) * kSegScr; }
