@@ -183,7 +183,7 @@ hipError_t launch_encode(np_ctx* c, const np::EncodeArgs& a, hipStream_t s) {
     const size_t tiles = ((a.payload_len + 2 * a.k - 1) / (2 * a.k) + 255) / 256;
     uint8_t* scr = nullptr;
     size_t bytes = 0;
-    hipError_t e = big_scratch(c, a.batch * tiles * np::big_encode_scratch_per_tile(), s, &scr, &bytes);
+    hipError_t e = big_scratch(c, std::max<size_t>(a.batch * tiles, 8) * np::big_encode_scratch_per_tile(), s, &scr, &bytes);
     if (e == hipSuccess) e = np::launch_encode_big(c->T, a, scr, bytes, s);
     return big_done(c, s, e);
   }
@@ -199,7 +199,8 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
     const size_t tiles = (a.shard_len / 2 + 255) / 256;
     uint8_t* scr = nullptr;
     size_t bytes = 0;
-    hipError_t e = big_scratch(c, a.batch * tiles * np::big_reconstruct_scratch_per_tile(a.n), s, &scr, &bytes);
+    hipError_t e = big_scratch(c, std::max<size_t>(a.batch * tiles, 8) * np::big_reconstruct_scratch_per_tile(a.n), s, &scr,
+                                &bytes);
     if (e == hipSuccess) e = np::launch_reconstruct_big(c->T, a, scr, bytes, s);
     return big_done(c, s, e);
   }

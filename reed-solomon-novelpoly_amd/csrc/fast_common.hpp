@@ -34,6 +34,22 @@ struct Geo {
   static constexpr int kVPWords = 8 * K;  // one staged transform: K - 1 slots of 8 dwords (rounded)
 };
 
+// Workgroup -> (batch entry, tile).  Workgroups are handed to the 8 XCDs
+// round-robin (b % 8), so when the batch is a multiple of 8 all tiles of one
+// batch entry go to the same XCD and share its L2 (per-entry data: multiplier
+// tables of the locator values, the EXP gathers, present flags).  Any mapping
+// is correct; this one only buys locality.
+struct TileRef {
+  uint32_t pb, tl;
+};
+__device__ __forceinline__ TileRef tile_of(uint32_t b, uint32_t tiles, bool xcd_major) {
+  if (xcd_major) {
+    const uint32_t slot = b >> 3;
+    return TileRef{(slot / tiles) * 8 + (b & 7u), slot % tiles};
+  }
+  return TileRef{b / tiles, b % tiles};
+}
+
 // ------------------------------------------------------------ LDS tile ----
 // Block (column c, quad m) lives at 8 * (cs * W + ((ci * Q + m) ^ f(cs))) with
 // cs = c / P, ci = c % P and f a linear map of cs found by

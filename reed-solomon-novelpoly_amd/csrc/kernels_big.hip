@@ -77,7 +77,8 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   uint8_t* tile = smem;
   uint32_t* VP = reinterpret_cast<uint32_t*>(smem + G::kTileBytes);
   const uint32_t blk = tile0 + blockIdx.x;
-  const uint32_t pb = blk / tiles, tl = blk - pb * tiles;
+  const TileRef tr = tile_of(blk, tiles, (a.batch & 7u) == 0);
+  const uint32_t pb = tr.pb, tl = tr.tl;
   const uint32_t ch0 = tl * kTile;
   const uint32_t ncols = min(static_cast<uint32_t>(kTile), nchunks - ch0);
   const uint8_t* pay = a.payloads + static_cast<size_t>(pb) * a.payload_stride;
@@ -218,7 +219,8 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   uint16_t* E = reinterpret_cast<uint16_t*>(smem + G::kTileBytes + 4 * G::kVPWords);
   uint8_t* PR = smem + G::kTileBytes + 4 * G::kVPWords + 2 * N;
   const uint32_t blk = tile0 + blockIdx.x;
-  const uint32_t pb = blk / tiles, tl = blk - pb * tiles;
+  const TileRef tr = tile_of(blk, tiles, (a.batch & 7u) == 0);
+  const uint32_t pb = tr.pb, tl = tr.tl;
   const uint32_t col0 = tl * kTile;
   const uint32_t ncols = min(static_cast<uint32_t>(kTile), nsyms - col0);
   const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);
@@ -454,7 +456,7 @@ hipError_t launch_encode_big(const DevTables& T, const EncodeArgs& a, uint8_t* s
   if (nchunks == 0 || a.batch == 0) return hipSuccess;
   const uint32_t tiles = static_cast<uint32_t>((nchunks + kTile - 1) / kTile);
   const size_t total = a.batch * tiles;
-  const size_t per_launch = scratch_bytes / kEncScratch;
+  const size_t per_launch = scratch_bytes / kEncScratch / 8 * 8;  // keeps tile0 % 8 == 0 (tile_of)
   if (per_launch == 0 || total > 0xffffffffu) return hipErrorInvalidValue;
   for (size_t t0 = 0; t0 < total; t0 += per_launch) {
     const uint32_t blocks = static_cast<uint32_t>(std::min(per_launch, total - t0));
@@ -473,7 +475,7 @@ hipError_t launch_reconstruct_big(const DevTables& T, const ReconstructArgs& a, 
   const uint32_t tiles = static_cast<uint32_t>((nsyms + kTile - 1) / kTile);
   const size_t total = a.batch * tiles;
   const size_t per_tile = big_reconstruct_scratch_per_tile(a.n);
-  const size_t per_launch = scratch_bytes / per_tile;
+  const size_t per_launch = scratch_bytes / per_tile / 8 * 8;  // keeps tile0 % 8 == 0 (tile_of)
   if (per_launch == 0 || total > 0xffffffffu) return hipErrorInvalidValue;
   for (size_t t0 = 0; t0 < total; t0 += per_launch) {
     const uint32_t blocks = static_cast<uint32_t>(std::min(per_launch, total - t0));

@@ -41,7 +41,8 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
   uint32_t* VP = reinterpret_cast<uint32_t*>(smem + G::kTileBytes);  // 2 staged transforms
-  const uint32_t pb = blockIdx.x / tiles, tl = blockIdx.x - pb * tiles;
+  const TileRef tr = tile_of(blockIdx.x, tiles, (a.batch & 7u) == 0);
+  const uint32_t pb = tr.pb, tl = tr.tl;
   const uint32_t ch0 = tl * kTile;
   const uint32_t ncols = min(static_cast<uint32_t>(kTile), nchunks - ch0);
   const uint8_t* pay = a.payloads + static_cast<size_t>(pb) * a.payload_stride;
@@ -241,7 +242,8 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
   uint32_t* VP = reinterpret_cast<uint32_t*>(smem + G::kTileBytes);  // 2 staged transforms
   uint16_t* E = reinterpret_cast<uint16_t*>(smem + G::kTileBytes + 8 * G::kVPWords);  // multiplier of every row
   uint8_t* PR = smem + G::kTileBytes + 8 * G::kVPWords + 2 * N;                        // present flags
-  const uint32_t pb = blockIdx.x / tiles, tl = blockIdx.x - pb * tiles;
+  const TileRef tr = tile_of(blockIdx.x, tiles, (a.batch & 7u) == 0);
+  const uint32_t pb = tr.pb, tl = tr.tl;
   const uint32_t col0 = tl * kTile;
   const uint32_t ncols = min(static_cast<uint32_t>(kTile), nsyms - col0);
   const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);

@@ -18,6 +18,7 @@ dst = os.path.join(ROOT, "profiles")
 os.makedirs(dst, exist_ok=True)
 
 KERNELS = {"encode": "k_encode_fast", "reconstruct": "k_reconstruct_fast", "locator": "k_error_locator",
+           "encode_big": "k_encode_big", "reconstruct_big": "k_reconstruct_big",
            "calib_read8": "read8", "calib_copy8": "copy8"}
 
 
@@ -28,8 +29,14 @@ def kind(name):
     return None
 
 
+def newest(pattern):
+    """Latest file of a pass (gpurun merges every call's outputs into gpurun_out/)."""
+    f = sorted(glob.glob(pattern), key=os.path.getmtime)
+    return f[-1:] if f else []
+
+
 def counters(pass_name):
-    f = glob.glob(os.path.join(src, pass_name, "*", "*_counter_collection.csv"))
+    f = newest(os.path.join(src, pass_name, "*", "*_counter_collection.csv"))
     agg = defaultdict(lambda: defaultdict(list))
     if not f:
         return agg
@@ -58,7 +65,7 @@ out["calibration"] = {"read8_FETCH_SIZE_KB": f_read8, "copy8_WRITE_SIZE_KB": w_c
                       "fetch_factor": fetch_factor, "write_factor": write_factor,
                       "note": "factor = known bytes / (counter * 1024) for 8-byte-per-lane coalesced access, "
                               "1 GiB buffers (beyond the 256 MiB Infinity Cache)"}
-for k in ("encode", "reconstruct", "locator"):
+for k in ("encode", "reconstruct", "locator", "encode_big", "reconstruct_big"):
     fs, ws = mean(fetch[k].get("FETCH_SIZE", [])), mean(write[k].get("WRITE_SIZE", []))
     if fs is None or ws is None:
         continue
@@ -68,11 +75,11 @@ for k in ("encode", "reconstruct", "locator"):
                          "traffic_bytes": rd + wr}
 for pname in ("sq", "sq2"):
     c = counters(pname)
-    for k in ("encode", "reconstruct", "locator"):
+    for k in ("encode", "reconstruct", "locator", "encode_big", "reconstruct_big"):
         for name, vals in c[k].items():
             out["kernels"].setdefault(k, {})[name] = mean(vals)
 # kernel-trace averages
-st = glob.glob(os.path.join(src, "stats", "*", "*_kernel_stats.csv"))
+st = newest(os.path.join(src, "stats", "*", "*_kernel_stats.csv"))
 if st:
     for r in csv.DictReader(open(st[0])):
         k = kind(r["Name"])
