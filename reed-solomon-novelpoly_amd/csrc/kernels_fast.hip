@@ -223,71 +223,80 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, uint32_t (&AL)[16]
   }
 }
 
-// One workgroup: 256 symbol columns of one batch entry.  NQ = n / K segments.
-// The inverse transform of size n is NQ inverse transforms of size K (index
-// qK) followed by log2(NQ) top levels whose skews at index 0 are 0 (t = 0) or
+// Decode of one tile from the first NQ segments (NQ * K rows).  The inverse
+// transform of size NQ * K is NQ inverse transforms of size K (index qK)
+// followed by log2(NQ) top levels whose skews at index 0 are 0 (t = 0) or
 // beta = Cantor(2) (t = 1).  Only the first k = K outputs are needed; for them
 //   NQ = 2:  d = D_K(x0) ^ x0 ^ x1
 //   NQ = 4:  d = D_K(x0) ^ x1 ^ x2 ^ beta * (x2 ^ x3)
 // where x_q = IFFT(K, qK)(premultiplied segment q) and D_K is the formal
 // derivative of size K; then out = FFT(K, 0)(d) (the size-n forward transform
 // restricted to its first K outputs is FFT(K, 0): its t = 0 skews are 0).
+// NQ = 1: every systematic row is present, the output is those rows.
+//
+// Decoding from a prefix.  The first NQ * K codeword symbols are the
+// codeword of the same message under the (NQ * K, K) code: the size-n forward
+// transform of the zero-padded coefficients copies its lower half into the
+// upper half at every top level (inc_afft.rs:267-332 with x[i + d] = 0), so its
+// first NQ * K outputs are FFT(NQ * K, 0) of the same coefficients.  A message
+// of K symbols is determined by any K of its codeword symbols, so decoding the
+// prefix with the rows beyond it treated as erased yields the reference's
+// output whenever the prefix holds at least K present rows.
 template <int K, int NQ>
-__global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void k_reconstruct_fast(DevTables T, ReconstructArgs a, uint32_t nsyms,
-                                                            uint32_t tiles) {
+__device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructArgs& a, const uint8_t* sh,
+                                         const uint8_t* pres, const uint16_t* loc, uint8_t* smem, uint32_t pb,
+                                         uint32_t col0, uint32_t ncols, bool full) {
   using G = Geo<K>;
   constexpr int N = NQ * K;
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
   uint32_t* VP = reinterpret_cast<uint32_t*>(smem + G::kTileBytes);  // 2 staged transforms
   uint16_t* E = reinterpret_cast<uint16_t*>(smem + G::kTileBytes + 8 * G::kVPWords);  // multiplier of every row
-  uint8_t* PR = smem + G::kTileBytes + 8 * G::kVPWords + 2 * N;                        // present flags
-  const TileRef tr = tile_of(blockIdx.x, tiles, (a.batch & 7u) == 0);
-  const uint32_t pb = tr.pb, tl = tr.tl;
-  const uint32_t col0 = tl * kTile;
-  const uint32_t ncols = min(static_cast<uint32_t>(kTile), nsyms - col0);
-  const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);
-  const uint8_t* pres = a.present + static_cast<size_t>(pb) * N;
-  const uint16_t* loc = a.locators + static_cast<size_t>(pb) * N;
+  uint8_t* PR = smem + G::kTileBytes + 8 * G::kVPWords + 2 * 4 * K;                    // present flags
   const uint32_t tid = threadIdx.x, lane = tid & 63u, g = uniform(tid >> 6);
-  const bool full =
-      ncols == kTile && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
-
-  if (loc) {
-    for (uint32_t v = tid; v < static_cast<uint32_t>(N); v += G::kThreads) {
-      E[v] = T.exp[loc[v]];  // mul(x, log m) == x * EXP[m] (inc_log_mul.rs:42-49)
-      PR[v] = pres[v];
-    }
-  } else {
-    fused_locator<N, G::kThreads>(T, pres, reinterpret_cast<uint32_t*>(tile), E, PR);
-  }
-  // multiplier tables of the first two segment transforms (indices 2K, 3K or K, 0)
-  stage_vpools<K, G::kThreads>(T, (NQ == 4 ? 2u : 1u) * K, VP);
-  stage_vpools<K, G::kThreads>(T, (NQ == 4 ? 3u : 0u) * K, VP + G::kVPWords);
-  __syncthreads();
-
   const uint32_t cqb = col_base<K>(4 * lane) ^ (32u * g);
-  const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
-  uint32_t AL[16], AH[16];
 
-  // segment order: 2, 3, 1, 0 (NQ = 4) or 1, 0 (NQ = 2)
-  RecCtx c{T, a.shard_len, tile, E, PR, sh, VP, g, lane, tid, ncols, full, cqb, hb};
-  rec_segments<K, NQ>(c, AL, AH);
-  // ---- forward transform of size K at index 0, then postmultiply erased rows
-  const uint32_t* vp0 = VP + ((NQ - 1) & 1) * G::kVPWords;  // segment 0's tables = FFT(K, 0)'s
-  hi_levels<K, false, true>(T, vp0, 0, AL, AH);
-  __syncthreads();
-  hi_write<K>(tile, fresh_v(hb), AL, AH);
-  __syncthreads();
-  {
-    const uint32_t cqbf = fresh_v(cqb);
-    uint32_t XL[16], XH[16];
-    cq_read<K>(tile, cqbf, XL, XH);
+  uint32_t XL[16], XH[16];
+  if constexpr (NQ == 1) {
+    for (uint32_t v = tid; v < static_cast<uint32_t>(K); v += G::kThreads) PR[v] = 1;
+    __syncthreads();
+  } else {
+    if (loc) {
+      for (uint32_t v = tid; v < static_cast<uint32_t>(N); v += G::kThreads) {
+        E[v] = T.exp[loc[v]];  // mul(x, log m) == x * EXP[m] (inc_log_mul.rs:42-49)
+        PR[v] = pres[v];
+      }
+    } else {
+      fused_locator<N, G::kThreads>(T, pres, reinterpret_cast<uint32_t*>(tile), E, PR);
+    }
+    // multiplier tables of the first two segment transforms (indices 2K, 3K or K, 0)
+    stage_vpools<K, G::kThreads>(T, (NQ == 4 ? 2u : 1u) * K, VP);
+    stage_vpools<K, G::kThreads>(T, (NQ == 4 ? 3u : 0u) * K, VP + G::kVPWords);
+    __syncthreads();
+
+    const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
+    uint32_t AL[16], AH[16];
+    // segment order: 2, 3, 1, 0 (NQ = 4) or 1, 0 (NQ = 2)
+    RecCtx c{T, a.shard_len, tile, E, PR, sh, VP, g, lane, tid, ncols, full, cqb, hb};
+    rec_segments<K, NQ>(c, AL, AH);
+    // ---- forward transform of size K at index 0
+    const uint32_t* vp0 = VP + ((NQ - 1) & 1) * G::kVPWords;  // segment 0's tables = FFT(K, 0)'s
+    hi_levels<K, false, true>(T, vp0, 0, AL, AH);
+    __syncthreads();
+    hi_write<K>(tile, fresh_v(hb), AL, AH);
+    __syncthreads();
+    cq_read<K>(tile, fresh_v(cqb), XL, XH);
     cq_levels<K, false, true>(T, vp0, 0, g, XL, XH);
+  }
+  // ---- merge: received systematic rows, postmultiplied recovered ones
+  const uint32_t cqbf = fresh_v(cqb);
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      uint2 raw[8];
-      load_rows<8>(raw, sh, a.shard_len, PR, 16 * g + 8 * half, T.zeros, lane, ncols, full);
+  for (int half = 0; half < 2; ++half) {
+    uint2 raw[8];
+    load_rows<8>(raw, sh, a.shard_len, PR, 16 * g + 8 * half, T.zeros, lane, ncols, full);
+    if constexpr (NQ == 1) {
+#pragma unroll
+      for (int p = 0; p < 8; ++p) blk_to_quad(raw[p], XL[8 * half + p], XH[8 * half + p]);
+    } else {
       pipelined<8>(
           T, [&](auto pc) __attribute__((always_inline)) { return uniform(E[16 * g + 8 * half + decltype(pc)::value]); },
           [&](auto pc, const Mult& pool) __attribute__((always_inline)) {
@@ -303,9 +312,9 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
             }
           });
     }
-    __syncthreads();
-    cq_write<K>(tile, cqbf, XL, XH);
   }
+  __syncthreads();
+  cq_write<K>(tile, cqbf, XL, XH);
   __syncthreads();
   // ---- copy-out: column c of the tile is 2K contiguous bytes of the output
   {
@@ -329,6 +338,41 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
   }
 }
 
+// One workgroup: 256 symbol columns of one batch entry, n = NQ * K.  With the
+// locator computed here (a.locators == nullptr) the workgroup decodes from the
+// shortest prefix of K, 2K or n rows holding K present rows (rec_tile).
+// Precomputed locators are over all n rows, so they pin the full decode.
+template <int K, int NQ>
+__global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void k_reconstruct_fast(DevTables T, ReconstructArgs a, uint32_t nsyms,
+                                                            uint32_t tiles) {
+  constexpr int N = NQ * K;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const TileRef tr = tile_of(blockIdx.x, tiles, (a.batch & 7u) == 0);
+  const uint32_t pb = tr.pb, tl = tr.tl;
+  const uint32_t col0 = tl * kTile;
+  const uint32_t ncols = min(static_cast<uint32_t>(kTile), nsyms - col0);
+  const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);
+  const uint8_t* pres = a.present + static_cast<size_t>(pb) * N;
+  const uint16_t* loc = a.locators ? a.locators + static_cast<size_t>(pb) * N : nullptr;
+  const bool full =
+      ncols == kTile && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
+
+  int nq = NQ;
+  if (!loc) {
+    const uint32_t tid = threadIdx.x;  // 4K threads cover rows [0, 2K) twice over
+    const int have1 = __syncthreads_count(tid < static_cast<uint32_t>(K) && pres[tid] != 0);
+    const int have2 = __syncthreads_count(tid < static_cast<uint32_t>(2 * K) && pres[tid] != 0);
+    nq = have1 == K ? 1 : (NQ == 4 && have2 >= K) ? 2 : NQ;
+  }
+  if (nq == 1) {
+    rec_tile<K, 1>(T, a, sh, pres, loc, smem, pb, col0, ncols, full);
+  } else if (NQ == 4 && nq == 2) {
+    rec_tile<K, 2>(T, a, sh, pres, loc, smem, pb, col0, ncols, full);
+  } else {
+    rec_tile<K, NQ>(T, a, sh, pres, loc, smem, pb, col0, ncols, full);
+  }
+}
+
 // ------------------------------------------------------------- launchers ----
 template <int K>
 size_t encode_lds_bytes() {
@@ -337,7 +381,7 @@ size_t encode_lds_bytes() {
 
 template <int K, int NQ>
 size_t reconstruct_lds_bytes() {
-  return static_cast<size_t>(Geo<K>::kTileBytes) + 2u * 4u * Geo<K>::kVPWords + 3u * NQ * K;
+  return static_cast<size_t>(Geo<K>::kTileBytes) + 2u * 4u * Geo<K>::kVPWords + 3u * 4 * K;
 }
 
 template <int K>

@@ -75,3 +75,15 @@ def present_mask(index: int, n: int, count: int) -> np.ndarray:
     m = np.ones(n, dtype=np.uint8)
     m[erasure_indices(index, n, count)] = 0
     return m
+
+
+def decode_rows(present: np.ndarray, n: int, k: int, fast_nq: tuple = (1, 2, 4)) -> int:
+    """Shard rows the fused-locator reconstruct kernel reads for one payload: it
+    decodes from the shortest prefix of q*k rows (q in ``fast_nq``, q*k <= n)
+    that holds k present rows (kernels_fast.hip, rec_tile), reading only the
+    present rows of that prefix.  Used for the algorithmic byte count."""
+    present = np.asarray(present).astype(bool)
+    for q in fast_nq:
+        if q * k <= n and int(present[: q * k].sum()) >= k:
+            return int(present[: q * k].sum())
+    return int(present[:n].sum())

@@ -348,3 +348,62 @@ def test_device_reconstruct_locator_modes(gpu, oracle, nw, kw, plen, batch):
         for o in outs:
             assert o[b].tobytes() == want, b
         assert want[:plen] == pls[b].tobytes()
+
+
+def _prefix_patterns(n, k, rng):
+    """Erasure patterns that steer the fused-locator reconstruct kernel into each
+    prefix mode: all systematic rows present (decode = copy), at least k present
+    rows in [0, 2k) (2k-row prefix), exactly k there (boundary), fewer (full n)."""
+    pats = []
+    pres = np.ones(n, np.uint8)
+    pres[k + rng.choice(n - k, (n - k) // 2, replace=False)] = 0
+    pats.append(pres)
+    if n >= 2 * k:
+        pres = np.ones(n, np.uint8)
+        pres[rng.choice(k, k // 3, replace=False)] = 0
+        if n > 2 * k:
+            pres[2 * k + rng.choice(n - 2 * k, (n - 2 * k) // 2, replace=False)] = 0
+        pats.append(pres)
+        pres = np.ones(n, np.uint8)
+        pres[rng.choice(2 * k, k, replace=False)] = 0  # exactly k present in the prefix
+        pats.append(pres)
+    if n > 2 * k:
+        pres = np.ones(n, np.uint8)
+        pres[rng.choice(2 * k, k + 1, replace=False)] = 0  # k - 1 present in the prefix
+        pres[2 * k + rng.choice(n - 2 * k, n - 2 * k - 2, replace=False)] = 0  # k + 1 present overall
+        pats.append(pres)
+    return pats
+
+
+@pytest.mark.parametrize("nw,kw,plen", [(1024, 342, 512 * 256), (1024, 342, 512 * 37 + 3), (256, 86, 128 * 256),
+                                        (512, 256, 512 * 256), (256, 128, 256 * 99)])
+def test_reconstruct_prefix_modes(gpu, oracle, nw, kw, plen):
+    """Fast reconstruct with the locator computed in the kernel picks the shortest
+    row prefix (k, 2k or n rows) that holds k present rows; every mode gives the
+    oracle's bytes.  Mixed modes in one batch."""
+    import torch
+
+    p = npa.CodeParams.derive_parameters(nw, kw)
+    n, k = p.n(), p.k()
+    rng = np.random.default_rng(nw * 7 + plen)
+    pats = _prefix_patterns(n, k, rng)
+    batch = len(pats) * 2
+    sl = p.make_encoder(gpu).shard_len(plen)
+    pls = np.stack([np.frombuffer(synth.payload(4000 + b, plen), dtype=np.uint8) for b in range(batch)])
+    dp = dev(pls)
+    ds = torch.empty((batch, n, sl), dtype=torch.uint8, device="cuda")
+    npa.encode_batch_dev(p, dp.data_ptr(), plen, plen, batch, ds.data_ptr(), n * sl, ctx=gpu, stream=stream())
+    pres = np.stack([pats[b % len(pats)] for b in range(batch)])
+    dpres = dev(pres)
+    olen = (sl // 2) * 2 * k
+    out = torch.empty((batch, olen), dtype=torch.uint8, device="cuda")
+    npa.reconstruct_batch_dev2(p, ds.data_ptr(), sl, n * sl, dpres.data_ptr(), 0, batch, out.data_ptr(), olen,
+                               ctx=gpu, stream=stream())
+    o = host(out)
+    hs = host(ds)
+    for b in range(batch):
+        recv = [hs[b, i].tobytes() if pres[b, i] else None for i in range(n)]
+        st, want = oracle.reconstruct(recv, n, k)
+        assert st == 0
+        assert o[b].tobytes() == want, (b, b % len(pats))
+        assert want[:plen] == pls[b].tobytes()
