@@ -99,7 +99,7 @@ struct np_ctx {
   np::DevTables T{};
   std::vector<void*> table_allocs;
   std::mutex mu;  // serialises host-API calls (they share the scratch buffers)
-  DevBuf d_in, d_out, d_present, d_loc;
+  DevBuf d_in, d_out, d_present;
   HostBuf h_in, h_out;
   // Per-workgroup scratch of the k = 1024 kernels (kernels_big.hip).  Launches
   // on different streams are ordered through big_done so they never share it.
@@ -190,11 +190,34 @@ hipError_t launch_encode(np_ctx* c, const np::EncodeArgs& a, hipStream_t s) {
   return np::launch_encode_generic(c->T, a, s);
 }
 
-// a.locators == nullptr: the locators are computed on the device (fused into
-// the fast kernel; a locator launch into the context scratch otherwise, which
-// needs the context lock held by the caller).
+// a.locators == nullptr: the locators are computed on the device, into the
+// ordered context scratch (prefix locators on the fast path, full locators on
+// the generic path; fused into the k = 1024 kernels).  Caller holds the
+// context lock.
 hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream_t s) {
-  if (np::fast_reconstruct_supported(a.n, a.k)) return np::launch_reconstruct_fast(c->T, a, s);
+  if (np::fast_reconstruct_supported(a.n, a.k)) {
+    if (a.locators) return np::launch_reconstruct_fast(c->T, a, s);
+    // per-payload decode prefix + row multipliers, then the decode; batches
+    // larger than the scratch cap go in slices
+    const size_t stride = np::prefix_stride(a.n, a.k);
+    const size_t per = std::max<size_t>(1, kBigScratchCap / stride);
+    for (size_t b0 = 0; b0 < a.batch; b0 += per) {
+      np::ReconstructArgs sub = a;
+      sub.batch = std::min(per, a.batch - b0);
+      sub.shards = a.shards + b0 * a.batch_stride;
+      sub.present = a.present + b0 * a.n;
+      sub.out = a.out + b0 * a.out_stride;
+      uint8_t* scr = nullptr;
+      size_t bytes = 0;
+      hipError_t e = big_scratch(c, sub.batch * stride, s, &scr, &bytes);
+      if (e == hipSuccess) e = np::launch_prefix_locator(c->T, sub, scr, s);
+      sub.prefix = scr;
+      if (e == hipSuccess) e = np::launch_reconstruct_fast(c->T, sub, s);
+      e = big_done(c, s, e);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
   if (np::big_reconstruct_supported(a.n, a.k)) {
     const size_t tiles = (a.shard_len / 2 + 255) / 256;
     uint8_t* scr = nullptr;
@@ -205,12 +228,24 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
     return big_done(c, s, e);
   }
   if (a.locators) return np::launch_reconstruct_generic(c->T, a, s);
-  np::ReconstructArgs b = a;
-  hipError_t e = c->d_loc.ensure(std::max<size_t>(a.batch * a.n * sizeof(uint16_t), 2));
-  if (e == hipSuccess) e = np::launch_error_locator(c->T, a.n, a.present, a.batch, c->d_loc.as<uint16_t>(), s);
-  if (e != hipSuccess) return e;
-  b.locators = c->d_loc.as<uint16_t>();
-  return np::launch_reconstruct_generic(c->T, b, s);
+  // locators into the ordered context scratch, in slices of at most its cap
+  const size_t per = std::max<size_t>(1, kBigScratchCap / (a.n * sizeof(uint16_t)));
+  for (size_t b0 = 0; b0 < a.batch; b0 += per) {
+    np::ReconstructArgs b = a;
+    b.batch = std::min(per, a.batch - b0);
+    b.shards = a.shards + b0 * a.batch_stride;
+    b.present = a.present + b0 * a.n;
+    b.out = a.out + b0 * a.out_stride;
+    uint8_t* scr = nullptr;
+    size_t bytes = 0;
+    hipError_t e = big_scratch(c, b.batch * a.n * sizeof(uint16_t), s, &scr, &bytes);
+    if (e == hipSuccess) e = np::launch_error_locator(c->T, a.n, b.present, b.batch, reinterpret_cast<uint16_t*>(scr), s);
+    b.locators = reinterpret_cast<uint16_t*>(scr);
+    if (e == hipSuccess) e = np::launch_reconstruct_generic(c->T, b, s);
+    e = big_done(c, s, e);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipStream_t pick(np_ctx* c, void* s) { return s ? static_cast<hipStream_t>(s) : c->stream; }
@@ -333,7 +368,6 @@ void np_ctx_destroy(np_ctx* c) {
   c->d_in.release();
   c->d_out.release();
   c->d_present.release();
-  c->d_loc.release();
   c->d_big.release();
   if (c->big_done) (void)hipEventDestroy(c->big_done);
   c->h_in.release();

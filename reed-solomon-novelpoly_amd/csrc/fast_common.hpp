@@ -13,7 +13,23 @@ namespace np {
 namespace {
 
 constexpr int kTile = 256;  // columns per workgroup
+
+// Experiment builds only (tools/exp_variants.sh; the product is built with 0):
+// bit 0 skips the transform levels, bit 1 the shard stores, bit 2 the payload
+// loads, so the phases of a kernel can be timed apart.
+#ifndef NP_EXP
+#define NP_EXP 0
+#endif
+constexpr int kExp = NP_EXP;
 constexpr int kPoolWords = 20;
+
+// Prefix-locator record of one payload (k_prefix_locator): header (byte 0 =
+// prefix segments) then one u16 row multiplier per row of the prefix.
+constexpr uint32_t kPrefixHeader = 16;
+__host__ __device__ constexpr size_t prefix_stride_c(uint32_t n, uint32_t k) {
+  (void)k;
+  return (kPrefixHeader + 2u * static_cast<size_t>(n) + 15u) & ~static_cast<size_t>(15);
+}
 
 __host__ __device__ constexpr int ilog2(int v) {
   int r = 0;
@@ -450,6 +466,7 @@ __host__ __device__ constexpr int hi_groups() {
 template <int K, bool INVERSE, bool INDEX0>
 __device__ __forceinline__ void cq_levels(const DevTables& T, const uint32_t* VP, uint32_t index, uint32_t g,
                                           uint32_t (&L)[16], uint32_t (&H)[16]) {
+  if constexpr (kExp & 1) return;
   auto cval = [&](auto fc) __attribute__((always_inline)) {
     constexpr GroupRef r = cq_group<INVERSE>(decltype(fc)::value);
     return 2u * (g * (8u >> r.b) + r.t) + (index >> r.b);
@@ -484,6 +501,7 @@ __device__ __forceinline__ void cq_levels(const DevTables& T, const uint32_t* VP
 template <int K, bool INVERSE, bool INDEX0>
 __device__ __forceinline__ void hi_levels(const DevTables& T, const uint32_t* VP, uint32_t index, uint32_t (&L)[16],
                                           uint32_t (&H)[16]) {
+  if constexpr (kExp & 1) return;
   constexpr int logR = Geo<K>::kLogR;
   auto cval = [&](auto fc) __attribute__((always_inline)) {
     constexpr GroupRef r = hi_group<K, INVERSE>(decltype(fc)::value);

@@ -61,7 +61,8 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     if (fast) {
       uint2 v[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = *reinterpret_cast<const uint2*>(pay + gbase + static_cast<size_t>(i) * 32 * K);
+      for (int i = 0; i < 16; ++i)
+        v[i] = (kExp & 4) ? make_uint2(i, tid) : *reinterpret_cast<const uint2*>(pay + gbase + static_cast<size_t>(i) * 32 * K);
 #pragma unroll
       for (int i = 0; i < 16; ++i) *reinterpret_cast<uint2*>(tile + (base ^ col_base_c<K>(16u * i))) = v[i];
     } else {
@@ -77,6 +78,7 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     }
   }
   const uint32_t nshift = a.n / K;
+  const uint32_t wanted_store = ((kExp & 2) && a.k != 12345u) ? 0u : a.wanted_n;  // experiment: no stores
   stage_vpools<K, G::kThreads>(T, 0, VP);                              // inverse transform, index 0
   if (nshift > 1) stage_vpools<K, G::kThreads>(T, K, VP + G::kVPWords);  // first shift
   __syncthreads();
@@ -86,7 +88,7 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
   {
     uint32_t CL[16], CH[16];
     cq_read<K>(tile, cqb, CL, CH);
-    store_rows(out, a.shard_len, 16 * g, a.wanted_n, CL, CH, lane, ncols, full);
+    store_rows(out, a.shard_len, 16 * g, wanted_store, CL, CH, lane, ncols, full);
     cq_levels<K, true, true>(T, VP, 0, g, CL, CH);
     cq_write<K>(tile, cqb, CL, CH);
   }
@@ -117,7 +119,7 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     __syncthreads();
     cq_read<K>(tile, fresh_v(cqb), XL, XH);
     cq_levels<K, false, false>(T, vp, index, g, XL, XH);
-    store_rows(out, a.shard_len, index + 16 * g, a.wanted_n, XL, XH, lane, ncols, full);
+    store_rows(out, a.shard_len, index + 16 * g, wanted_store, XL, XH, lane, ncols, full);
   }
 }
 
@@ -127,7 +129,6 @@ struct RecCtx {
   size_t shard_len;
   uint8_t* tile;
   const uint16_t* E;
-  const uint8_t* PR;
   const uint8_t* sh;
   uint32_t* VP;  // 2 staged transforms
   uint32_t g, lane, tid, ncols;
@@ -135,53 +136,113 @@ struct RecCtx {
   uint32_t cqb, hb;
 };
 
-// The segment sweep (segments 2, 3, 1, 0 for NQ = 4; 1, 0 for NQ = 2): x_q =
-// IFFT(K, qK)(premultiplied segment q), folded into A.  A runtime loop keeps the
-// kernel small; at index 0 the t = 0 multipliers are the zero element, whose
-// table yields 0 (the reference's skipped multiply).
+// Segment q of the sweep at step `step` (segments 2, 3, 1, 0 for NQ = 4; 1, 0
+// for NQ = 2).
+template <int NQ>
+__host__ __device__ constexpr int seg_of(int step) {
+  return NQ == 4 ? (step == 0 ? 2 : step == 1 ? 3 : 3 - step) : 1 - step;
+}
+
+// Presence of rows row0..row0+15 as bits (wave-uniform): one byte load per
+// lane and a ballot, so row sources can be chosen before the flags reach LDS.
+__device__ __forceinline__ uint32_t row_mask16(const uint8_t* pres, uint32_t row0, uint32_t lane) {
+  const bool p = lane < 16u && pres[row0 + lane] != 0;
+  return static_cast<uint32_t>(__ballot(p));
+}
+
+// Issues the loads of the lane's pieces of rows row0..row0+15 (absent rows
+// read the zero page: no branch, no HBM traffic); the data is consumed later.
+__device__ __forceinline__ void issue_rows(uint2 (&raw)[16], const uint8_t* sh, size_t shard_len, uint32_t mask,
+                                           uint32_t row0, const uint8_t* zeros, uint32_t lane, uint32_t ncols,
+                                           bool full) {
+  const uint8_t* src[16];
+#pragma unroll
+  for (int p = 0; p < 16; ++p) src[p] = ((mask >> p) & 1u) ? sh + static_cast<size_t>(row0 + p) * shard_len : zeros;
+  if (full) {
+#pragma unroll
+    for (int p = 0; p < 16; ++p) raw[p] = *reinterpret_cast<const uint2*>(src[p] + 8u * lane);
+  } else {
+#pragma unroll
+    for (int p = 0; p < 16; ++p) raw[p] = load4(src[p], lane, ncols, false);
+  }
+}
+
+// Row loads run one step ahead of their use where the registers allow it
+// (prefixes of up to 2 segments); the 4-segment decode, which keeps more
+// state live, loads each step's rows where it uses them.
+template <int NQ>
+constexpr bool kRowPrefetch = NQ <= 2;
+
+// The segment sweep: x_q = IFFT(K, qK)(premultiplied segment q), folded into
+// A.  With kRowPrefetch `raw` holds segment seg_of(0)'s rows on entry and the
+// systematic rows (for the merge) on exit.  A runtime loop keeps
+// the kernel small; at index 0 the t = 0 multipliers are the zero element,
+// whose table yields 0 (the reference's skipped multiply).
 template <int K, int NQ>
-__device__ __forceinline__ void rec_segments(const RecCtx& c, uint32_t (&AL)[16], uint32_t (&AH)[16]) {
+__device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&msk)[NQ], uint2 (&raw)[16],
+                                             uint32_t (&AL)[16], uint32_t (&AH)[16]) {
   const DevTables& T = c.T;
 #pragma unroll 1
   for (int step = 0; step < NQ; ++step) {
-    const int q = NQ == 4 ? (step == 0 ? 2 : step == 1 ? 3 : 3 - step) : 1 - step;
+    const int q = seg_of<NQ>(step);
     const uint32_t index = uniform(static_cast<uint32_t>(q) * K);
     __builtin_amdgcn_sched_barrier(0);
     const uint32_t g = fresh(c.g);
     const uint8_t* sh = fresh(c.sh);
     const uint16_t* E = fresh(c.E);
-    const uint8_t* PR = fresh(c.PR);
     const size_t shard_len = fresh(c.shard_len);
     const uint32_t cqb = fresh_v(c.cqb), hb = fresh_v(c.hb);
-    uint32_t XL[16], XH[16];
+    uint32_t m = msk[0];
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      uint2 raw[8];
-      load_rows<8>(raw, sh, shard_len, PR, index + 16 * g + 8 * half, T.zeros, c.lane, c.ncols, c.full);
-      pipelined<8>(
-          T, [&](auto pc) __attribute__((always_inline)) { return uniform(E[index + 16 * g + 8 * half + decltype(pc)::value]); },
-          [&](auto pc, const Mult& pool) __attribute__((always_inline)) {
-            constexpr int p = decltype(pc)::value;
-            const int x = 8 * half + p;
-            XL[x] = 0;  // absent rows contribute zero
-            XH[x] = 0;
-            if (uniform(PR[index + 16 * g + x])) {
-              uint32_t l, h;
-              blk_to_quad(raw[p], l, h);
+    for (int i = 1; i < NQ; ++i) m = step == i ? msk[i] : m;
+    m = uniform(m);
+    if constexpr (!kRowPrefetch<NQ>)
+      issue_rows(raw, (kExp & 32) ? T.zeros : sh, (kExp & 32) ? 0 : shard_len, m, index + 16 * g, T.zeros, c.lane,
+                 c.ncols, c.full);
+    uint32_t XL[16], XH[16];
+    pipelined<16>(
+        T, [&](auto pc) __attribute__((always_inline)) { return uniform(E[index + 16 * g + decltype(pc)::value]); },
+        [&](auto pc, const Mult& pool) __attribute__((always_inline)) {
+          constexpr int x = decltype(pc)::value;
+          XL[x] = 0;  // absent rows contribute zero
+          XH[x] = 0;
+          if ((m >> x) & 1u) {
+            uint32_t l, h;
+            blk_to_quad(raw[x], l, h);
+            if constexpr (kExp & 16) {  // experiment: no premultiply
+              XL[x] = l;
+              XH[x] = h;
+            } else {
               qmul_set(XL[x], XH[x], l, h, pool);
             }
-          });
-    }
+          }
+        });
     const uint32_t* vp = c.VP + (step & 1) * Geo<K>::kVPWords;
     cq_levels<K, true, false>(T, vp, index, g, XL, XH);
     if (step > 0) {
       __syncthreads();  // the previous high pass is done with the tile and the other table buffer
       if (step + 1 < NQ) {
-        const int qn = NQ == 4 ? (step + 1 == 1 ? 3 : 2 - step) : 0;
+        const int qn = seg_of<NQ>(step + 1);
         stage_vpools<K, Geo<K>::kThreads>(T, static_cast<uint32_t>(qn) * K, c.VP + ((step + 1) & 1) * Geo<K>::kVPWords);
       }
     }
     cq_write<K>(c.tile, cqb, XL, XH);
+    // next step's rows (the systematic rows after the last step) load during
+    // this step's high pass
+    if constexpr (kRowPrefetch<NQ>) {
+      uint32_t mn = msk[0];
+      uint32_t qn = 0;
+#pragma unroll
+      for (int i = 1; i < NQ; ++i) {
+        if (step + 1 == i) {
+          mn = msk[i];
+          qn = static_cast<uint32_t>(seg_of<NQ>(i));
+        }
+      }
+      if (step + 1 == NQ) mn = msk[NQ - 1], qn = 0;  // segment 0 is the last step's
+      issue_rows(raw, (kExp & 32) ? T.zeros : sh, (kExp & 32) ? 0 : shard_len, uniform(mn), uniform(qn) * K + 16 * g,
+                 T.zeros, c.lane, c.ncols, c.full);
+    }
     __syncthreads();
     hi_read<K>(c.tile, hb, XL, XH);
     hi_levels<K, true, false>(T, vp, index, XL, XH);
@@ -244,40 +305,42 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, uint32_t (&AL)[16]
 // output whenever the prefix holds at least K present rows.
 template <int K, int NQ>
 __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructArgs& a, const uint8_t* sh,
-                                         const uint8_t* pres, const uint16_t* loc, uint8_t* smem, uint32_t pb,
-                                         uint32_t col0, uint32_t ncols, bool full) {
+                                         const uint8_t* pres, const uint16_t* loc, const uint16_t* pre_e, uint8_t* smem,
+                                         uint32_t pb, uint32_t col0, uint32_t ncols, bool full) {
   using G = Geo<K>;
   constexpr int N = NQ * K;
   uint8_t* tile = smem;
   uint32_t* VP = reinterpret_cast<uint32_t*>(smem + G::kTileBytes);  // 2 staged transforms
   uint16_t* E = reinterpret_cast<uint16_t*>(smem + G::kTileBytes + 8 * G::kVPWords);  // multiplier of every row
-  uint8_t* PR = smem + G::kTileBytes + 8 * G::kVPWords + 2 * 4 * K;                    // present flags
   const uint32_t tid = threadIdx.x, lane = tid & 63u, g = uniform(tid >> 6);
   const uint32_t cqb = col_base<K>(4 * lane) ^ (32u * g);
 
+  // presence bits of this wave's rows in every segment of the prefix; the
+  // first step's rows start loading before the tables are staged
+  uint32_t msk[NQ];
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) msk[i] = row_mask16(pres, static_cast<uint32_t>(NQ == 1 ? 0 : seg_of<NQ>(i)) * K + 16 * g, lane);
+  uint2 raw[16];
+  if constexpr (kRowPrefetch<NQ>)
+    issue_rows(raw, (NQ > 1 && (kExp & 32)) ? T.zeros : sh, (NQ > 1 && (kExp & 32)) ? 0 : a.shard_len, msk[0],
+               static_cast<uint32_t>(NQ == 1 ? 0 : seg_of<NQ>(0)) * K + 16 * g, T.zeros, lane, ncols, full);
+
   uint32_t XL[16], XH[16];
-  if constexpr (NQ == 1) {
-    for (uint32_t v = tid; v < static_cast<uint32_t>(K); v += G::kThreads) PR[v] = 1;
-    __syncthreads();
-  } else {
-    if (loc) {
-      for (uint32_t v = tid; v < static_cast<uint32_t>(N); v += G::kThreads) {
-        E[v] = T.exp[loc[v]];  // mul(x, log m) == x * EXP[m] (inc_log_mul.rs:42-49)
-        PR[v] = pres[v];
-      }
-    } else {
-      fused_locator<N, G::kThreads>(T, pres, reinterpret_cast<uint32_t*>(tile), E, PR);
+  if constexpr (NQ > 1) {
+    for (uint32_t v = tid; v < static_cast<uint32_t>(N); v += G::kThreads) {
+      // mul(x, log m) == x * EXP[m] (inc_log_mul.rs:42-49); the prefix
+      // locator already holds the multipliers (launch_prefix_locator)
+      E[v] = loc ? T.exp[loc[v]] : pre_e[v];
     }
     // multiplier tables of the first two segment transforms (indices 2K, 3K or K, 0)
-    stage_vpools<K, G::kThreads>(T, (NQ == 4 ? 2u : 1u) * K, VP);
-    stage_vpools<K, G::kThreads>(T, (NQ == 4 ? 3u : 0u) * K, VP + G::kVPWords);
+    stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(0)) * K, VP);
+    stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(1)) * K, VP + G::kVPWords);
     __syncthreads();
 
     const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
     uint32_t AL[16], AH[16];
-    // segment order: 2, 3, 1, 0 (NQ = 4) or 1, 0 (NQ = 2)
-    RecCtx c{T, a.shard_len, tile, E, PR, sh, VP, g, lane, tid, ncols, full, cqb, hb};
-    rec_segments<K, NQ>(c, AL, AH);
+    RecCtx c{T, a.shard_len, tile, E, sh, VP, g, lane, tid, ncols, full, cqb, hb};
+    rec_segments<K, NQ>(c, msk, raw, AL, AH);
     // ---- forward transform of size K at index 0
     const uint32_t* vp0 = VP + ((NQ - 1) & 1) * G::kVPWords;  // segment 0's tables = FFT(K, 0)'s
     hi_levels<K, false, true>(T, vp0, 0, AL, AH);
@@ -289,29 +352,25 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
   }
   // ---- merge: received systematic rows, postmultiplied recovered ones
   const uint32_t cqbf = fresh_v(cqb);
+  const uint32_t m0 = uniform(msk[NQ == 1 ? 0 : NQ - 1]);  // segment 0 = the last step's
+  if constexpr (!kRowPrefetch<NQ>) issue_rows(raw, sh, a.shard_len, m0, 16 * g, T.zeros, lane, ncols, full);
+  if constexpr (NQ == 1) {
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    uint2 raw[8];
-    load_rows<8>(raw, sh, a.shard_len, PR, 16 * g + 8 * half, T.zeros, lane, ncols, full);
-    if constexpr (NQ == 1) {
-#pragma unroll
-      for (int p = 0; p < 8; ++p) blk_to_quad(raw[p], XL[8 * half + p], XH[8 * half + p]);
-    } else {
-      pipelined<8>(
-          T, [&](auto pc) __attribute__((always_inline)) { return uniform(E[16 * g + 8 * half + decltype(pc)::value]); },
-          [&](auto pc, const Mult& pool) __attribute__((always_inline)) {
-            constexpr int p = decltype(pc)::value;
-            const int x = 8 * half + p;
-            // present: the received symbol (mod.rs:225-235); erased: the
-            // postmultiplied recovered symbol (inc_reconstruct.rs:76-84)
-            if (uniform(PR[16 * g + x])) {
-              blk_to_quad(raw[p], XL[x], XH[x]);
-            } else {
-              const uint32_t l = XL[x], h = XH[x];
-              qmul_set(XL[x], XH[x], l, h, pool);
-            }
-          });
-    }
+    for (int p = 0; p < 16; ++p) blk_to_quad(raw[p], XL[p], XH[p]);
+  } else {
+    pipelined<16>(
+        T, [&](auto pc) __attribute__((always_inline)) { return uniform(E[16 * g + decltype(pc)::value]); },
+        [&](auto pc, const Mult& pool) __attribute__((always_inline)) {
+          constexpr int x = decltype(pc)::value;
+          // present: the received symbol (mod.rs:225-235); erased: the
+          // postmultiplied recovered symbol (inc_reconstruct.rs:76-84)
+          if ((m0 >> x) & 1u) {
+            blk_to_quad(raw[x], XL[x], XH[x]);
+          } else {
+            const uint32_t l = XL[x], h = XH[x];
+            qmul_set(XL[x], XH[x], l, h, pool);
+          }
+        });
   }
   __syncthreads();
   cq_write<K>(tile, cqbf, XL, XH);
@@ -338,13 +397,17 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
   }
 }
 
-// One workgroup: 256 symbol columns of one batch entry, n = NQ * K.  With the
-// locator computed here (a.locators == nullptr) the workgroup decodes from the
-// shortest prefix of K, 2K or n rows holding K present rows (rec_tile).
-// Precomputed locators are over all n rows, so they pin the full decode.
-template <int K, int NQ>
-__global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void k_reconstruct_fast(DevTables T, ReconstructArgs a, uint32_t nsyms,
-                                                            uint32_t tiles) {
+// One workgroup: 256 symbol columns of one batch entry, n = NQ * K.  Without
+// caller locators (a.locators == nullptr) the workgroup decodes from the
+// prefix that k_prefix_locator chose (K, 2K or n rows holding K present rows,
+// rec_tile) with its row multipliers.  Caller locators are over all n rows, so
+// they pin the full decode.  An instance serves the payloads whose prefix has
+// at most SERVE segments (SERVE = 2: prefixes of 1 and 2 segments; SERVE = 4:
+// the 4-segment ones only), so each code path gets its own register allocation;
+// for n = 4K the host launches both over the same grid.
+template <int K, int NQ, int SERVE>
+__global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void k_reconstruct_fast(
+    DevTables T, ReconstructArgs a, uint32_t nsyms, uint32_t tiles) {
   constexpr int N = NQ * K;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const TileRef tr = tile_of(blockIdx.x, tiles, (a.batch & 7u) == 0);
@@ -358,18 +421,50 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
       ncols == kTile && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
 
   int nq = NQ;
+  const uint16_t* pre_e = nullptr;
   if (!loc) {
-    const uint32_t tid = threadIdx.x;  // 4K threads cover rows [0, 2K) twice over
-    const int have1 = __syncthreads_count(tid < static_cast<uint32_t>(K) && pres[tid] != 0);
-    const int have2 = __syncthreads_count(tid < static_cast<uint32_t>(2 * K) && pres[tid] != 0);
-    nq = have1 == K ? 1 : (NQ == 4 && have2 >= K) ? 2 : NQ;
+    const uint8_t* rec = a.prefix + static_cast<size_t>(pb) * prefix_stride_c(N, K);
+    nq = uniform(rec[0]);
+    pre_e = reinterpret_cast<const uint16_t*>(rec + kPrefixHeader);
   }
-  if (nq == 1) {
-    rec_tile<K, 1>(T, a, sh, pres, loc, smem, pb, col0, ncols, full);
-  } else if (NQ == 4 && nq == 2) {
-    rec_tile<K, 2>(T, a, sh, pres, loc, smem, pb, col0, ncols, full);
+  if constexpr (SERVE == 4) {
+    if (nq == 4) rec_tile<K, 4>(T, a, sh, pres, loc, pre_e, smem, pb, col0, ncols, full);
+  } else if (nq == 1) {
+    rec_tile<K, 1>(T, a, sh, pres, loc, pre_e, smem, pb, col0, ncols, full);
+  } else if (nq == 2) {
+    rec_tile<K, 2>(T, a, sh, pres, loc, pre_e, smem, pb, col0, ncols, full);
+  }
+}
+
+// ---------------------------------------------------------- prefix locator ----
+// One workgroup per payload: the decode prefix (rec_tile) and the erasure
+// locator folded to it (fused_locator, SURVEY F8: eval_error_polynomial
+// inc_reconstruct.rs:90-113 over [0, NQ' * K)), as row multipliers EXP[loc]
+// (present) / EXP[-loc] (erased).  Record: byte 0 = NQ' in {1, 2, NQ}, u16
+// multipliers from kPrefixHeader.  Computed once per payload instead of once
+// per column tile.
+template <int K, int NQ>
+__global__ __launch_bounds__(256) void k_prefix_locator(DevTables T, ReconstructArgs a, uint8_t* out) {
+  constexpr int N = NQ * K;
+  __shared__ uint32_t W[N];
+  __shared__ uint8_t PR[N];
+  const uint32_t pb = blockIdx.x, tid = threadIdx.x;
+  const uint8_t* pres = a.present + static_cast<size_t>(pb) * N;
+  uint8_t* rec = out + static_cast<size_t>(pb) * prefix_stride_c(N, K);
+  uint16_t* E = reinterpret_cast<uint16_t*>(rec + kPrefixHeader);
+  int have1 = 0, have2 = 0;  // present rows in [0, K) and [0, 2K)
+  for (int r = 0; r < 2 * K; r += 256) {
+    const int v = static_cast<int>(tid) + r;
+    have1 += __syncthreads_count(v < K && pres[v] != 0);
+    have2 += __syncthreads_count(v < 2 * K && pres[v] != 0);
+  }
+  const int nq = have1 == K ? 1 : (NQ == 4 && have2 >= K) ? 2 : NQ;
+  if (tid == 0) rec[0] = static_cast<uint8_t>(nq);
+  if (nq == 1) return;
+  if (NQ == 4 && nq == 2) {
+    fused_locator<2 * K, 256>(T, pres, W, E, PR);
   } else {
-    rec_tile<K, NQ>(T, a, sh, pres, loc, smem, pb, col0, ncols, full);
+    fused_locator<N, 256>(T, pres, W, E, PR);
   }
 }
 
@@ -381,7 +476,7 @@ size_t encode_lds_bytes() {
 
 template <int K, int NQ>
 size_t reconstruct_lds_bytes() {
-  return static_cast<size_t>(Geo<K>::kTileBytes) + 2u * 4u * Geo<K>::kVPWords + 3u * 4 * K;
+  return static_cast<size_t>(Geo<K>::kTileBytes) + 2u * 4u * Geo<K>::kVPWords + 2u * 4 * K;
 }
 
 template <int K>
@@ -397,14 +492,25 @@ hipError_t launch_encode_k(const DevTables& T, const EncodeArgs& a, hipStream_t 
 }
 
 template <int K, int NQ>
+hipError_t launch_prefix_k(const DevTables& T, const ReconstructArgs& a, uint8_t* out, hipStream_t s) {
+  if (a.batch == 0) return hipSuccess;
+  if (a.batch > 0x7fffffffu) return hipErrorInvalidValue;
+  k_prefix_locator<K, NQ><<<static_cast<uint32_t>(a.batch), 256, 0, s>>>(T, a, out);
+  return hipGetLastError();
+}
+
+template <int K, int NQ>
 hipError_t launch_reconstruct_k(const DevTables& T, const ReconstructArgs& a, hipStream_t s) {
   const size_t nsyms = a.shard_len / 2;
   if (nsyms == 0 || a.batch == 0) return hipSuccess;
   const uint32_t tiles = static_cast<uint32_t>((nsyms + kTile - 1) / kTile);
   const size_t blocks = a.batch * tiles;
   if (blocks > 0x7fffffffu || nsyms > 0xffffffffu) return hipErrorInvalidValue;
-  k_reconstruct_fast<K, NQ><<<static_cast<uint32_t>(blocks), Geo<K>::kThreads, reconstruct_lds_bytes<K, NQ>(), s>>>(
+  k_reconstruct_fast<K, NQ, 2><<<static_cast<uint32_t>(blocks), Geo<K>::kThreads, reconstruct_lds_bytes<K, NQ>(), s>>>(
       T, a, static_cast<uint32_t>(nsyms), tiles);
+  if constexpr (NQ == 4)
+    k_reconstruct_fast<K, NQ, 4><<<static_cast<uint32_t>(blocks), Geo<K>::kThreads, reconstruct_lds_bytes<K, NQ>(), s>>>(
+        T, a, static_cast<uint32_t>(nsyms), tiles);
   return hipGetLastError();
 }
 
@@ -423,6 +529,18 @@ hipError_t launch_encode_fast(const DevTables& T, const EncodeArgs& a, hipStream
     case 64: return launch_encode_k<64>(T, a, s);
     case 128: return launch_encode_k<128>(T, a, s);
     case 256: return launch_encode_k<256>(T, a, s);
+    default: return hipErrorNotSupported;
+  }
+}
+
+size_t prefix_stride(uint32_t n, uint32_t k) { return prefix_stride_c(n, k); }
+
+hipError_t launch_prefix_locator(const DevTables& T, const ReconstructArgs& a, uint8_t* out, hipStream_t s) {
+  const bool q4 = a.n == 4 * a.k;
+  switch (a.k) {
+    case 64: return q4 ? launch_prefix_k<64, 4>(T, a, out, s) : launch_prefix_k<64, 2>(T, a, out, s);
+    case 128: return q4 ? launch_prefix_k<128, 4>(T, a, out, s) : launch_prefix_k<128, 2>(T, a, out, s);
+    case 256: return q4 ? launch_prefix_k<256, 4>(T, a, out, s) : launch_prefix_k<256, 2>(T, a, out, s);
     default: return hipErrorNotSupported;
   }
 }
@@ -446,12 +564,15 @@ hipError_t configure_fast_kernels() {
   set(reinterpret_cast<const void*>(&k_encode_fast<64>), encode_lds_bytes<64>());
   set(reinterpret_cast<const void*>(&k_encode_fast<128>), encode_lds_bytes<128>());
   set(reinterpret_cast<const void*>(&k_encode_fast<256>), encode_lds_bytes<256>());
-  set(reinterpret_cast<const void*>(&k_reconstruct_fast<64, 2>), reconstruct_lds_bytes<64, 2>());
-  set(reinterpret_cast<const void*>(&k_reconstruct_fast<64, 4>), reconstruct_lds_bytes<64, 4>());
-  set(reinterpret_cast<const void*>(&k_reconstruct_fast<128, 2>), reconstruct_lds_bytes<128, 2>());
-  set(reinterpret_cast<const void*>(&k_reconstruct_fast<128, 4>), reconstruct_lds_bytes<128, 4>());
-  set(reinterpret_cast<const void*>(&k_reconstruct_fast<256, 2>), reconstruct_lds_bytes<256, 2>());
-  set(reinterpret_cast<const void*>(&k_reconstruct_fast<256, 4>), reconstruct_lds_bytes<256, 4>());
+  set(reinterpret_cast<const void*>(&k_reconstruct_fast<64, 2, 2>), reconstruct_lds_bytes<64, 2>());
+  set(reinterpret_cast<const void*>(&k_reconstruct_fast<64, 4, 2>), reconstruct_lds_bytes<64, 4>());
+  set(reinterpret_cast<const void*>(&k_reconstruct_fast<64, 4, 4>), reconstruct_lds_bytes<64, 4>());
+  set(reinterpret_cast<const void*>(&k_reconstruct_fast<128, 2, 2>), reconstruct_lds_bytes<128, 2>());
+  set(reinterpret_cast<const void*>(&k_reconstruct_fast<128, 4, 2>), reconstruct_lds_bytes<128, 4>());
+  set(reinterpret_cast<const void*>(&k_reconstruct_fast<128, 4, 4>), reconstruct_lds_bytes<128, 4>());
+  set(reinterpret_cast<const void*>(&k_reconstruct_fast<256, 2, 2>), reconstruct_lds_bytes<256, 2>());
+  set(reinterpret_cast<const void*>(&k_reconstruct_fast<256, 4, 2>), reconstruct_lds_bytes<256, 4>());
+  set(reinterpret_cast<const void*>(&k_reconstruct_fast<256, 4, 4>), reconstruct_lds_bytes<256, 4>());
   return e;
 }
 

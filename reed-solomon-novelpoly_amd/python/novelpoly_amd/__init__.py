@@ -22,7 +22,8 @@ from typing import List, Optional, Sequence
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.abspath(os.path.join(_HERE, "..", ".."))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libnovelpoly_hip.so")
+# NP_LIB_PATH: an experiment build of the same library (tools/exp_variants.sh)
+LIB_PATH = os.environ.get("NP_LIB_PATH") or os.path.join(PKG_ROOT, "lib", "libnovelpoly_hip.so")
 FIELD_SIZE = 65536
 
 _sz = C.c_size_t

@@ -1,0 +1,196 @@
+// Microbenchmark: issue throughput of single VALU instructions on gfx950 at 4
+// and 8 waves per SIMD (8 independent register chains, wall clock over
+// ITERS x 8 instructions).  Used to price the GF(2^16) multiply designs
+// (DESIGN.md).  Not product code.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
+constexpr int ITERS = 8192;
+__global__ __launch_bounds__(1024) void k_perm_svv(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_perm_b32 %0, %8, %1, %0\n\tv_perm_b32 %1, %8, %2, %1\n\tv_perm_b32 %2, %8, %3, %2\n\tv_perm_b32 %3, %8, %4, %3\n\tv_perm_b32 %4, %8, %5, %4\n\tv_perm_b32 %5, %8, %6, %5\n\tv_perm_b32 %6, %8, %7, %6\n\tv_perm_b32 %7, %8, %0, %7" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_perm_vvv(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_perm_b32 %0, %2, %1, %0\n\tv_perm_b32 %1, %3, %2, %1\n\tv_perm_b32 %2, %4, %3, %2\n\tv_perm_b32 %3, %5, %4, %3\n\tv_perm_b32 %4, %6, %5, %4\n\tv_perm_b32 %5, %7, %6, %5\n\tv_perm_b32 %6, %0, %7, %6\n\tv_perm_b32 %7, %1, %0, %7" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_bitop3_vvv(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_bitop3_b32 %0, %1, %2, %0 bitop3:0x96\n\tv_bitop3_b32 %1, %2, %3, %1 bitop3:0x96\n\tv_bitop3_b32 %2, %3, %4, %2 bitop3:0x96\n\tv_bitop3_b32 %3, %4, %5, %3 bitop3:0x96\n\tv_bitop3_b32 %4, %5, %6, %4 bitop3:0x96\n\tv_bitop3_b32 %5, %6, %7, %5 bitop3:0x96\n\tv_bitop3_b32 %6, %7, %0, %6 bitop3:0x96\n\tv_bitop3_b32 %7, %0, %1, %7 bitop3:0x96" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_bitop3_svv(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_bitop3_b32 %0, %8, %1, %0 bitop3:0x96\n\tv_bitop3_b32 %1, %8, %2, %1 bitop3:0x96\n\tv_bitop3_b32 %2, %8, %3, %2 bitop3:0x96\n\tv_bitop3_b32 %3, %8, %4, %3 bitop3:0x96\n\tv_bitop3_b32 %4, %8, %5, %4 bitop3:0x96\n\tv_bitop3_b32 %5, %8, %6, %5 bitop3:0x96\n\tv_bitop3_b32 %6, %8, %7, %6 bitop3:0x96\n\tv_bitop3_b32 %7, %8, %0, %7 bitop3:0x96" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_and_lit_vop2(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_and_b32 %0, 0x07070707, %1\n\tv_and_b32 %1, 0x07070707, %2\n\tv_and_b32 %2, 0x07070707, %3\n\tv_and_b32 %3, 0x07070707, %4\n\tv_and_b32 %4, 0x07070707, %5\n\tv_and_b32 %5, 0x07070707, %6\n\tv_and_b32 %6, 0x07070707, %7\n\tv_and_b32 %7, 0x07070707, %0" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_and_sgpr_vop2(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_and_b32_e32 %0, %8, %1\n\tv_and_b32_e32 %1, %8, %2\n\tv_and_b32_e32 %2, %8, %3\n\tv_and_b32_e32 %3, %8, %4\n\tv_and_b32_e32 %4, %8, %5\n\tv_and_b32_e32 %5, %8, %6\n\tv_and_b32_e32 %6, %8, %7\n\tv_and_b32_e32 %7, %8, %0" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_and_sgpr_vop3(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_and_b32_e64 %0, %8, %1\n\tv_and_b32_e64 %1, %8, %2\n\tv_and_b32_e64 %2, %8, %3\n\tv_and_b32_e64 %3, %8, %4\n\tv_and_b32_e64 %4, %8, %5\n\tv_and_b32_e64 %5, %8, %6\n\tv_and_b32_e64 %6, %8, %7\n\tv_and_b32_e64 %7, %8, %0" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_and_vvv_vop3(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_and_b32_e64 %0, %2, %1\n\tv_and_b32_e64 %1, %3, %2\n\tv_and_b32_e64 %2, %4, %3\n\tv_and_b32_e64 %3, %5, %4\n\tv_and_b32_e64 %4, %6, %5\n\tv_and_b32_e64 %5, %7, %6\n\tv_and_b32_e64 %6, %0, %7\n\tv_and_b32_e64 %7, %1, %0" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_xor_vop2(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_xor_b32 %0, %1, %0\n\tv_xor_b32 %1, %2, %1\n\tv_xor_b32 %2, %3, %2\n\tv_xor_b32 %3, %4, %3\n\tv_xor_b32 %4, %5, %4\n\tv_xor_b32 %5, %6, %5\n\tv_xor_b32 %6, %7, %6\n\tv_xor_b32 %7, %0, %7" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_lshr_vop2(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_lshrrev_b32 %0, 3, %1\n\tv_lshrrev_b32 %1, 3, %2\n\tv_lshrrev_b32 %2, 3, %3\n\tv_lshrrev_b32 %3, 3, %4\n\tv_lshrrev_b32 %4, 3, %5\n\tv_lshrrev_b32 %5, 3, %6\n\tv_lshrrev_b32 %6, 3, %7\n\tv_lshrrev_b32 %7, 3, %0" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_lshr_vop3(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_lshrrev_b32_e64 %0, 3, %1\n\tv_lshrrev_b32_e64 %1, 3, %2\n\tv_lshrrev_b32_e64 %2, 3, %3\n\tv_lshrrev_b32_e64 %3, 3, %4\n\tv_lshrrev_b32_e64 %4, 3, %5\n\tv_lshrrev_b32_e64 %5, 3, %6\n\tv_lshrrev_b32_e64 %6, 3, %7\n\tv_lshrrev_b32_e64 %7, 3, %0" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_and_or(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_and_or_b32 %0, %1, %2, %0\n\tv_and_or_b32 %1, %2, %3, %1\n\tv_and_or_b32 %2, %3, %4, %2\n\tv_and_or_b32 %3, %4, %5, %3\n\tv_and_or_b32 %4, %5, %6, %4\n\tv_and_or_b32 %5, %6, %7, %5\n\tv_and_or_b32 %6, %7, %0, %6\n\tv_and_or_b32 %7, %0, %1, %7" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_bfi(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_bfi_b32 %0, %1, %2, %0\n\tv_bfi_b32 %1, %2, %3, %1\n\tv_bfi_b32 %2, %3, %4, %2\n\tv_bfi_b32 %3, %4, %5, %3\n\tv_bfi_b32 %4, %5, %6, %4\n\tv_bfi_b32 %5, %6, %7, %5\n\tv_bfi_b32 %6, %7, %0, %6\n\tv_bfi_b32 %7, %0, %1, %7" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_lshl_or(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_lshl_or_b32 %0, %1, 3, %0\n\tv_lshl_or_b32 %1, %2, 3, %1\n\tv_lshl_or_b32 %2, %3, 3, %2\n\tv_lshl_or_b32 %3, %4, 3, %3\n\tv_lshl_or_b32 %4, %5, 3, %4\n\tv_lshl_or_b32 %5, %6, 3, %5\n\tv_lshl_or_b32 %6, %7, 3, %6\n\tv_lshl_or_b32 %7, %0, 3, %7" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_cndmask_vcc(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_cndmask_b32 %0, %1, %2, vcc\n\tv_cndmask_b32 %1, %2, %3, vcc\n\tv_cndmask_b32 %2, %3, %4, vcc\n\tv_cndmask_b32 %3, %4, %5, vcc\n\tv_cndmask_b32 %4, %5, %6, vcc\n\tv_cndmask_b32 %5, %6, %7, vcc\n\tv_cndmask_b32 %6, %7, %0, vcc\n\tv_cndmask_b32 %7, %0, %1, vcc" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_mov_dpp(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\tv_mov_b32_dpp %1, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\tv_mov_b32_dpp %2, %3 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\tv_mov_b32_dpp %3, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\tv_mov_b32_dpp %4, %5 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\tv_mov_b32_dpp %5, %6 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\tv_mov_b32_dpp %6, %7 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\tv_mov_b32_dpp %7, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_alignbit(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_alignbit_b32 %0, %1, %2, 3\n\tv_alignbit_b32 %1, %2, %3, 3\n\tv_alignbit_b32 %2, %3, %4, 3\n\tv_alignbit_b32 %3, %4, %5, 3\n\tv_alignbit_b32 %4, %5, %6, 3\n\tv_alignbit_b32 %5, %6, %7, 3\n\tv_alignbit_b32 %6, %7, %0, 3\n\tv_alignbit_b32 %7, %0, %1, 3" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_bfe(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_bfe_u32 %0, %1, 3, 3\n\tv_bfe_u32 %1, %2, 3, 3\n\tv_bfe_u32 %2, %3, 3, 3\n\tv_bfe_u32 %3, %4, 3, 3\n\tv_bfe_u32 %4, %5, 3, 3\n\tv_bfe_u32 %5, %6, 3, 3\n\tv_bfe_u32 %6, %7, 3, 3\n\tv_bfe_u32 %7, %0, 3, 3" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_mov_b32(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_mov_b32 %0, %1\n\tv_mov_b32 %1, %2\n\tv_mov_b32 %2, %3\n\tv_mov_b32 %3, %4\n\tv_mov_b32 %4, %5\n\tv_mov_b32 %5, %6\n\tv_mov_b32 %6, %7\n\tv_mov_b32 %7, %0" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+
+template <typename F>
+int run(const char* name, F kern, int cus, uint32_t* out) {
+  printf("%-16s", name);
+  for (int per_cu : {1, 2}) {  // 1024-thread blocks: 4 or 8 waves per SIMD
+    kern<<<cus * per_cu, 1024>>>(out, 7);
+    CK(hipDeviceSynchronize());
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    float best = 1e9;
+    for (int r = 0; r < 3; ++r) {
+      CK(hipEventRecord(e0));
+      kern<<<cus * per_cu, 1024>>>(out, 7);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      if (ms < best) best = ms;
+    }
+    const double per_simd = 4.0 * per_cu * ITERS * 8;  // wave-instructions per SIMD
+    printf("   %d w/SIMD: %.2f cyc@2.4GHz", 4 * per_cu, best * 1e6 / per_simd * 2.4);
+  }
+  printf("\n");
+  return 0;
+}
+
+int main() {
+  hipDeviceProp_t p;
+  CK(hipGetDeviceProperties(&p, 0));
+  const int cus = p.multiProcessorCount;
+  uint32_t* out;
+  CK(hipMalloc(&out, sizeof(uint32_t) * 2048 * cus));
+  run("perm_svv", k_perm_svv, cus, out);
+  run("perm_vvv", k_perm_vvv, cus, out);
+  run("bitop3_vvv", k_bitop3_vvv, cus, out);
+  run("bitop3_svv", k_bitop3_svv, cus, out);
+  run("and_lit_vop2", k_and_lit_vop2, cus, out);
+  run("and_sgpr_vop2", k_and_sgpr_vop2, cus, out);
+  run("and_sgpr_vop3", k_and_sgpr_vop3, cus, out);
+  run("and_vvv_vop3", k_and_vvv_vop3, cus, out);
+  run("xor_vop2", k_xor_vop2, cus, out);
+  run("lshr_vop2", k_lshr_vop2, cus, out);
+  run("lshr_vop3", k_lshr_vop3, cus, out);
+  run("and_or", k_and_or, cus, out);
+  run("bfi", k_bfi, cus, out);
+  run("lshl_or", k_lshl_or, cus, out);
+  run("cndmask_vcc", k_cndmask_vcc, cus, out);
+  run("mov_dpp", k_mov_dpp, cus, out);
+  run("alignbit", k_alignbit, cus, out);
+  run("bfe", k_bfe, cus, out);
+  run("mov_b32", k_mov_b32, cus, out);
+  return 0;
+}
