@@ -21,6 +21,14 @@ constexpr int kTile = 256;  // columns per workgroup
 #define NP_EXP 0
 #endif
 constexpr int kExp = NP_EXP;
+
+// Experiment builds with NP_EXP bit 6: thread 0 of a workgroup writes
+// s_memtime stamps at phase boundaries to `dbg` (tools/phase_stamps.py).
+__device__ __forceinline__ void stamp(uint64_t* dbg, int slot) {
+  if constexpr (kExp & 64) {
+    if (threadIdx.x == 0) dbg[slot] = __builtin_amdgcn_s_memtime();
+  }
+}
 constexpr int kPoolWords = 20;
 
 // Prefix-locator record of one payload (k_prefix_locator): header (byte 0 =

@@ -134,6 +134,7 @@ struct RecCtx {
   uint32_t g, lane, tid, ncols;
   bool full;
   uint32_t cqb, hb;
+  uint64_t* dbg;  // experiment builds only (stamp)
 };
 
 // Segment q of the sweep at step `step` (segments 2, 3, 1, 0 for NQ = 4; 1, 0
@@ -200,6 +201,7 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
       issue_rows(raw, (kExp & 32) ? T.zeros : sh, (kExp & 32) ? 0 : shard_len, m, index + 16 * g, T.zeros, c.lane,
                  c.ncols, c.full);
     uint32_t XL[16], XH[16];
+    stamp(c.dbg, 2 + 6 * step);
     pipelined<16>(
         T, [&](auto pc) __attribute__((always_inline)) { return uniform(E[index + 16 * g + decltype(pc)::value]); },
         [&](auto pc, const Mult& pool) __attribute__((always_inline)) {
@@ -218,7 +220,9 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
           }
         });
     const uint32_t* vp = c.VP + (step & 1) * Geo<K>::kVPWords;
+    stamp(c.dbg, 3 + 6 * step);
     cq_levels<K, true, false>(T, vp, index, g, XL, XH);
+    stamp(c.dbg, 4 + 6 * step);
     if (step > 0) {
       __syncthreads();  // the previous high pass is done with the tile and the other table buffer
       if (step + 1 < NQ) {
@@ -244,8 +248,10 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
                  T.zeros, c.lane, c.ncols, c.full);
     }
     __syncthreads();
+    stamp(c.dbg, 5 + 6 * step);
     hi_read<K>(c.tile, hb, XL, XH);
     hi_levels<K, true, false>(T, vp, index, XL, XH);
+    stamp(c.dbg, 6 + 6 * step);
     __builtin_amdgcn_sched_barrier(0);
     if (step == 0) {
 #pragma unroll
@@ -306,7 +312,7 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
 template <int K, int NQ>
 __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructArgs& a, const uint8_t* sh,
                                          const uint8_t* pres, const uint16_t* loc, const uint16_t* pre_e, uint8_t* smem,
-                                         uint32_t pb, uint32_t col0, uint32_t ncols, bool full) {
+                                         uint32_t pb, uint32_t col0, uint32_t ncols, bool full, uint64_t* dbg) {
   using G = Geo<K>;
   constexpr int N = NQ * K;
   uint8_t* tile = smem;
@@ -317,6 +323,7 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
 
   // presence bits of this wave's rows in every segment of the prefix; the
   // first step's rows start loading before the tables are staged
+  stamp(dbg, 0);
   uint32_t msk[NQ];
 #pragma unroll
   for (int i = 0; i < NQ; ++i) msk[i] = row_mask16(pres, static_cast<uint32_t>(NQ == 1 ? 0 : seg_of<NQ>(i)) * K + 16 * g, lane);
@@ -336,19 +343,24 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
     stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(0)) * K, VP);
     stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(1)) * K, VP + G::kVPWords);
     __syncthreads();
+    stamp(dbg, 1);
 
     const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
     uint32_t AL[16], AH[16];
-    RecCtx c{T, a.shard_len, tile, E, sh, VP, g, lane, tid, ncols, full, cqb, hb};
+    RecCtx c{T, a.shard_len, tile, E, sh, VP, g, lane, tid, ncols, full, cqb, hb, dbg};
     rec_segments<K, NQ>(c, msk, raw, AL, AH);
     // ---- forward transform of size K at index 0
     const uint32_t* vp0 = VP + ((NQ - 1) & 1) * G::kVPWords;  // segment 0's tables = FFT(K, 0)'s
+    stamp(dbg, 26);
     hi_levels<K, false, true>(T, vp0, 0, AL, AH);
+    stamp(dbg, 27);
     __syncthreads();
     hi_write<K>(tile, fresh_v(hb), AL, AH);
     __syncthreads();
+    stamp(dbg, 28);
     cq_read<K>(tile, fresh_v(cqb), XL, XH);
     cq_levels<K, false, true>(T, vp0, 0, g, XL, XH);
+    stamp(dbg, 29);
   }
   // ---- merge: received systematic rows, postmultiplied recovered ones
   const uint32_t cqbf = fresh_v(cqb);
@@ -372,6 +384,7 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
           }
         });
   }
+  stamp(dbg, 30);
   __syncthreads();
   cq_write<K>(tile, cqbf, XL, XH);
   __syncthreads();
@@ -395,6 +408,7 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
       }
     }
   }
+  stamp(dbg, 31);
 }
 
 // One workgroup: 256 symbol columns of one batch entry, n = NQ * K.  Without
@@ -427,12 +441,15 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     nq = uniform(rec[0]);
     pre_e = reinterpret_cast<const uint16_t*>(rec + kPrefixHeader);
   }
+  uint64_t* dbg = (kExp & 64) ? reinterpret_cast<uint64_t*>(a.out + static_cast<size_t>(pb) * a.out_stride +
+                                                             static_cast<size_t>(nsyms) * 2 * K + 256u * tl)
+                               : nullptr;
   if constexpr (SERVE == 4) {
-    if (nq == 4) rec_tile<K, 4>(T, a, sh, pres, loc, pre_e, smem, pb, col0, ncols, full);
+    if (nq == 4) rec_tile<K, 4>(T, a, sh, pres, loc, pre_e, smem, pb, col0, ncols, full, dbg);
   } else if (nq == 1) {
-    rec_tile<K, 1>(T, a, sh, pres, loc, pre_e, smem, pb, col0, ncols, full);
+    rec_tile<K, 1>(T, a, sh, pres, loc, pre_e, smem, pb, col0, ncols, full, dbg);
   } else if (nq == 2) {
-    rec_tile<K, 2>(T, a, sh, pres, loc, pre_e, smem, pb, col0, ncols, full);
+    rec_tile<K, 2>(T, a, sh, pres, loc, pre_e, smem, pb, col0, ncols, full, dbg);
   }
 }
 
@@ -473,6 +490,7 @@ template <int K>
 size_t encode_lds_bytes() {
   return static_cast<size_t>(Geo<K>::kTileBytes) + 2u * 4u * Geo<K>::kVPWords;
 }
+
 
 template <int K, int NQ>
 size_t reconstruct_lds_bytes() {

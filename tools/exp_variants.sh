@@ -5,7 +5,7 @@
 set -e
 cd "$(dirname "$0")/.."
 if [ "$1" != "--run" ]; then
-  for b in 1 2 3 4 6 8 16 32 56 57; do
+  for b in ${BITS:-1 2 3 4 6 8 16 32 56 57 64}; do
     make -s -j8 -C reed-solomon-novelpoly_amd OUT=$PWD/tools/exp/lib_$b.so OBJDIR=$PWD/tools/exp/build_$b EXTRA=-DNP_EXP=$b 2>&1 | grep -i error || true
   done
   exit 0
