@@ -119,22 +119,24 @@ __device__ __forceinline__ uint32_t vperm(uint32_t s0, uint32_t s1, uint32_t sel
 }
 
 // Byte-table selectors of four byte-planar symbols: bits 0-2, 3-5, 6-7 of
-// every byte of the low plane (s[0..2]) and of the high plane (s[3..5]).  One
-// asm block, so the extraction of a whole level is not hoisted ahead of use.
+// every byte of the low plane (s[0..2]) and of the high plane (s[3..5]).  The
+// two planes shift as one 64-bit value: the bits the high plane shifts into
+// the low plane's top byte land above each byte's mask.  One asm block, so the
+// extraction of a whole level is not hoisted ahead of use.
 __device__ __forceinline__ void selectors(uint32_t yl, uint32_t yh, uint32_t (&s)[6]) {
+  const uint64_t y = (static_cast<uint64_t>(yh) << 32) | yl;
+  uint64_t t3, t6;
+  asm volatile("v_lshrrev_b64 %0, 3, %2\n\tv_lshrrev_b64 %1, 6, %2" : "=&v"(t3), "=&v"(t6) : "v"(y));
   asm volatile(
       "v_and_b32 %0, 0x07070707, %6\n\t"
-      "v_lshrrev_b32 %1, 3, %6\n\t"
-      "v_lshrrev_b32 %2, 6, %6\n\t"
       "v_and_b32 %3, 0x07070707, %7\n\t"
-      "v_lshrrev_b32 %4, 3, %7\n\t"
-      "v_lshrrev_b32 %5, 6, %7\n\t"
-      "v_and_b32 %1, 0x07070707, %1\n\t"
-      "v_and_b32 %2, 0x03030303, %2\n\t"
-      "v_and_b32 %4, 0x07070707, %4\n\t"
-      "v_and_b32 %5, 0x03030303, %5"
+      "v_and_b32 %1, 0x07070707, %8\n\t"
+      "v_and_b32 %4, 0x07070707, %9\n\t"
+      "v_and_b32 %2, 0x03030303, %10\n\t"
+      "v_and_b32 %5, 0x03030303, %11"
       : "=&v"(s[0]), "=&v"(s[1]), "=&v"(s[2]), "=&v"(s[3]), "=&v"(s[4]), "=&v"(s[5])
-      : "v"(yl), "v"(yh));
+      : "v"(yl), "v"(yh), "v"(static_cast<uint32_t>(t3)), "v"(static_cast<uint32_t>(t3 >> 32)),
+        "v"(static_cast<uint32_t>(t6)), "v"(static_cast<uint32_t>(t6 >> 32)));
 }
 
 // One output byte plane of c*y: acc ^= XOR of the 6 table lookups (tables

@@ -141,6 +141,120 @@ __global__ __launch_bounds__(1024) void k_mov_b32(uint32_t* out, uint32_t seed) 
   out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
 }
 
+__global__ __launch_bounds__(1024) void k_mix_perm_and_1_1(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_perm_b32 %0, %8, %1, %0\n\tv_and_b32 %1, 0x07070707, %2\n\tv_perm_b32 %2, %8, %3, %2\n\tv_and_b32 %3, 0x07070707, %4\n\tv_perm_b32 %4, %8, %5, %4\n\tv_and_b32 %5, 0x07070707, %6\n\tv_perm_b32 %6, %8, %7, %6\n\tv_and_b32 %7, 0x07070707, %0" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_mix_perm_and_1_2(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_perm_b32 %0, %8, %1, %0\n\tv_and_b32 %1, 0x07070707, %2\n\tv_xor_b32 %2, %3, %2\n\tv_perm_b32 %3, %8, %4, %3\n\tv_and_b32 %4, 0x07070707, %5\n\tv_xor_b32 %5, %6, %5\n\tv_perm_b32 %6, %8, %7, %6\n\tv_and_b32 %7, 0x07070707, %0" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_mix_perm_bitop3_1_1(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_perm_b32 %0, %8, %1, %0\n\tv_bitop3_b32 %1, %2, %3, %1 bitop3:0x96\n\tv_perm_b32 %2, %8, %3, %2\n\tv_bitop3_b32 %3, %4, %5, %3 bitop3:0x96\n\tv_perm_b32 %4, %8, %5, %4\n\tv_bitop3_b32 %5, %6, %7, %5 bitop3:0x96\n\tv_perm_b32 %6, %8, %7, %6\n\tv_bitop3_b32 %7, %0, %1, %7 bitop3:0x96" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_mix_permvvv_and_1_1(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_perm_b32 %0, %2, %1, %0\n\tv_and_b32 %1, 0x07070707, %2\n\tv_perm_b32 %2, %4, %3, %2\n\tv_and_b32 %3, 0x07070707, %4\n\tv_perm_b32 %4, %6, %5, %4\n\tv_and_b32 %5, 0x07070707, %6\n\tv_perm_b32 %6, %0, %7, %6\n\tv_and_b32 %7, 0x07070707, %0" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_mix_and_xor(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_and_b32 %0, 0x07070707, %1\n\tv_xor_b32 %1, %2, %1\n\tv_and_b32 %2, 0x07070707, %3\n\tv_xor_b32 %3, %4, %3\n\tv_and_b32 %4, 0x07070707, %5\n\tv_xor_b32 %5, %6, %5\n\tv_and_b32 %6, 0x07070707, %7\n\tv_xor_b32 %7, %0, %7" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+
+__device__ __forceinline__ void qm(uint32_t& xl, uint32_t& xh, uint32_t yl, uint32_t yh, uint32_t va, uint32_t vb,
+                                   uint32_t vc, uint32_t vd, uint32_t ve, uint32_t vf, uint32_t vg, uint32_t vh,
+                                   uint32_t s0, uint32_t s1, uint32_t s2) {
+  uint32_t a, b, c, d, e, f, t0, t1, t2;
+  asm volatile(
+      "v_and_b32 %[a], 0x07070707, %[yl]\n\tv_lshrrev_b32 %[b], 3, %[yl]\n\tv_lshrrev_b32 %[c], 6, %[yl]\n\t"
+      "v_and_b32 %[d], 0x07070707, %[yh]\n\tv_lshrrev_b32 %[e], 3, %[yh]\n\tv_lshrrev_b32 %[f], 6, %[yh]\n\t"
+      "v_and_b32 %[b], 0x07070707, %[b]\n\tv_and_b32 %[c], 0x03030303, %[c]\n\t"
+      "v_and_b32 %[e], 0x07070707, %[e]\n\tv_and_b32 %[f], 0x03030303, %[f]\n\t"
+      "v_perm_b32 %[t0], %[s0], %[va], %[a]\n\tv_perm_b32 %[t1], %[s1], %[vb], %[b]\n\tv_perm_b32 %[t2], %[s2], %[s2], %[c]\n\t"
+      "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t"
+      "v_perm_b32 %[t1], %[s0], %[vc], %[d]\n\tv_perm_b32 %[t2], %[s1], %[vd], %[e]\n\t"
+      "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t"
+      "v_perm_b32 %[t1], %[s2], %[s2], %[f]\n\tv_bitop3_b32 %[xl], %[xl], %[t0], %[t1] bitop3:0x96\n\t"
+      "v_perm_b32 %[t0], %[s0], %[ve], %[a]\n\tv_perm_b32 %[t1], %[s1], %[vf], %[b]\n\tv_perm_b32 %[t2], %[s2], %[s2], %[c]\n\t"
+      "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t"
+      "v_perm_b32 %[t1], %[s0], %[vg], %[d]\n\tv_perm_b32 %[t2], %[s1], %[vh], %[e]\n\t"
+      "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t"
+      "v_perm_b32 %[t1], %[s2], %[s2], %[f]\n\tv_bitop3_b32 %[xh], %[xh], %[t0], %[t1] bitop3:0x96"
+      : [xl] "+v"(xl), [xh] "+v"(xh), [a] "=&v"(a), [b] "=&v"(b), [c] "=&v"(c), [d] "=&v"(d), [e] "=&v"(e),
+        [f] "=&v"(f), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2)
+      : [yl] "v"(yl), [yh] "v"(yh), [va] "v"(va), [vb] "v"(vb), [vc] "v"(vc), [vd] "v"(vd), [ve] "v"(ve), [vf] "v"(vf),
+        [vg] "v"(vg), [vh] "v"(vh), [s0] "s"(s0), [s1] "s"(s1), [s2] "s"(s2));
+}
+// 4 independent quads per iteration, each x ^= c * y then y ^= x (the butterfly)
+__global__ __launch_bounds__(1024) void k_qmul(uint32_t* out, uint32_t seed) {
+  uint32_t x[8], y[8], v[8];
+  for (int i = 0; i < 8; ++i) { x[i] = threadIdx.x * seed + i; y[i] = x[i] * 747796405u; v[i] = seed * (i + 3); }
+  const uint32_t s0 = seed | 0x01020304u, s1 = seed ^ 0x05060708u, s2 = seed + 7;
+  for (int it = 0; it < ITERS / 16; ++it) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      qm(x[2 * q], x[2 * q + 1], y[2 * q], y[2 * q + 1], v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], s0, s1, s2);
+      y[2 * q] ^= x[2 * q];
+      y[2 * q + 1] ^= x[2 * q + 1];
+    }
+  }
+  uint32_t acc = 0;
+  for (int i = 0; i < 8; ++i) acc ^= x[i] ^ y[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
+__global__ __launch_bounds__(1024) void k_blk_pppp_aaaa(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_perm_b32 %0, %8, %1, %0\n\tv_perm_b32 %1, %8, %2, %1\n\tv_perm_b32 %2, %8, %3, %2\n\tv_perm_b32 %3, %8, %4, %3\n\tv_and_b32 %4, 0x07070707, %5\n\tv_and_b32 %5, 0x07070707, %6\n\tv_and_b32 %6, 0x07070707, %7\n\tv_and_b32 %7, 0x07070707, %0" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_blk_pp_aa(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_perm_b32 %0, %8, %1, %0\n\tv_perm_b32 %1, %8, %2, %1\n\tv_and_b32 %2, 0x07070707, %3\n\tv_and_b32 %3, 0x07070707, %4\n\tv_perm_b32 %4, %8, %5, %4\n\tv_perm_b32 %5, %8, %6, %5\n\tv_and_b32 %6, 0x07070707, %7\n\tv_and_b32 %7, 0x07070707, %0" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_mix_perm_xorvop2(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_perm_b32 %0, %8, %1, %0\n\tv_xor_b32 %1, %2, %1\n\tv_perm_b32 %2, %8, %3, %2\n\tv_xor_b32 %3, %4, %3\n\tv_perm_b32 %4, %8, %5, %4\n\tv_xor_b32 %5, %6, %5\n\tv_perm_b32 %6, %8, %7, %6\n\tv_xor_b32 %7, %0, %7" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_mix_bfi_and(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_bfi_b32 %0, %1, %2, %0\n\tv_and_b32 %1, 0x07070707, %2\n\tv_bfi_b32 %2, %3, %4, %2\n\tv_and_b32 %3, 0x07070707, %4\n\tv_bfi_b32 %4, %5, %6, %4\n\tv_and_b32 %5, 0x07070707, %6\n\tv_bfi_b32 %6, %7, %0, %6\n\tv_and_b32 %7, 0x07070707, %0" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_mix_bitop3s_and(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_bitop3_b32 %0, %8, %1, %0 bitop3:0x96\n\tv_and_b32 %1, 0x07070707, %2\n\tv_bitop3_b32 %2, %8, %3, %2 bitop3:0x96\n\tv_and_b32 %3, 0x07070707, %4\n\tv_bitop3_b32 %4, %8, %5, %4 bitop3:0x96\n\tv_and_b32 %5, 0x07070707, %6\n\tv_bitop3_b32 %6, %8, %7, %6 bitop3:0x96\n\tv_and_b32 %7, 0x07070707, %0" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+
 template <typename F>
 int run(const char* name, F kern, int cus, uint32_t* out) {
   printf("%-16s", name);
@@ -162,6 +276,32 @@ int run(const char* name, F kern, int cus, uint32_t* out) {
     }
     const double per_simd = 4.0 * per_cu * ITERS * 8;  // wave-instructions per SIMD
     printf("   %d w/SIMD: %.2f cyc@2.4GHz", 4 * per_cu, best * 1e6 / per_simd * 2.4);
+  }
+  printf("\n");
+  return 0;
+}
+
+template <typename F>
+int run_q(const char* name, F kern, int cus, uint32_t* out) {
+  printf("%-28s", name);
+  for (int per_cu : {1, 2}) {
+    kern<<<cus * per_cu, 1024>>>(out, 7);
+    CK(hipDeviceSynchronize());
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    float best = 1e9;
+    for (int r = 0; r < 3; ++r) {
+      CK(hipEventRecord(e0));
+      kern<<<cus * per_cu, 1024>>>(out, 7);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      if (ms < best) best = ms;
+    }
+    const double quads = 4.0 * per_cu * (ITERS / 16) * 4;  // quad-multiplies per SIMD
+    printf("   %d w/SIMD: %.1f cyc/quad-mul@2.4GHz", 4 * per_cu, best * 1e6 / quads * 2.4);
   }
   printf("\n");
   return 0;
@@ -192,5 +332,16 @@ int main() {
   run("alignbit", k_alignbit, cus, out);
   run("bfe", k_bfe, cus, out);
   run("mov_b32", k_mov_b32, cus, out);
+  run("mix_perm_and_1_1", k_mix_perm_and_1_1, cus, out);
+  run("mix_perm_and_1_2", k_mix_perm_and_1_2, cus, out);
+  run("mix_perm_bitop3_1_1", k_mix_perm_bitop3_1_1, cus, out);
+  run("mix_permvvv_and_1_1", k_mix_permvvv_and_1_1, cus, out);
+  run("mix_and_xor", k_mix_and_xor, cus, out);
+  run_q("qmul (28+2 instr per quad)", k_qmul, cus, out);
+  run("blk_pppp_aaaa", k_blk_pppp_aaaa, cus, out);
+  run("blk_pp_aa", k_blk_pp_aa, cus, out);
+  run("mix_perm_xorvop2", k_mix_perm_xorvop2, cus, out);
+  run("mix_bfi_and", k_mix_bfi_and, cus, out);
+  run("mix_bitop3s_and", k_mix_bitop3s_and, cus, out);
   return 0;
 }
