@@ -130,17 +130,37 @@ int np_reconstruct_batch_dev(np_ctx* ctx, const np_code_params* params, const ui
 /* Same as np_reconstruct_batch_dev with the present mask on the device
  * (d_present: batch rows of n bytes) and optionally the erasure locators already
  * computed (d_locators: batch rows of n uint16, see np_error_locator_dev).
- * d_locators == NULL: the locators are computed on the device (fused into the
- * reconstruct kernel on the fast path).  No host-side NeedMoreShards check. */
+ * d_locators == NULL: the locators are computed on the device (on the fast path
+ * by a per-payload kernel that also picks the shortest row prefix holding k
+ * present rows).  No host-side NeedMoreShards check. */
 int np_reconstruct_batch_dev2(np_ctx* ctx, const np_code_params* params, const uint8_t* d_shards,
                               size_t shard_len, size_t batch_stride, const uint8_t* d_present,
                               const uint16_t* d_locators, size_t batch, uint8_t* d_out, size_t out_stride,
                               void* stream);
+/* mod.rs:247-285 ReedSolomon::reconstruct_from_systematic for `batch` payloads
+ * whose first k shards are all present: d_shards as for np_encode_batch_dev
+ * (batch_stride >= k*shard_len, only rows 0..k-1 are read), d_out as for
+ * np_reconstruct_batch_dev.  A transpose-gather, no field arithmetic. */
+int np_reconstruct_from_systematic_batch_dev(np_ctx* ctx, const np_code_params* params, const uint8_t* d_shards,
+                                             size_t shard_len, size_t batch_stride, size_t batch, uint8_t* d_out,
+                                             size_t out_stride, void* stream);
 /* inc_reconstruct.rs:90-113 eval_error_polynomial for `batch` erasure patterns
  * (d_present: batch rows of n bytes, nonzero = present).  Writes the first n
  * entries of each 65536-entry locator (log form) to d_locators (batch x n). */
 int np_error_locator_dev(np_ctx* ctx, size_t n, const uint8_t* d_present, size_t batch, uint16_t* d_locators,
                          void* stream);
+
+/* ---- host-memory batch API: the caller's buffers in host memory ----------
+ * Same layouts as the device batch API, host pointers.  The batch is
+ * pipelined over several streams in sub-batches (H2D, kernel, D2H overlap);
+ * pinned host memory (hipHostMalloc / hipHostRegister) gives full overlap.
+ * Reconstruct copies only the shard rows the kernels read.  Both calls return
+ * when the outputs are in host memory. */
+int np_encode_batch_host(np_ctx* ctx, const np_code_params* params, const uint8_t* payloads, size_t payload_len,
+                         size_t payload_stride, size_t batch, uint8_t* shards, size_t batch_stride);
+int np_reconstruct_batch_host(np_ctx* ctx, const np_code_params* params, const uint8_t* shards, size_t shard_len,
+                              size_t batch_stride, const uint8_t* present, size_t batch, uint8_t* out,
+                              size_t out_stride);
 
 /* ---- low-level parity hooks (device pointers, `cols` independent columns) ----
  * data layout: column c, position i at d_data[c*size + i] (uint16, plain values). */

@@ -106,6 +106,11 @@ struct np_ctx {
   DevBuf d_big;
   hipEvent_t big_done = nullptr;
   bool big_used = false;
+  // Host-memory batch pipeline (np_*_batch_host): per slot a stream and
+  // device buffers for one sub-batch; created on first use.
+  static constexpr int kPipe = 3;
+  hipStream_t pipe_s[kPipe] = {};
+  DevBuf pipe_in[kPipe], pipe_out[kPipe], pipe_pres[kPipe];
 };
 
 namespace {
@@ -370,6 +375,13 @@ void np_ctx_destroy(np_ctx* c) {
   c->d_present.release();
   c->d_big.release();
   if (c->big_done) (void)hipEventDestroy(c->big_done);
+  for (int i = 0; i < np_ctx::kPipe; ++i) {
+    if (c->pipe_s[i]) (void)hipStreamSynchronize(c->pipe_s[i]);
+    c->pipe_in[i].release();
+    c->pipe_out[i].release();
+    c->pipe_pres[i].release();
+    if (c->pipe_s[i]) (void)hipStreamDestroy(c->pipe_s[i]);
+  }
   c->h_in.release();
   c->h_out.release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -432,6 +444,142 @@ int np_encode_batch_dev(np_ctx* c, const np_code_params* p, const uint8_t* d_pay
   (void)hipSetDevice(c->device);
   np::EncodeArgs a = enc_args(p, d_payloads, len, pstride, batch, d_shards, bstride);
   return dev_err(launch_encode(c, a, pick(c, stream)));
+}
+
+// ------------------------------------------------- host-memory pipeline ----
+// the caller's view of encode / reconstruct, buffers in host
+// memory.  The batch goes in sub-batches of about kPipeSlotBytes over
+// np_ctx::kPipe streams; each sub-batch is H2D -> kernel -> D2H on its
+// stream, so the copies of one overlap the kernels and the opposite-direction
+// copies of the others (PCIe is full duplex).  Host buffers allocated with
+// hipHostMalloc / registered with hipHostRegister are copied by DMA directly;
+// pageable ones are staged by the runtime and overlap less.
+namespace {
+
+constexpr size_t kPipeSlotBytes = size_t(64) << 20;
+
+hipError_t pipe_init(np_ctx* c) {
+  for (int i = 0; i < np_ctx::kPipe; ++i)
+    if (!c->pipe_s[i]) {
+      hipError_t e = hipStreamCreateWithFlags(&c->pipe_s[i], hipStreamNonBlocking);
+      if (e != hipSuccess) return e;
+    }
+  return hipSuccess;
+}
+
+hipError_t pipe_sync(np_ctx* c, hipError_t e) {
+  for (int i = 0; i < np_ctx::kPipe; ++i) {
+    const hipError_t r = hipStreamSynchronize(c->pipe_s[i]);
+    if (e == hipSuccess) e = r;
+  }
+  return e;
+}
+
+// Rows of each payload the reconstruct kernels read: the fast path decodes
+// from the shortest prefix of k, 2k or n rows holding k present rows
+// (kernels_fast.hip rec_tile), every other path reads all n rows.
+size_t rows_needed(const np_code_params* p, const uint8_t* present, size_t batch) {
+  if (!np::fast_reconstruct_supported(static_cast<uint32_t>(p->n), static_cast<uint32_t>(p->k))) return p->n;
+  size_t rows = p->k;
+  for (size_t b = 0; b < batch && rows < p->n; ++b) {
+    const uint8_t* pr = present + b * p->n;
+    size_t have1 = 0, have2 = 0;
+    for (size_t v = 0; v < 2 * p->k; ++v) {
+      have1 += (v < p->k && pr[v]) ? 1 : 0;
+      have2 += pr[v] ? 1 : 0;
+    }
+    const size_t need = have1 == p->k ? p->k : (p->n == 4 * p->k && have2 >= p->k) ? 2 * p->k : p->n;
+    rows = std::max(rows, need);
+  }
+  return rows;
+}
+
+}  // namespace
+
+int np_encode_batch_host(np_ctx* c, const np_code_params* p, const uint8_t* payloads, size_t len, size_t pstride,
+                         size_t batch, uint8_t* shards, size_t bstride) {
+  if (!c) return fail(NP_ERR_INVALID_ARGUMENT);
+  int st = check_params(p);
+  if (st) return st;
+  if (len == 0) return fail(NP_ERR_PAYLOAD_SIZE_IS_ZERO);
+  const size_t sl = np_shard_len(p, len), row_bytes = p->wanted_n * sl;
+  if (!payloads || !shards || pstride < len || bstride < row_bytes) return fail(NP_ERR_INVALID_ARGUMENT);
+  if (batch == 0) return NP_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
+  hipError_t e = pipe_init(c);
+  const size_t sb = std::min(batch, std::max<size_t>(1, kPipeSlotBytes / (len + row_bytes)));
+  for (int i = 0; e == hipSuccess && i < np_ctx::kPipe; ++i) {
+    e = c->pipe_in[i].ensure(sb * len);
+    if (e == hipSuccess) e = c->pipe_out[i].ensure(sb * row_bytes);
+  }
+  size_t slot = 0;
+  for (size_t b0 = 0; e == hipSuccess && b0 < batch; b0 += sb, slot = (slot + 1) % np_ctx::kPipe) {
+    const size_t cnt = std::min(sb, batch - b0);
+    hipStream_t s = c->pipe_s[slot];
+    uint8_t* din = c->pipe_in[slot].as<uint8_t>();
+    uint8_t* dout = c->pipe_out[slot].as<uint8_t>();
+    e = hipMemcpy2DAsync(din, len, payloads + b0 * pstride, pstride, len, cnt, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = launch_encode(c, enc_args(p, din, len, len, cnt, dout, row_bytes), s);
+    if (e == hipSuccess)
+      e = hipMemcpy2DAsync(shards + b0 * bstride, bstride, dout, row_bytes, row_bytes, cnt, hipMemcpyDeviceToHost, s);
+  }
+  return dev_err(pipe_sync(c, e));
+}
+
+int np_reconstruct_batch_host(np_ctx* c, const np_code_params* p, const uint8_t* shards, size_t shard_len,
+                              size_t bstride, const uint8_t* present, size_t batch, uint8_t* out,
+                              size_t out_stride) {
+  if (!c || !present) return fail(NP_ERR_INVALID_ARGUMENT);
+  int st = check_params(p);
+  if (st) return st;
+  for (size_t b = 0; b < batch; ++b) {  // mod.rs:171-180
+    size_t have = 0;
+    for (size_t v = 0; v < p->n; ++v) have += present[b * p->n + v] ? 1 : 0;
+    if (have < p->k) return fail(NP_ERR_NEED_MORE_SHARDS, have, p->k, p->n);
+  }
+  if (shard_len == 0 || (shard_len & 1)) return fail(NP_ERR_EMPTY_SHARD);
+  const size_t olen = (shard_len / 2) * 2 * p->k;
+  if (!shards || !out || bstride < p->n * shard_len || out_stride < olen) return fail(NP_ERR_INVALID_ARGUMENT);
+  if (batch == 0) return NP_OK;
+  // only the rows the kernels read cross PCIe; the device stride stays n rows
+  const size_t rows = rows_needed(p, present, batch), in_bytes = rows * shard_len, dstride = p->n * shard_len;
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
+  hipError_t e = pipe_init(c);
+  const size_t sb = std::min(batch, std::max<size_t>(1, kPipeSlotBytes / (in_bytes + olen)));
+  for (int i = 0; e == hipSuccess && i < np_ctx::kPipe; ++i) {
+    e = c->pipe_in[i].ensure((sb - 1) * dstride + in_bytes);
+    if (e == hipSuccess) e = c->pipe_out[i].ensure(sb * olen);
+    if (e == hipSuccess) e = c->pipe_pres[i].ensure(sb * p->n);
+  }
+  size_t slot = 0;
+  for (size_t b0 = 0; e == hipSuccess && b0 < batch; b0 += sb, slot = (slot + 1) % np_ctx::kPipe) {
+    const size_t cnt = std::min(sb, batch - b0);
+    hipStream_t s = c->pipe_s[slot];
+    uint8_t* din = c->pipe_in[slot].as<uint8_t>();
+    uint8_t* dout = c->pipe_out[slot].as<uint8_t>();
+    e = hipMemcpy2DAsync(din, dstride, shards + b0 * bstride, bstride, in_bytes, cnt, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(c->pipe_pres[slot].p, present + b0 * p->n, cnt * p->n, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) {
+      np::ReconstructArgs a{};
+      a.shards = din;
+      a.shard_len = shard_len;
+      a.batch_stride = dstride;
+      a.present = c->pipe_pres[slot].as<uint8_t>();
+      a.locators = nullptr;  // computed on the device
+      a.batch = cnt;
+      a.n = static_cast<uint32_t>(p->n);
+      a.k = static_cast<uint32_t>(p->k);
+      a.out = dout;
+      a.out_stride = olen;
+      e = launch_reconstruct(c, a, s);
+    }
+    if (e == hipSuccess)
+      e = hipMemcpy2DAsync(out + b0 * out_stride, out_stride, dout, olen, olen, cnt, hipMemcpyDeviceToHost, s);
+  }
+  return dev_err(pipe_sync(c, e));
 }
 
 // ---------------------------------------------------------- reconstruct ----
@@ -586,7 +734,8 @@ int np_reconstruct(np_ctx* c, const uint8_t* const* shards, const size_t* lens, 
 int np_rs_reconstruct_from_systematic(np_ctx* c, const np_code_params* p, const uint8_t* const* chunks,
                                       const size_t* lens, size_t n_chunks, uint8_t* out, size_t cap,
                                       size_t* out_len) {
-  // mod.rs:247-285: a pure gather of the first k shards, no field arithmetic.
+  // mod.rs:247-285: validation as the crate, then the column gather of the
+  // first k shards on the device (kernels_systematic.hip)
   if (!c || !p || (n_chunks && (!chunks || !lens))) return fail(NP_ERR_INVALID_ARGUMENT);
   if (n_chunks == 0) return fail(NP_ERR_NEED_MORE_SHARDS, 0, p->k, p->n);
   if (n_chunks < p->k) return fail(NP_ERR_NEED_MORE_SHARDS, n_chunks, p->k, p->n);
@@ -594,16 +743,44 @@ int np_rs_reconstruct_from_systematic(np_ctx* c, const np_code_params* p, const 
   if (syms == 0) return fail(NP_ERR_EMPTY_SHARD);
   for (size_t i = 0; i < n_chunks; ++i)
     if ((lens[i] + 1) / 2 != syms) return fail(NP_ERR_INCONSISTENT_SHARD_LENGTHS, syms, (lens[i] + 1) / 2);
-  const size_t k = p->k, need = syms * 2 * k;
+  const size_t k = p->k, need = syms * 2 * k, sl = 2 * syms;
   if (!out || !out_len || cap < need) return fail(NP_ERR_INVALID_ARGUMENT, need);
-  for (size_t s = 0; s < syms; ++s)
-    for (size_t j = 0; j < k; ++j) {
-      const uint8_t* ch = chunks[j];
-      out[s * 2 * k + 2 * j] = (2 * s < lens[j]) ? ch[2 * s] : 0;
-      out[s * 2 * k + 2 * j + 1] = (2 * s + 1 < lens[j]) ? ch[2 * s + 1] : 0;
-    }
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
+  hipError_t e = c->h_in.ensure(k * sl);
+  if (e == hipSuccess) e = c->d_in.ensure(k * sl);
+  if (e == hipSuccess) e = c->d_out.ensure(need);
+  if (e == hipSuccess) e = c->h_out.ensure(need);
+  if (e != hipSuccess) return dev_err(e);
+  uint8_t* stage = c->h_in.as<uint8_t>();
+  for (size_t j = 0; j < k; ++j) {
+    std::memcpy(stage + j * sl, chunks[j], lens[j]);
+    if (lens[j] < sl) std::memset(stage + j * sl + lens[j], 0, sl - lens[j]);  // WrappedShard zero pad
+  }
+  hipStream_t s = c->stream;
+  e = hipMemcpyAsync(c->d_in.p, stage, k * sl, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = np::launch_systematic(c->d_in.as<uint8_t>(), sl, k * sl, static_cast<uint32_t>(k), 1,
+                                                 c->d_out.as<uint8_t>(), need, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(c->h_out.p, c->d_out.p, need, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return dev_err(e);
+  std::memcpy(out, c->h_out.p, need);
   *out_len = need;
   return NP_OK;
+}
+
+int np_reconstruct_from_systematic_batch_dev(np_ctx* c, const np_code_params* p, const uint8_t* d_shards,
+                                             size_t shard_len, size_t bstride, size_t batch, uint8_t* d_out,
+                                             size_t out_stride, void* stream) {
+  if (!c) return fail(NP_ERR_INVALID_ARGUMENT);
+  int st = check_params(p);
+  if (st) return st;
+  if (shard_len == 0 || (shard_len & 1)) return fail(NP_ERR_EMPTY_SHARD);
+  if (!d_shards || !d_out || bstride < p->k * shard_len || out_stride < (shard_len / 2) * 2 * p->k)
+    return fail(NP_ERR_INVALID_ARGUMENT);
+  (void)hipSetDevice(c->device);
+  return dev_err(np::launch_systematic(d_shards, shard_len, bstride, static_cast<uint32_t>(p->k), batch, d_out,
+                                       out_stride, pick(c, stream)));
 }
 
 // --------------------------------------------------------- parity hooks ----

@@ -49,6 +49,11 @@ hipError_t launch_encode_low(const DevTables& T, const uint16_t* data, uint32_t 
 hipError_t launch_decode_main(const DevTables& T, uint16_t* codeword, uint32_t upto, const uint8_t* present,
                               const uint16_t* locator, uint32_t n, size_t cols, hipStream_t s);
 
+// ---- reconstruct_from_systematic (kernels_systematic.hip) ----
+// out[b][2(c*k + j) .. +2) = shards[b][j][2c .. +2) for j < k, c < shard_len / 2.
+hipError_t launch_systematic(const uint8_t* shards, size_t shard_len, size_t bstride, uint32_t k, size_t batch,
+                             uint8_t* out, size_t ostride, hipStream_t s);
+
 // ---- fast path (kernels_fast.hip) ----
 // Returns true if a specialised kernel serves (n, k).
 bool fast_encode_supported(uint32_t n, uint32_t k);

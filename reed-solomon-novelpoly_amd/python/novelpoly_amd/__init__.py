@@ -70,6 +70,9 @@ def lib() -> C.CDLL:
             "np_reconstruct_batch_dev": (C.c_int, [vp, P, vp, _sz, _sz, vp, _sz, vp, _sz, vp]),
             "np_reconstruct_batch_dev2": (C.c_int, [vp, P, vp, _sz, _sz, vp, vp, _sz, vp, _sz, vp]),
             "np_error_locator_dev": (C.c_int, [vp, _sz, vp, _sz, vp, vp]),
+            "np_reconstruct_from_systematic_batch_dev": (C.c_int, [vp, P, vp, _sz, _sz, _sz, vp, _sz, vp]),
+            "np_encode_batch_host": (C.c_int, [vp, P, vp, _sz, _sz, _sz, vp, _sz]),
+            "np_reconstruct_batch_host": (C.c_int, [vp, P, vp, _sz, _sz, vp, _sz, vp, _sz]),
             "np_afft_dev": (C.c_int, [vp, vp, _sz, _sz, _sz, vp]),
             "np_inverse_afft_dev": (C.c_int, [vp, vp, _sz, _sz, _sz, vp]),
             "np_walsh_dev": (C.c_int, [vp, vp, _sz, vp]),
@@ -411,6 +414,31 @@ def reconstruct_batch_dev2(params: CodeParams, d_shards: int, shard_len: int, ba
     _raise(lib().np_reconstruct_batch_dev2(ctx.handle, C.byref(params._c()), d_shards, shard_len, batch_stride,
                                            d_present, d_locators or None, batch, d_out, out_stride,
                                            stream or None))
+
+
+def encode_batch_host(params: CodeParams, payloads: int, payload_len: int, payload_stride: int, batch: int,
+                      shards: int, batch_stride: int, ctx: Optional[Context] = None) -> None:
+    """Host-memory batch encode (addresses of host buffers, e.g. numpy / pinned torch)."""
+    ctx = ctx or default_context()
+    _raise(lib().np_encode_batch_host(ctx.handle, C.byref(params._c()), payloads, payload_len, payload_stride, batch,
+                                      shards, batch_stride))
+
+
+def reconstruct_batch_host(params: CodeParams, shards: int, shard_len: int, batch_stride: int, present: int,
+                           batch: int, out: int, out_stride: int, ctx: Optional[Context] = None) -> None:
+    """Host-memory batch reconstruct; present: address of batch*n host flags."""
+    ctx = ctx or default_context()
+    _raise(lib().np_reconstruct_batch_host(ctx.handle, C.byref(params._c()), shards, shard_len, batch_stride, present,
+                                           batch, out, out_stride))
+
+
+def reconstruct_from_systematic_batch_dev(params: CodeParams, d_shards: int, shard_len: int, batch_stride: int,
+                                          batch: int, d_out: int, out_stride: int, ctx: Optional[Context] = None,
+                                          stream: int = 0) -> None:
+    """mod.rs:247-285 for a device batch whose first k shards are present."""
+    ctx = ctx or default_context()
+    _raise(lib().np_reconstruct_from_systematic_batch_dev(ctx.handle, C.byref(params._c()), d_shards, shard_len,
+                                                          batch_stride, batch, d_out, out_stride, stream or None))
 
 
 def reconstruct_batch_dev(params: CodeParams, d_shards: int, shard_len: int, batch_stride: int, present,

@@ -407,3 +407,70 @@ def test_reconstruct_prefix_modes(gpu, oracle, nw, kw, plen):
         assert st == 0
         assert o[b].tobytes() == want, (b, b % len(pats))
         assert want[:plen] == pls[b].tobytes()
+
+
+@pytest.mark.parametrize("nw,kw,plen,batch", [(1024, 342, 512 * 300 + 7, 3), (16, 8, 4096, 2), (256, 86, 99, 5),
+                                              (4096, 1366, 2048 * 70, 2), (2, 1, 3, 4), (300, 100, 64 * 129, 2)])
+def test_reconstruct_from_systematic_batch_dev(gpu, oracle, nw, kw, plen, batch):
+    """Device batch reconstruct_from_systematic (mod.rs:247-285): the column
+    gather of the first k shards equals the oracle's, payload by payload, for
+    k below, at and above the 64 x 64 tile."""
+    import torch
+
+    p = npa.CodeParams.derive_parameters(nw, kw)
+    n, k = p.n(), p.k()
+    sl = p.make_encoder(gpu).shard_len(plen)
+    pls = np.stack([np.frombuffer(synth.payload(7000 + b, plen), dtype=np.uint8) for b in range(batch)])
+    dp = dev(pls)
+    ds = torch.empty((batch, n, sl), dtype=torch.uint8, device="cuda")
+    npa.encode_batch_dev(p, dp.data_ptr(), plen, plen, batch, ds.data_ptr(), n * sl, ctx=gpu, stream=stream())
+    olen = (sl // 2) * 2 * k
+    out = torch.empty((batch, olen), dtype=torch.uint8, device="cuda")
+    npa.reconstruct_from_systematic_batch_dev(p, ds.data_ptr(), sl, n * sl, batch, out.data_ptr(), olen, ctx=gpu,
+                                              stream=stream())
+    o, hs = host(out), host(ds)
+    for b in range(batch):
+        st, want = oracle.reconstruct_from_systematic([hs[b, i].tobytes() for i in range(k)], n, k)
+        assert st == 0 and o[b].tobytes() == want
+        assert want[:plen] == pls[b].tobytes()
+
+
+@pytest.mark.parametrize("nw,kw,plen,batch", [(1024, 342, 512 * 256, 9), (256, 86, 128 * 99 + 1, 7),
+                                              (300, 100, 5000, 3), (4096, 1366, 2048 * 40, 2)])
+def test_host_batch_pipeline(gpu, oracle, nw, kw, plen, batch):
+    """np_encode_batch_host / np_reconstruct_batch_host (host buffers, pipelined
+    sub-batches over several streams) give the oracle's shards and payloads;
+    strided host layouts included."""
+    p = npa.CodeParams.derive_parameters(nw, kw)
+    n, k = p.n(), p.k()
+    sl = p.make_encoder(gpu).shard_len(plen)
+    pstride = plen + 3
+    pay = np.zeros((batch, pstride), dtype=np.uint8)
+    for b in range(batch):
+        pay[b, :plen] = np.frombuffer(synth.payload(9100 + b, plen), dtype=np.uint8)
+    wn = p.wanted_n
+    bstride = n * sl + 64
+    sh = np.full((batch, bstride), 0xAB, dtype=np.uint8)
+    npa.encode_batch_host(p, pay.ctypes.data, plen, pstride, batch, sh.ctypes.data, bstride, ctx=gpu)
+    for b in range(batch):
+        st, want = oracle.encode(pay[b, :plen].tobytes(), n, k, wn)
+        assert st == 0
+        got = [sh[b, i * sl:(i + 1) * sl].tobytes() for i in range(wn)]
+        assert got == want, b
+    assert (sh[:, wn * sl:] == 0xAB).all()  # nothing written past wanted_n rows
+    rng = np.random.default_rng(plen)
+    pres = np.zeros((batch, n), dtype=np.uint8)
+    for b in range(batch):  # erasures among the wanted_n rows that exist
+        pres[b, :wn] = 1
+        gone = (wn - k) if b % 2 else (wn - k) // 3
+        pres[b, rng.choice(wn, gone, replace=False)] = 0
+    olen = (sl // 2) * 2 * k
+    ostride = olen + 5
+    out = np.zeros((batch, ostride), dtype=np.uint8)
+    npa.reconstruct_batch_host(p, sh.ctypes.data, sl, bstride, pres.ctypes.data, batch, out.ctypes.data, ostride,
+                               ctx=gpu)
+    for b in range(batch):
+        recv = [sh[b, i * sl:(i + 1) * sl].tobytes() if pres[b, i] else None for i in range(n)]
+        st, want = oracle.reconstruct(recv, n, k)
+        assert st == 0 and out[b, :olen].tobytes() == want, b
+        assert want[:plen] == pay[b, :plen].tobytes()

@@ -1,8 +1,9 @@
-"""Host-memory end-to-end rate (SURVEY §8(d) "End-to-end"):
-payloads start in pinned host memory, shards/outputs end in pinned host memory.
-Measures (1) serial: H2D -> kernel -> D2H on one stream, and (2) pipelined:
-the batch split into chunks over two streams so that copies overlap kernels.
-Never the bench `value` (that one is device-resident)."""
+"""Host-memory end-to-end rate (SURVEY §8(d) "End-to-end", §8(f) 2):
+payloads start in pinned host memory and shards / outputs end in pinned host
+memory, through the C ABI's host batch calls (np_encode_batch_host,
+np_reconstruct_batch_host: sub-batches pipelined over streams, H2D / kernel /
+D2H overlapped).  Also reports the PCIe bound for the same bytes.  Never the
+bench `value` (that one is device-resident)."""
 import argparse
 import json
 import os
@@ -12,16 +13,15 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "reed-solomon-novelpoly_amd", "python"))
 
-import numpy as np
-import torch
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
 
-import novelpoly_amd as npa
-from novelpoly_amd import synth
+import novelpoly_amd as npa  # noqa: E402
+from novelpoly_amd import synth  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", type=int, default=3)
 ap.add_argument("--batch", type=int, default=256)
-ap.add_argument("--chunks", type=int, default=8)
 ap.add_argument("--reps", type=int, default=3)
 args = ap.parse_args()
 
@@ -35,50 +35,41 @@ olen = (sl // 2) * 2 * k
 h_pay = torch.randint(0, 256, (B, plen), dtype=torch.uint8).pin_memory()
 h_sh = torch.empty((B, n, sl), dtype=torch.uint8).pin_memory()
 h_out = torch.empty((B, olen), dtype=torch.uint8).pin_memory()
-pres = torch.from_numpy(np.stack([synth.present_mask(i, n, erase) for i in range(B)]))
-d_pay = torch.empty((B, plen), dtype=torch.uint8, device="cuda")
-d_sh = torch.empty((B, n, sl), dtype=torch.uint8, device="cuda")
-d_out = torch.empty((B, olen), dtype=torch.uint8, device="cuda")
-d_pres = pres.cuda()
-streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+pres = np.ascontiguousarray(np.stack([synth.present_mask(i, n, erase) for i in range(B)]).astype(np.uint8))
 
-
-def enc_range(lo, hi, s):
-    with torch.cuda.stream(s):
-        d_pay[lo:hi].copy_(h_pay[lo:hi], non_blocking=True)
-        npa.encode_batch_dev(p, d_pay[lo].data_ptr(), plen, plen, hi - lo, d_sh[lo].data_ptr(), n * sl, ctx=ctx,
-                             stream=s.cuda_stream)
-        h_sh[lo:hi].copy_(d_sh[lo:hi], non_blocking=True)
-
-
-def rec_range(lo, hi, s):
-    # only present shards travel: gather rows on the host side would cost a CPU
-    # copy, so we ship the whole shard matrix rows that are present (mask view)
-    with torch.cuda.stream(s):
-        d_sh[lo:hi].copy_(h_sh[lo:hi], non_blocking=True)
-        npa.reconstruct_batch_dev2(p, d_sh[lo].data_ptr(), sl, n * sl, d_pres[lo].data_ptr(), 0, hi - lo,
-                                   d_out[lo].data_ptr(), olen, ctx=ctx, stream=s.cuda_stream)
-        h_out[lo:hi].copy_(d_out[lo:hi], non_blocking=True)
-
-
-def run(fn, chunks):
-    step = (B + chunks - 1) // chunks
+# PCIe reference: one pinned H2D and one D2H of 256 MiB
+buf_h = torch.empty(256 << 20, dtype=torch.uint8).pin_memory()
+buf_d = torch.empty(256 << 20, dtype=torch.uint8, device="cuda")
+for direction in ("h2d", "d2h"):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for r in range(args.reps):
-        for i, lo in enumerate(range(0, B, step)):
-            fn(lo, min(B, lo + step), streams[i % 2] if chunks > 1 else streams[0])
+    for _ in range(3):
+        (buf_d.copy_(buf_h, non_blocking=True) if direction == "h2d" else buf_h.copy_(buf_d, non_blocking=True))
     torch.cuda.synchronize()
+    globals()["bw_" + direction] = 3 * (256 << 20) / (time.perf_counter() - t0) / 1e9
+
+
+def timed(fn):
+    fn()  # warm
+    t0 = time.perf_counter()
+    for _ in range(args.reps):
+        fn()
     return (time.perf_counter() - t0) / args.reps
 
 
-res = {"config": args.config, "batch": B, "payload_bytes": plen, "n": n, "k": k}
-for name, fn in (("encode", enc_range), ("reconstruct", rec_range)):
-    run(fn, 1)  # warm
-    t1 = run(fn, 1)
-    tp = run(fn, args.chunks)
-    res[name] = {"serial_GiB_s": B * plen / t1 / 2**30, "pipelined_GiB_s": B * plen / tp / 2**30,
-                 "serial_ms": t1 * 1e3, "pipelined_ms": tp * 1e3, "chunks": args.chunks}
+t_enc = timed(lambda: npa.encode_batch_host(p, h_pay.data_ptr(), plen, plen, B, h_sh.data_ptr(), n * sl, ctx=ctx))
+t_rec = timed(lambda: npa.reconstruct_batch_host(p, h_sh.data_ptr(), sl, n * sl, pres.ctypes.data, B,
+                                                 h_out.data_ptr(), olen, ctx=ctx))
 ok = torch.equal(h_out[:, :plen], h_pay)
-res["roundtrip_ok"] = bool(ok)
+# bytes crossing PCIe: encode P in + n*sl out; reconstruct the prefix rows in (+ flags) and 2k*sl/2 out
+rows = max(k if pres[b, :k].all() else (2 * k if (n == 4 * k and pres[b, :2 * k].sum() >= k) else n) for b in range(B))
+res = {
+    "config": args.config, "batch": B, "payload_bytes": plen, "n": n, "k": k,
+    "pcie_GB_s": {"h2d": round(bw_h2d, 1), "d2h": round(bw_d2h, 1)},
+    "encode": {"GiB_s": round(B * plen / t_enc / 2**30, 2), "ms": round(t_enc * 1e3, 2),
+               "pcie_bound_GiB_s": round(B * plen / max(B * plen / (bw_h2d * 1e9), B * n * sl / (bw_d2h * 1e9)) / 2**30, 2)},
+    "reconstruct": {"GiB_s": round(B * plen / t_rec / 2**30, 2), "ms": round(t_rec * 1e3, 2), "rows_copied": rows,
+                    "pcie_bound_GiB_s": round(B * plen / max(B * rows * sl / (bw_h2d * 1e9), B * olen / (bw_d2h * 1e9)) / 2**30, 2)},
+    "roundtrip_ok": bool(ok),
+}
 print(json.dumps(res))
