@@ -17,14 +17,29 @@ src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
 dst = os.path.join(ROOT, "profiles")
 os.makedirs(dst, exist_ok=True)
 
-KERNELS = {"encode": "k_encode_fast", "reconstruct": "k_reconstruct_fast", "locator": "k_error_locator",
-           "encode_big": "k_encode_big", "reconstruct_big": "k_reconstruct_big",
-           "calib_read8": "read8", "calib_copy8": "copy8"}
+# The bench's "reconstruct" span is the prefix-locator launch plus both fast
+# reconstruct instances (prefixes of <= 2 and of 4 segments); their per-launch
+# traffic and durations add up.  Each instance is also reported on its own.
+KINDS = {"encode": ("k_encode_fast",), "reconstruct": ("k_reconstruct_fast", "k_prefix_locator"),
+         "locator": ("k_error_locator",), "encode_big": ("k_encode_big",), "reconstruct_big": ("k_reconstruct_big",),
+         "calib_read8": ("read8",), "calib_copy8": ("copy8",)}
 
 
-def kind(name):
-    for k, pat in KERNELS.items():
-        if pat + "(" in name or pat + "<" in name:
+def instance(name):
+    """Kernel instance (template arguments kept, parameter list dropped)."""
+    for pats in KINDS.values():
+        for pat in pats:
+            i = name.find(pat + "(")
+            if i < 0:
+                i = name.find(pat + "<")
+            if i >= 0:
+                return name[i:].split("(")[0]
+    return None
+
+
+def kind(inst):
+    for k, pats in KINDS.items():
+        if any(inst == p or inst.startswith(p + "<") for p in pats):
             return k
     return None
 
@@ -36,15 +51,22 @@ def newest(pattern):
 
 
 def counters(pass_name):
+    """{instance: {counter: [per-launch values]}}"""
     f = newest(os.path.join(src, pass_name, "*", "*_counter_collection.csv"))
     agg = defaultdict(lambda: defaultdict(list))
     if not f:
         return agg
     for r in csv.DictReader(open(f[0])):
-        k = kind(r["Kernel_Name"])
-        if k:
-            agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        i = instance(r["Kernel_Name"])
+        if i:
+            agg[i][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return agg
+
+
+def by_kind(c, k, name):
+    """Per-launch value of counter `name` for kind k: the sum over its instances."""
+    vals = [mean(v[name]) for i, v in c.items() if kind(i) == k and v.get(name)]
+    return sum(vals) if vals else None
 
 
 def mean(v):
@@ -56,8 +78,8 @@ fetch, write = counters("fetch"), counters("write")
 cf, cw = counters("calib_fetch"), counters("calib_write")
 GIB = 1 << 30
 # calibration: read8 reads exactly 1 GiB per dispatch; copy8 reads 1 GiB and writes 1 GiB
-f_read8 = mean(cf["calib_read8"].get("FETCH_SIZE", []))
-w_copy8 = mean(cw["calib_copy8"].get("WRITE_SIZE", []))
+f_read8 = by_kind(cf, "calib_read8", "FETCH_SIZE")
+w_copy8 = by_kind(cw, "calib_copy8", "WRITE_SIZE")
 # FETCH_SIZE / WRITE_SIZE are reported in KB (1024 B) by rocprofv3
 fetch_factor = GIB / (f_read8 * 1024) if f_read8 else None
 write_factor = GIB / (w_copy8 * 1024) if w_copy8 else None
@@ -66,32 +88,33 @@ out["calibration"] = {"read8_FETCH_SIZE_KB": f_read8, "copy8_WRITE_SIZE_KB": w_c
                       "note": "factor = known bytes / (counter * 1024) for 8-byte-per-lane coalesced access, "
                               "1 GiB buffers (beyond the 256 MiB Infinity Cache)"}
 for k in ("encode", "reconstruct", "locator", "encode_big", "reconstruct_big"):
-    fs, ws = mean(fetch[k].get("FETCH_SIZE", [])), mean(write[k].get("WRITE_SIZE", []))
+    fs, ws = by_kind(fetch, k, "FETCH_SIZE"), by_kind(write, k, "WRITE_SIZE")
     if fs is None or ws is None:
         continue
     rd = fs * 1024 * (fetch_factor or 1.0)
     wr = ws * 1024 * (write_factor or 1.0)
     out["kernels"][k] = {"FETCH_SIZE_KB": fs, "WRITE_SIZE_KB": ws, "read_bytes": rd, "write_bytes": wr,
                          "traffic_bytes": rd + wr}
-for pname in ("sq", "sq2"):
+out["instances"] = {}
+for pname in ("sq", "sq2", "fetch", "write"):
     c = counters(pname)
-    for k in ("encode", "reconstruct", "locator", "encode_big", "reconstruct_big"):
-        for name, vals in c[k].items():
-            out["kernels"].setdefault(k, {})[name] = mean(vals)
+    for i, cs in c.items():
+        if kind(i) and not kind(i).startswith("calib"):
+            for name, vals in cs.items():
+                out["instances"].setdefault(i, {})[name] = mean(vals)
 # kernel-trace averages
 st = newest(os.path.join(src, "stats", "*", "*_kernel_stats.csv"))
 if st:
     for r in csv.DictReader(open(st[0])):
-        k = kind(r["Name"])
-        if k:
-            out["kernels"].setdefault(k, {})["avg_ns"] = float(r["AverageNs"])
-            out["kernels"][k]["calls"] = int(r["Calls"])
+        i = instance(r["Name"])
+        if i and kind(i) and not kind(i).startswith("calib"):
+            out["instances"].setdefault(i, {})["avg_ns"] = float(r["AverageNs"])
+            out["instances"][i]["calls"] = int(r["Calls"])
+            k = out["kernels"].setdefault(kind(i), {})
+            k["avg_ns"] = k.get("avg_ns", 0.0) + float(r["AverageNs"])
     shutil.copy(st[0], os.path.join(dst, f"{tag}_kernel_stats.csv"))
-for k, v in out["kernels"].items():
-    if "SQ_INSTS_VALU" in v and "SQ_WAVES" in v:
+for i, v in out["instances"].items():
+    if "SQ_INSTS_VALU" in v and v.get("SQ_WAVES"):
         v["valu_insts_per_wave"] = v["SQ_INSTS_VALU"] / v["SQ_WAVES"]
-    if "SQ_ACTIVE_INST_VALU" in v and "SQ_BUSY_CYCLES" in v:
-        # SQ_ACTIVE_INST_VALU counts quad-cycles summed over SIMDs; busy cycles summed over SEs (32)
-        pass
 json.dump(out, open(os.path.join(dst, f"{tag}_pmc_summary.json"), "w"), indent=1, sort_keys=True)
 print(json.dumps(out, indent=1, sort_keys=True))
