@@ -350,14 +350,28 @@ __device__ __forceinline__ void load_rows(uint2 (&raw)[NR], const uint8_t* sh, s
   }
 }
 
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// Raw buffer descriptor (V#) over [base, base + bytes): buffer loads and
+// stores take the wave-uniform part of an address from SGPRs (base, soffset)
+// and only the lane part from a VGPR, so row addressing costs no VALU.  A load
+// at or beyond `bytes` returns zeros without touching memory.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, static_cast<int>(bytes), 0x00020000);
+}
+
 // Shard rows row0..row0+15 (those below wanted_n) from cq registers.
 __device__ __forceinline__ void store_rows(uint8_t* out, size_t shard_len, uint32_t row0, uint32_t wanted_n,
                                            const uint32_t (&L)[16], const uint32_t (&H)[16], uint32_t lane,
                                            uint32_t ncols, bool full) {
-  if (full && row0 + 16 <= wanted_n) {
+  if (full && row0 + 16 <= wanted_n && 16 * shard_len < 0x7fffffffu) {
+    const __amdgpu_buffer_rsrc_t r = buf_rsrc(out + static_cast<size_t>(row0) * shard_len, 16 * static_cast<uint32_t>(shard_len));
 #pragma unroll
-    for (int p = 0; p < 16; ++p)
-      *reinterpret_cast<uint2*>(out + static_cast<size_t>(row0 + p) * shard_len + 8u * lane) = cq_row(L[p], H[p]);
+    for (int p = 0; p < 16; ++p) {
+      const uint2 v = cq_row(L[p], H[p]);
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, r, 8u * lane,
+                                            static_cast<uint32_t>(p * shard_len), 0);
+    }
   } else {
 #pragma unroll
     for (int p = 0; p < 16; ++p)

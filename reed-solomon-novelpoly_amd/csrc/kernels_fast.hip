@@ -151,20 +151,26 @@ __device__ __forceinline__ uint32_t row_mask16(const uint8_t* pres, uint32_t row
   return static_cast<uint32_t>(__ballot(p));
 }
 
-// Issues the loads of the lane's pieces of rows row0..row0+15 (absent rows
-// read the zero page: no branch, no HBM traffic); the data is consumed later.
+// Issues the loads of the lane's pieces of rows row0..row0+15; the data is
+// consumed later.  Full tiles: one buffer descriptor per row whose size is 0
+// for an absent row, so that load returns zeros with no HBM traffic and no
+// branch.  Partial tiles: absent rows read the zero page.
 __device__ __forceinline__ void issue_rows(uint2 (&raw)[16], const uint8_t* sh, size_t shard_len, uint32_t mask,
                                            uint32_t row0, const uint8_t* zeros, uint32_t lane, uint32_t ncols,
                                            bool full) {
-  const uint8_t* src[16];
-#pragma unroll
-  for (int p = 0; p < 16; ++p) src[p] = ((mask >> p) & 1u) ? sh + static_cast<size_t>(row0 + p) * shard_len : zeros;
   if (full) {
 #pragma unroll
-    for (int p = 0; p < 16; ++p) raw[p] = *reinterpret_cast<const uint2*>(src[p] + 8u * lane);
+    for (int p = 0; p < 16; ++p) {
+      const __amdgpu_buffer_rsrc_t r = buf_rsrc(sh + static_cast<size_t>(row0 + p) * shard_len, ((mask >> p) & 1u) ? 512u : 0u);
+      const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, 8u * lane, 0, 0);
+      raw[p] = make_uint2(v.x, v.y);
+    }
   } else {
 #pragma unroll
-    for (int p = 0; p < 16; ++p) raw[p] = load4(src[p], lane, ncols, false);
+    for (int p = 0; p < 16; ++p) {
+      const uint8_t* src = ((mask >> p) & 1u) ? sh + static_cast<size_t>(row0 + p) * shard_len : zeros;
+      raw[p] = load4(src, lane, ncols, false);
+    }
   }
 }
 
