@@ -180,12 +180,17 @@ __device__ __forceinline__ Mult make_mult(const uint32_t (&p)[20]) {
   Mult m;
 #pragma unroll
   for (int i = 0; i < 12; ++i) m.s[i] = p[8 + i];
+  // 64-bit moves: the pool's SGPRs come in aligned pairs from s_load_dwordx8
+  uint64_t v01, v23, v45, v67;
   asm volatile(
-      "v_mov_b32 %0, %8\n\tv_mov_b32 %1, %9\n\tv_mov_b32 %2, %10\n\tv_mov_b32 %3, %11\n\t"
-      "v_mov_b32 %4, %12\n\tv_mov_b32 %5, %13\n\tv_mov_b32 %6, %14\n\tv_mov_b32 %7, %15"
-      : "=v"(m.v[0]), "=v"(m.v[1]), "=v"(m.v[2]), "=v"(m.v[3]), "=v"(m.v[4]), "=v"(m.v[5]), "=v"(m.v[6]),
-        "=v"(m.v[7])
-      : "s"(p[0]), "s"(p[1]), "s"(p[2]), "s"(p[3]), "s"(p[4]), "s"(p[5]), "s"(p[6]), "s"(p[7]));
+      "v_mov_b64 %0, %4\n\tv_mov_b64 %1, %5\n\tv_mov_b64 %2, %6\n\tv_mov_b64 %3, %7"
+      : "=v"(v01), "=v"(v23), "=v"(v45), "=v"(v67)
+      : "s"((static_cast<uint64_t>(p[1]) << 32) | p[0]), "s"((static_cast<uint64_t>(p[3]) << 32) | p[2]),
+        "s"((static_cast<uint64_t>(p[5]) << 32) | p[4]), "s"((static_cast<uint64_t>(p[7]) << 32) | p[6]));
+  m.v[0] = static_cast<uint32_t>(v01), m.v[1] = static_cast<uint32_t>(v01 >> 32);
+  m.v[2] = static_cast<uint32_t>(v23), m.v[3] = static_cast<uint32_t>(v23 >> 32);
+  m.v[4] = static_cast<uint32_t>(v45), m.v[5] = static_cast<uint32_t>(v45 >> 32);
+  m.v[6] = static_cast<uint32_t>(v67), m.v[7] = static_cast<uint32_t>(v67 >> 32);
   return m;
 }
 
