@@ -164,6 +164,28 @@ __device__ __forceinline__ void qplane(uint32_t& acc, const uint32_t (&s)[6], ui
         [sd] "s"(sd), [se] "s"(se), [sf] "s"(sf));
 }
 
+// One output byte plane of c*y, written (not accumulated): the last XOR3 takes
+// the third partial sum instead of an accumulator, so no zeroing move.
+__device__ __forceinline__ void qplane_set(uint32_t& out, const uint32_t (&s)[6], uint32_t va, uint32_t vb, uint32_t vc,
+                                           uint32_t vd, uint32_t sa, uint32_t sb, uint32_t sc, uint32_t sd, uint32_t se,
+                                           uint32_t sf) {
+  uint32_t t0, t1, t2, t3;
+  asm volatile(
+      "v_perm_b32 %[t0], %[sa], %[va], %[s0]\n\t"
+      "v_perm_b32 %[t1], %[sb], %[vb], %[s1]\n\t"
+      "v_perm_b32 %[t2], %[sc], %[sc], %[s2]\n\t"
+      "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t"
+      "v_perm_b32 %[t1], %[sd], %[vc], %[s3]\n\t"
+      "v_perm_b32 %[t2], %[se], %[vd], %[s4]\n\t"
+      "v_perm_b32 %[t3], %[sf], %[sf], %[s5]\n\t"
+      "v_bitop3_b32 %[out], %[t0], %[t1], %[t2] bitop3:0x96\n\t"
+      "v_xor_b32 %[out], %[out], %[t3]"
+      : [out] "=&v"(out), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3)
+      : [s0] "v"(s[0]), [s1] "v"(s[1]), [s2] "v"(s[2]), [s3] "v"(s[3]), [s4] "v"(s[4]), [s5] "v"(s[5]),
+        [va] "v"(va), [vb] "v"(vb), [vc] "v"(vc), [vd] "v"(vd), [sa] "s"(sa), [sb] "s"(sb), [sc] "s"(sc),
+        [sd] "s"(sd), [se] "s"(se), [sf] "s"(sf));
+}
+
 // A multiplier ready for use: its 20 table dwords in SGPRs plus VGPR copies of
 // the 8 dwords that v_perm must read from a VGPR.  The copies are made by an
 // asm block where the butterfly group starts, so that they are neither hoisted
@@ -216,9 +238,10 @@ __device__ __forceinline__ void qmul(uint32_t& xl, uint32_t& xh, uint32_t yl, ui
 
 // (ol, oh) = c*y.
 __device__ __forceinline__ void qmul_set(uint32_t& ol, uint32_t& oh, uint32_t yl, uint32_t yh, const Mult& m) {
-  ol = 0;
-  oh = 0;
-  qmul(ol, oh, yl, yh, m);
+  uint32_t s[6];
+  selectors(yl, yh, s);
+  qplane_set(ol, s, m.v[0], m.v[1], m.v[2], m.v[3], m.s[0], m.s[1], m.s[2], m.s[3], m.s[4], m.s[5]);
+  qplane_set(oh, s, m.v[4], m.v[5], m.v[6], m.v[7], m.s[6], m.s[7], m.s[8], m.s[9], m.s[10], m.s[11]);
 }
 
 typedef const __attribute__((address_space(4))) uint32_t* cpool_t;
