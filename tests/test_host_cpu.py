@@ -117,3 +117,20 @@ def test_ctx_without_gpu_reports_no_device():
         pytest.skip("a GPU is visible")
     with pytest.raises(npa.DeviceError):
         npa.Context(0)
+
+
+def test_decode_rows_prefix_rule():
+    """synth.decode_rows mirrors the fast reconstruct's prefix choice
+    (kernels_fast.hip rec_tile, engine.cpp rows_needed): k rows if every
+    systematic row is present, 2k if [0, 2k) holds k present rows, else n."""
+    from novelpoly_amd import synth
+
+    n, k = 1024, 256
+    pres = np.ones(n, np.uint8)
+    assert synth.decode_rows(pres, n, k) == k
+    pres[:10] = 0
+    assert synth.decode_rows(pres, n, k) == 2 * k - 10
+    pres[:] = 1
+    pres[: 2 * k - k + 1] = 0  # k - 1 present in [0, 2k)
+    assert synth.decode_rows(pres, n, k) == int(pres.sum())
+    assert synth.decode_rows(pres, n, k, (n // k,)) == int(pres.sum())

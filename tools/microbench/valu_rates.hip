@@ -255,6 +255,28 @@ __global__ __launch_bounds__(1024) void k_mix_bitop3s_and(uint32_t* out, uint32_
   out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
 }
 
+__global__ __launch_bounds__(1024) void k_perm4_salu4(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_perm_b32 %0, %8, %1, %0\n\ts_add_u32 s100, s100, 1\n\tv_perm_b32 %1, %8, %2, %1\n\ts_add_u32 s100, s100, 1\n\tv_perm_b32 %2, %8, %3, %2\n\ts_add_u32 s100, s100, 1\n\tv_perm_b32 %3, %8, %4, %3\n\ts_add_u32 s100, s100, 1" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc", "s100", "scc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_perm4_salu2(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_perm_b32 %0, %8, %1, %0\n\tv_perm_b32 %1, %8, %2, %1\n\ts_add_u32 s100, s100, 1\n\tv_perm_b32 %2, %8, %3, %2\n\tv_perm_b32 %3, %8, %4, %3\n\ts_add_u32 s100, s100, 1\n\tv_perm_b32 %4, %8, %5, %4\n\tv_perm_b32 %5, %8, %6, %5\n\ts_add_u32 s100, s100, 1\n\tv_perm_b32 %6, %8, %7, %6\n\tv_perm_b32 %7, %8, %0, %7\n\ts_add_u32 s100, s100, 1" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc", "s100", "scc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ __launch_bounds__(1024) void k_perm_only_ref(uint32_t* out, uint32_t seed) {
+  uint32_t a0 = threadIdx.x * seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t s = seed | 0x01020304u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile("v_perm_b32 %0, %8, %1, %0\n\tv_perm_b32 %1, %8, %2, %1\n\tv_perm_b32 %2, %8, %3, %2\n\tv_perm_b32 %3, %8, %4, %3\n\tv_perm_b32 %4, %8, %5, %4\n\tv_perm_b32 %5, %8, %6, %5\n\tv_perm_b32 %6, %8, %7, %6\n\tv_perm_b32 %7, %8, %0, %7" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(s) : "vcc", "s100", "scc");
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+
 template <typename F>
 int run(const char* name, F kern, int cus, uint32_t* out) {
   printf("%-16s", name);
@@ -343,5 +365,8 @@ int main() {
   run("mix_perm_xorvop2", k_mix_perm_xorvop2, cus, out);
   run("mix_bfi_and", k_mix_bfi_and, cus, out);
   run("mix_bitop3s_and", k_mix_bitop3s_and, cus, out);
+  run("perm4_salu4 (4 valu/iter)", k_perm4_salu4, cus, out);
+  run("perm4_salu2 (8 valu/iter)", k_perm4_salu2, cus, out);
+  run("perm_only_ref (8 valu/iter)", k_perm_only_ref, cus, out);
   return 0;
 }
