@@ -76,31 +76,46 @@ def load_traffic(round_tag="r01"):
 
 
 def cpu_baseline(cfg, params, seconds):
-    """Oracle (C restatement, single thread) on a bounded sample of the same workload."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import np_oracle
-    from novelpoly_amd import synth
+    """The reference's own C implementation (oracle/_ref/cpu_bench_ref, built from
+    /root/reference by oracle/Makefile) -- or, where that build is absent, the C
+    restatement (oracle/cpu_bench_port) -- on a bounded sample of the same
+    workload: whole payloads encoded and reconstructed with the crate's glue
+    (oracle/cpu_bench.c), one payload per host thread at a time, every
+    reconstruction checked.  Timed on all host cores of this GPU's share and on
+    one core."""
+    import subprocess
 
-    orc = np_oracle.Oracle()
+    ref = os.path.join(ROOT, "oracle", "_ref", "cpu_bench_ref")
+    port = os.path.join(ROOT, "oracle", "cpu_bench_port")
+    exe = ref if os.path.exists(ref) else port
+    if not os.path.exists(exe):
+        raise RuntimeError("CPU baseline harness missing: run __graft_entry__.build()")
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    threads = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", "16")), 16))
     n, k, plen, erase = params.n(), params.k(), cfg["payload"], cfg["erase"]
-    done, t_total = 0, 0.0
-    while t_total < seconds and done < 10_000:
-        pl = synth.payload(10_000 + done, plen)
-        pres = synth.present_mask(10_000 + done, n, erase)
-        t0 = time.perf_counter()
-        st, shards = orc.encode(pl, n, k, n)
-        recv = [s if pres[i] else None for i, s in enumerate(shards)]
-        st2, rec = orc.reconstruct(recv, n, k)
-        t_total += time.perf_counter() - t0
-        assert st == 0 and st2 == 0 and rec[:plen] == pl
-        done += 1
+
+    def run(t, secs):
+        out = subprocess.run([exe, str(n), str(k), str(plen), str(erase), str(t), str(secs)],
+                             check=True, capture_output=True, text=True, timeout=secs + 300)
+        r = json.loads(out.stdout.strip().splitlines()[-1])
+        assert r["failures"] == 0 and r["payloads"] > 0, r
+        return r
+
+    multi = run(threads, seconds)
+    single = run(1, max(1.0, seconds / 3))
     return {
-        "value": round(done * plen / t_total / 2**30, 6),
+        "value": round(multi["gib_s"], 6),
         "unit": "GiB/s",
-        "cores": 1,
-        "kind": "port",
-        "sample": f"{done} payloads of config {cfg['id']} (encode + reconstruct with {erase} erasures), "
-                  f"oracle/np_oracle.c single thread, {t_total:.1f}s",
+        "cores": threads,
+        "kind": multi["kind"],
+        "single_core_value": round(single["gib_s"], 6),
+        "sample": f"{multi['payloads']} payloads of config {cfg['id']} in {multi['seconds']:.1f}s on {threads} threads "
+                  f"(+{single['payloads']} in {single['seconds']:.1f}s on 1 thread): encode + reconstruct with "
+                  f"{erase} erasures, {'reference cxx/RSErasureCode.c' if multi['kind'] == 'reference' else 'oracle/np_oracle.c'} "
+                  f"+ crate glue (oracle/cpu_bench.c), every payload round-trip checked",
     }
 
 
