@@ -549,22 +549,23 @@ __device__ __forceinline__ void cq_levels(const DevTables& T, const uint32_t* VP
 }
 
 // Levels 4..logK-1 in the high layout: quad j pairs with j + 2^(b-2-logR);
-// group t = j >> (b-1-logR).
-template <int K, bool INVERSE, bool INDEX0>
+// group t = j >> (b-1-logR).  FIRST > 0 starts at flat group FIRST (the
+// forward transform's top level, one group, done by the caller: fwd_top).
+template <int K, bool INVERSE, bool INDEX0, int FIRST = 0>
 __device__ __forceinline__ void hi_levels(const DevTables& T, const uint32_t* VP, uint32_t index, uint32_t (&L)[16],
                                           uint32_t (&H)[16]) {
   if constexpr (kExp & 1) return;
   constexpr int logR = Geo<K>::kLogR;
   auto cval = [&](auto fc) __attribute__((always_inline)) {
-    constexpr GroupRef r = hi_group<K, INVERSE>(decltype(fc)::value);
+    constexpr GroupRef r = hi_group<K, INVERSE>(decltype(fc)::value + FIRST);
     return 2u * r.t + (index >> r.b);
   };
   auto vaddr = [&](auto fc) __attribute__((always_inline)) {
-    constexpr GroupRef r = hi_group<K, INVERSE>(decltype(fc)::value);
+    constexpr GroupRef r = hi_group<K, INVERSE>(decltype(fc)::value + FIRST);
     return VP + 8u * vslot<K>(r.b, r.t);
   };
   auto group = [&](auto fc, const Mult& p) __attribute__((always_inline)) {
-    constexpr GroupRef r = hi_group<K, INVERSE>(decltype(fc)::value);
+    constexpr GroupRef r = hi_group<K, INVERSE>(decltype(fc)::value + FIRST);
     constexpr int dj = 1 << (r.b - 2 - logR);
     constexpr bool live = !INDEX0 || r.t != 0;
 #pragma unroll
@@ -581,7 +582,43 @@ __device__ __forceinline__ void hi_levels(const DevTables& T, const uint32_t* VP
       }
     }
   };
-  pipelined_staged<hi_groups<K>()>(T, cval, vaddr, group);
+  pipelined_staged<hi_groups<K>() - FIRST>(T, cval, vaddr, group);
+}
+
+// Top level (b = logK - 1, one group, quads j and j + 8) of the forward
+// transform FFT(K, index) in the high layout, as the encode's shift loop runs
+// it.  Its skew is Cantor(index >> b) = Cantor(2s) at index = sK: linear in s,
+// so the products c_s * X[j + 8] of shift 3 are those of shifts 1 and 2 XORed
+// (the inputs X = M are the same for every shift).  MODE 0: multiply; 1:
+// multiply and keep the products in P; 2: multiply and XOR them into P; 3:
+// take the products from P (no multiply).
+template <int K, int MODE>
+__device__ __forceinline__ void fwd_top(const DevTables& T, const uint32_t* VP, uint32_t index, uint32_t (&L)[16],
+                                        uint32_t (&H)[16], uint32_t (&PL)[8], uint32_t (&PH)[8]) {
+  if constexpr (kExp & 1) return;
+  constexpr int b = Geo<K>::kLog - 1;
+  static_assert(b - 2 - Geo<K>::kLogR == 3, "top level pairs quads j, j + 8");
+  Mult m;
+  if constexpr (MODE != 3) {
+    uint32_t sp[12];
+    spool_of(T, index >> b, sp);
+    m = staged_mult(sp, VP + 8u * vslot<K>(b, 0));
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    uint32_t pl, ph;
+    if constexpr (MODE == 3) {
+      pl = PL[u], ph = PH[u];
+    } else {
+      qmul_set(pl, ph, L[u + 8], H[u + 8], m);
+      if constexpr (MODE == 1) PL[u] = pl, PH[u] = ph;
+      if constexpr (MODE == 2) PL[u] ^= pl, PH[u] ^= ph;
+    }
+    L[u] ^= pl;
+    H[u] ^= ph;
+    L[u + 8] ^= L[u];
+    H[u + 8] ^= H[u];
+  }
 }
 
 // A ^= D_K(X) for one byte plane in the high layout: D(x)[j] = x[j] ^ XOR over

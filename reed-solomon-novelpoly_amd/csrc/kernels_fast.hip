@@ -101,6 +101,7 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
 #pragma unroll
   for (int q = 0; q < 16; ++q) asm volatile("" : "+v"(ML[q]), "+v"(MH[q]));  // materialise M once
 
+  uint32_t PL[8], PH[8];  // top-level products of shift 1, then of shifts 1 ^ 2 (fwd_top)
   for (uint32_t sh = 1; sh < nshift; ++sh) {
     const uint32_t index = sh * K;
     if (index >= a.wanted_n) break;
@@ -111,7 +112,16 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
       XH[q] = MH[q];
     }
     const uint32_t* vp = VP + (sh & 1u) * G::kVPWords;
-    hi_levels<K, false, false>(T, vp, index, XL, XH);
+    if (sh == 1) {
+      fwd_top<K, 1>(T, vp, index, XL, XH, PL, PH);
+    } else if (sh == 2) {
+      fwd_top<K, 2>(T, vp, index, XL, XH, PL, PH);
+    } else if (sh == 3) {
+      fwd_top<K, 3>(T, vp, index, XL, XH, PL, PH);
+    } else {
+      fwd_top<K, 0>(T, vp, index, XL, XH, PL, PH);
+    }
+    hi_levels<K, false, false, 1>(T, vp, index, XL, XH);
     __syncthreads();  // the previous cq pass is done with the tile and with the other table buffer
     if (sh + 1 < nshift && (sh + 1) * K < a.wanted_n)
       stage_vpools<K, G::kThreads>(T, (sh + 1) * K, VP + ((sh + 1) & 1u) * G::kVPWords);

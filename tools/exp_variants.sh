@@ -10,7 +10,7 @@ if [ "$1" != "--run" ]; then
   done
   exit 0
 fi
-for b in 0 1 2 3 4 6 8 16 32 56 57; do
+for b in ${RUNBITS:-0 1 2 3 4 6 8 16 32 56 57}; do
   lib=$PWD/tools/exp/lib_$b.so
   [ $b = 0 ] && lib=$PWD/reed-solomon-novelpoly_amd/lib/libnovelpoly_hip.so
   NP_LIB_PATH=$lib timeout -k 10 120 python bench.py --no-cpu --steps 5 --warmup 2 > gpurun_out/exp_$b.log 2>&1 || true
