@@ -28,6 +28,9 @@
 // + mod.rs:162-239.  The skew of group t at level b and transform index I is
 // the field element with Cantor coordinates 2t + (I >> b)
 // (tests/test_oracle.py::test_skews_are_cantor_points).
+#include <algorithm>
+#include <cstdlib>
+
 #include "fast_common.hpp"
 
 namespace np {
@@ -184,6 +187,12 @@ __device__ __forceinline__ void issue_rows(uint2 (&raw)[16], const uint8_t* sh, 
   }
 }
 
+// Workgroups that decode several tiles of a payload (k_reconstruct_fast
+// `tpw`): K = 256 only; for smaller K the tile loop costs register spills
+// that outweigh the staging it saves.
+template <int K>
+constexpr bool kMultiTile = K == 256;
+
 // Row loads run one step ahead of their use where the registers allow it
 // (prefixes of up to 2 segments); the 4-segment decode, which keeps more
 // state live, loads each step's rows where it uses them.
@@ -197,7 +206,7 @@ constexpr bool kRowPrefetch = NQ <= 2;
 // whose table yields 0 (the reference's skipped multiply).
 template <int K, int NQ>
 __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&msk)[NQ], uint2 (&raw)[16],
-                                             uint32_t (&AL)[16], uint32_t (&AH)[16]) {
+                                             uint32_t (&AL)[16], uint32_t (&AH)[16], bool after_tile) {
   const DevTables& T = c.T;
 #pragma unroll 1
   for (int step = 0; step < NQ; ++step) {
@@ -239,8 +248,8 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
     stamp(c.dbg, 3 + 6 * step);
     cq_levels<K, true, false>(T, vp, index, g, XL, XH);
     stamp(c.dbg, 4 + 6 * step);
-    if (step > 0) {
-      __syncthreads();  // the previous high pass is done with the tile and the other table buffer
+    if (step > 0 || after_tile) {
+      __syncthreads();  // the previous high pass (or tile's copy-out) is done with the tile and the other table buffer
       if (step + 1 < NQ) {
         const int qn = seg_of<NQ>(step + 1);
         stage_vpools<K, Geo<K>::kThreads>(T, static_cast<uint32_t>(qn) * K, c.VP + ((step + 1) & 1) * Geo<K>::kVPWords);
@@ -306,25 +315,7 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
   }
 }
 
-// Decode of one tile from the first NQ segments (NQ * K rows).  The inverse
-// transform of size NQ * K is NQ inverse transforms of size K (index qK)
-// followed by log2(NQ) top levels whose skews at index 0 are 0 (t = 0) or
-// beta = Cantor(2) (t = 1).  Only the first k = K outputs are needed; for them
-//   NQ = 2:  d = D_K(x0) ^ x0 ^ x1
-//   NQ = 4:  d = D_K(x0) ^ x1 ^ x2 ^ beta * (x2 ^ x3)
-// where x_q = IFFT(K, qK)(premultiplied segment q) and D_K is the formal
-// derivative of size K; then out = FFT(K, 0)(d) (the size-n forward transform
-// restricted to its first K outputs is FFT(K, 0): its t = 0 skews are 0).
-// NQ = 1: every systematic row is present, the output is those rows.
-//
-// Decoding from a prefix.  The first NQ * K codeword symbols are the
-// codeword of the same message under the (NQ * K, K) code: the size-n forward
-// transform of the zero-padded coefficients copies its lower half into the
-// upper half at every top level (inc_afft.rs:267-332 with x[i + d] = 0), so its
-// first NQ * K outputs are FFT(NQ * K, 0) of the same coefficients.  A message
-// of K symbols is determined by any K of its codeword symbols, so decoding the
-// prefix with the rows beyond it treated as erased yields the reference's
-// output whenever the prefix holds at least K present rows.
+// Decode of one tile (K < 256: see kMultiTile), as rec_tiles with ntl = 1.
 template <int K, int NQ>
 __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructArgs& a, const uint8_t* sh,
                                          const uint8_t* pres, const uint16_t* loc, const uint16_t* pre_e, uint8_t* smem,
@@ -364,7 +355,7 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
     const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
     uint32_t AL[16], AH[16];
     RecCtx c{T, a.shard_len, tile, E, sh, VP, g, lane, tid, ncols, full, cqb, hb, dbg};
-    rec_segments<K, NQ>(c, msk, raw, AL, AH);
+    rec_segments<K, NQ>(c, msk, raw, AL, AH, false);
     // ---- forward transform of size K at index 0
     const uint32_t* vp0 = VP + ((NQ - 1) & 1) * G::kVPWords;  // segment 0's tables = FFT(K, 0)'s
     stamp(dbg, 26);
@@ -427,28 +418,195 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
   stamp(dbg, 31);
 }
 
-// One workgroup: 256 symbol columns of one batch entry, n = NQ * K.  Without
+// Decode of ntl consecutive tiles of one payload from the first NQ segments (NQ * K rows).  The inverse
+// transform of size NQ * K is NQ inverse transforms of size K (index qK)
+// followed by log2(NQ) top levels whose skews at index 0 are 0 (t = 0) or
+// beta = Cantor(2) (t = 1).  Only the first k = K outputs are needed; for them
+//   NQ = 2:  d = D_K(x0) ^ x0 ^ x1
+//   NQ = 4:  d = D_K(x0) ^ x1 ^ x2 ^ beta * (x2 ^ x3)
+// where x_q = IFFT(K, qK)(premultiplied segment q) and D_K is the formal
+// derivative of size K; then out = FFT(K, 0)(d) (the size-n forward transform
+// restricted to its first K outputs is FFT(K, 0): its t = 0 skews are 0).
+// NQ = 1: every systematic row is present, the output is those rows.
+//
+// Decoding from a prefix.  The first NQ * K codeword symbols are the
+// codeword of the same message under the (NQ * K, K) code: the size-n forward
+// transform of the zero-padded coefficients copies its lower half into the
+// upper half at every top level (inc_afft.rs:267-332 with x[i + d] = 0), so its
+// first NQ * K outputs are FFT(NQ * K, 0) of the same coefficients.  A message
+// of K symbols is determined by any K of its codeword symbols, so decoding the
+// prefix with the rows beyond it treated as erased yields the reference's
+// output whenever the prefix holds at least K present rows.
+template <int K, int NQ>
+__device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructArgs& a, const uint8_t* pres,
+                                          const uint16_t* loc, const uint16_t* pre_e, uint8_t* smem, uint32_t pb,
+                                          uint32_t tl0, uint32_t ntl, uint32_t nsyms) {
+  using G = Geo<K>;
+  constexpr int N = NQ * K;
+  uint8_t* tile = smem;
+  uint32_t* VP = reinterpret_cast<uint32_t*>(smem + G::kTileBytes);  // 2 staged transforms
+  uint16_t* E = reinterpret_cast<uint16_t*>(smem + G::kTileBytes + 8 * G::kVPWords);  // multiplier of every row
+  const uint32_t tid0 = threadIdx.x, g0 = uniform(tid0 >> 6);
+  const bool aligned = ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
+  const uint8_t* shp = a.shards + static_cast<size_t>(pb) * a.batch_stride;
+
+  // presence bits of this wave's rows in every segment of the prefix (the
+  // same for every tile of the payload); the first tile's first-step rows
+  // start loading before the tables are staged
+  uint32_t msk0[NQ];
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) msk0[i] = row_mask16(pres, static_cast<uint32_t>(NQ == 1 ? 0 : seg_of<NQ>(i)) * K + 16 * g0, tid0 & 63u);
+  auto tile_cols = [&](uint32_t tl) __attribute__((always_inline)) {
+    return min(static_cast<uint32_t>(kTile), nsyms - tl * kTile);
+  };
+  uint2 raw[16];
+  if constexpr (kRowPrefetch<NQ>) {
+    const uint32_t nc = tile_cols(tl0);
+    issue_rows(raw, (NQ > 1 && (kExp & 32)) ? T.zeros : shp + 2u * static_cast<size_t>(tl0) * kTile,
+               (NQ > 1 && (kExp & 32)) ? 0 : a.shard_len, msk0[0],
+               static_cast<uint32_t>(NQ == 1 ? 0 : seg_of<NQ>(0)) * K + 16 * g0, T.zeros, tid0 & 63u, nc,
+               nc == kTile && aligned);
+  }
+  if constexpr (NQ > 1) {
+    for (uint32_t v = tid0; v < static_cast<uint32_t>(N); v += G::kThreads) {
+      // mul(x, log m) == x * EXP[m] (inc_log_mul.rs:42-49); the prefix
+      // locator already holds the multipliers (launch_prefix_locator)
+      E[v] = loc ? T.exp[loc[v]] : pre_e[v];
+    }
+    // multiplier tables of the first two segment transforms (indices 2K, 3K or
+    // K, 0): for NQ = 2 these are all the tables, kept for every tile
+    stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(0)) * K, VP);
+    stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(1)) * K, VP + G::kVPWords);
+    __syncthreads();
+  }
+
+#pragma unroll 1
+  for (uint32_t t = 0; t < ntl; ++t) {
+    // per-tile copies the compiler must treat as new: otherwise it hoists the
+    // row offsets, sizes and descriptors derived from them out of the tile loop
+    // and keeps them live in (spilled) registers across it
+    const uint32_t g = fresh(g0);
+    const uint32_t tid = fresh_v(tid0), lane = tid & 63u;
+    const uint32_t cqb = col_base<K>(4 * lane) ^ (32u * g);
+    const size_t shard_len = fresh(a.shard_len);
+    uint32_t msk[NQ];
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) msk[i] = fresh(msk0[i]);
+    const uint32_t tl = tl0 + t, col0 = tl * kTile, ncols = tile_cols(tl);
+    const bool full = ncols == kTile && aligned;
+    const uint8_t* sh = shp + 2u * static_cast<size_t>(col0);
+    uint64_t* dbg = (kExp & 64) ? reinterpret_cast<uint64_t*>(a.out + static_cast<size_t>(pb) * a.out_stride +
+                                                               static_cast<size_t>(nsyms) * 2 * K + 256u * tl)
+                                 : nullptr;
+    stamp(dbg, 0);
+    if constexpr (NQ == 4) {
+      if (t > 0) {  // segment 2's tables were replaced during the previous tile
+        __syncthreads();
+        stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(0)) * K, VP);
+        stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(1)) * K, VP + G::kVPWords);
+        __syncthreads();
+      }
+    }
+    stamp(dbg, 1);
+    uint32_t XL[16], XH[16];
+    if constexpr (NQ > 1) {
+      const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
+      uint32_t AL[16], AH[16];
+      RecCtx c{T, shard_len, tile, E, sh, VP, g, lane, tid, ncols, full, cqb, hb, dbg};
+      rec_segments<K, NQ>(c, msk, raw, AL, AH, t > 0 && NQ == 2);
+      // ---- forward transform of size K at index 0
+      const uint32_t* vp0 = VP + ((NQ - 1) & 1) * G::kVPWords;  // segment 0's tables = FFT(K, 0)'s
+      stamp(dbg, 26);
+      hi_levels<K, false, true>(T, vp0, 0, AL, AH);
+      stamp(dbg, 27);
+      __syncthreads();
+      hi_write<K>(tile, fresh_v(hb), AL, AH);
+      __syncthreads();
+      stamp(dbg, 28);
+      cq_read<K>(tile, fresh_v(cqb), XL, XH);
+      cq_levels<K, false, true>(T, vp0, 0, g, XL, XH);
+      stamp(dbg, 29);
+    }
+    // ---- merge: received systematic rows, postmultiplied recovered ones
+    const uint32_t cqbf = fresh_v(cqb);
+    const uint32_t m0 = uniform(msk[NQ == 1 ? 0 : NQ - 1]);  // segment 0 = the last step's
+    if constexpr (!kRowPrefetch<NQ>) issue_rows(raw, sh, shard_len, m0, 16 * g, T.zeros, lane, ncols, full);
+    if constexpr (NQ == 1) {
+#pragma unroll
+      for (int p = 0; p < 16; ++p) blk_to_quad(raw[p], XL[p], XH[p]);
+    } else {
+      pipelined<16>(
+          T, [&](auto pc) __attribute__((always_inline)) { return uniform(E[16 * g + decltype(pc)::value]); },
+          [&](auto pc, const Mult& pool) __attribute__((always_inline)) {
+            constexpr int x = decltype(pc)::value;
+            // present: the received symbol (mod.rs:225-235); erased: the
+            // postmultiplied recovered symbol (inc_reconstruct.rs:76-84)
+            if ((m0 >> x) & 1u) {
+              blk_to_quad(raw[x], XL[x], XH[x]);
+            } else {
+              const uint32_t l = XL[x], h = XH[x];
+              qmul_set(XL[x], XH[x], l, h, pool);
+            }
+          });
+    }
+    stamp(dbg, 30);
+    // the next tile's first-step rows load during this tile's copy-out
+    if constexpr (kRowPrefetch<NQ>) {
+      if (t + 1 < ntl) {
+        const uint32_t nc = tile_cols(tl + 1);
+        issue_rows(raw, (NQ > 1 && (kExp & 32)) ? T.zeros : sh + 2u * kTile, (NQ > 1 && (kExp & 32)) ? 0 : shard_len,
+                   msk[0], static_cast<uint32_t>(NQ == 1 ? 0 : seg_of<NQ>(0)) * K + 16 * g, T.zeros, lane, nc,
+                   nc == kTile && aligned);
+      }
+    }
+    __syncthreads();
+    cq_write<K>(tile, cqbf, XL, XH);
+    __syncthreads();
+    // ---- copy-out: column c of the tile is 2K contiguous bytes of the output
+    {
+      uint8_t* out = a.out + static_cast<size_t>(pb) * a.out_stride + static_cast<size_t>(col0) * 2 * K;
+      const bool al_o = ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 7u) == 0;
+      const uint32_t c0 = tid / G::Q, q0 = tid % G::Q;
+      const uint32_t base = col_base<K>(c0) ^ (8u * q0);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t c = c0 + 16u * i;
+        if (c >= ncols) break;
+        const uint2 v = *reinterpret_cast<const uint2*>(tile + (base ^ col_base_c<K>(16u * i)));
+        uint8_t* o = out + static_cast<size_t>(c) * 2 * K + 8u * q0;
+        if (al_o) {
+          *reinterpret_cast<uint2*>(o) = v;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = static_cast<uint8_t>((e < 4 ? v.x : v.y) >> (8 * (e & 3)));
+        }
+      }
+    }
+    stamp(dbg, 31);
+  }
+}
+
+// One workgroup: `tpw` consecutive 256-column tiles of one batch entry (the
+// row multipliers and the staged tables of a payload serve all of them, and
+// the next tile's rows load during a tile's copy-out), n = NQ * K.  Without
 // caller locators (a.locators == nullptr) the workgroup decodes from the
 // prefix that k_prefix_locator chose (K, 2K or n rows holding K present rows,
-// rec_tile) with its row multipliers.  Caller locators are over all n rows, so
+// rec_tiles) with its row multipliers.  Caller locators are over all n rows, so
 // they pin the full decode.  An instance serves the payloads whose prefix has
 // at most SERVE segments (SERVE = 2: prefixes of 1 and 2 segments; SERVE = 4:
 // the 4-segment ones only), so each code path gets its own register allocation;
 // for n = 4K the host launches both over the same grid.
 template <int K, int NQ, int SERVE>
 __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void k_reconstruct_fast(
-    DevTables T, ReconstructArgs a, uint32_t nsyms, uint32_t tiles) {
+    DevTables T, ReconstructArgs a, uint32_t nsyms, uint32_t tiles, uint32_t tpw) {
   constexpr int N = NQ * K;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const TileRef tr = tile_of(blockIdx.x, tiles, (a.batch & 7u) == 0);
-  const uint32_t pb = tr.pb, tl = tr.tl;
-  const uint32_t col0 = tl * kTile;
-  const uint32_t ncols = min(static_cast<uint32_t>(kTile), nsyms - col0);
-  const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);
+  const uint32_t groups = (tiles + tpw - 1) / tpw;  // workgroups per batch entry
+  const TileRef tr = tile_of(blockIdx.x, groups, (a.batch & 7u) == 0);
+  const uint32_t pb = tr.pb, tl0 = tr.tl * tpw;
+  const uint32_t ntl = min(tpw, tiles - tl0);
   const uint8_t* pres = a.present + static_cast<size_t>(pb) * N;
   const uint16_t* loc = a.locators ? a.locators + static_cast<size_t>(pb) * N : nullptr;
-  const bool full =
-      ncols == kTile && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
 
   int nq = NQ;
   const uint16_t* pre_e = nullptr;
@@ -457,15 +615,30 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     nq = uniform(rec[0]);
     pre_e = reinterpret_cast<const uint16_t*>(rec + kPrefixHeader);
   }
-  uint64_t* dbg = (kExp & 64) ? reinterpret_cast<uint64_t*>(a.out + static_cast<size_t>(pb) * a.out_stride +
-                                                             static_cast<size_t>(nsyms) * 2 * K + 256u * tl)
-                               : nullptr;
-  if constexpr (SERVE == 4) {
-    if (nq == 4) rec_tile<K, 4>(T, a, sh, pres, loc, pre_e, smem, pb, col0, ncols, full, dbg);
-  } else if (nq == 1) {
-    rec_tile<K, 1>(T, a, sh, pres, loc, pre_e, smem, pb, col0, ncols, full, dbg);
-  } else if (nq == 2) {
-    rec_tile<K, 2>(T, a, sh, pres, loc, pre_e, smem, pb, col0, ncols, full, dbg);
+  if constexpr (kMultiTile<K>) {
+    if constexpr (SERVE == 4) {
+      if (nq == 4) rec_tiles<K, 4>(T, a, pres, loc, pre_e, smem, pb, tl0, ntl, nsyms);
+    } else if (nq == 1) {
+      rec_tiles<K, 1>(T, a, pres, loc, pre_e, smem, pb, tl0, ntl, nsyms);
+    } else if (nq == 2) {
+      rec_tiles<K, 2>(T, a, pres, loc, pre_e, smem, pb, tl0, ntl, nsyms);
+    }
+  } else {  // tpw == 1
+    const uint32_t col0 = tl0 * kTile;
+    const uint32_t ncols = min(static_cast<uint32_t>(kTile), nsyms - col0);
+    const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);
+    const bool full =
+        ncols == kTile && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
+    uint64_t* dbg = (kExp & 64) ? reinterpret_cast<uint64_t*>(a.out + static_cast<size_t>(pb) * a.out_stride +
+                                                               static_cast<size_t>(nsyms) * 2 * K + 256u * tl0)
+                                 : nullptr;
+    if constexpr (SERVE == 4) {
+      if (nq == 4) rec_tile<K, 4>(T, a, sh, pres, loc, pre_e, smem, pb, col0, ncols, full, dbg);
+    } else if (nq == 1) {
+      rec_tile<K, 1>(T, a, sh, pres, loc, pre_e, smem, pb, col0, ncols, full, dbg);
+    } else if (nq == 2) {
+      rec_tile<K, 2>(T, a, sh, pres, loc, pre_e, smem, pb, col0, ncols, full, dbg);
+    }
   }
 }
 
@@ -533,18 +706,28 @@ hipError_t launch_prefix_k(const DevTables& T, const ReconstructArgs& a, uint8_t
   return hipGetLastError();
 }
 
+// Reconstruct workgroups to keep in flight (4 per CU on 256 CUs) before
+// tiles are merged into one workgroup.
+constexpr size_t kRecWorkgroups = 1024;
+
 template <int K, int NQ>
 hipError_t launch_reconstruct_k(const DevTables& T, const ReconstructArgs& a, hipStream_t s) {
   const size_t nsyms = a.shard_len / 2;
   if (nsyms == 0 || a.batch == 0) return hipSuccess;
+  if (nsyms > 0xffffffffu) return hipErrorInvalidValue;
   const uint32_t tiles = static_cast<uint32_t>((nsyms + kTile - 1) / kTile);
-  const size_t blocks = a.batch * tiles;
-  if (blocks > 0x7fffffffu || nsyms > 0xffffffffu) return hipErrorInvalidValue;
+  // tiles per workgroup: as many as keep >= kRecWorkgroups workgroups in flight
+  const size_t all = a.batch * tiles;
+  size_t want = all / kRecWorkgroups;
+  if (const char* e = std::getenv("NP_REC_TPW")) want = std::strtoul(e, nullptr, 10);  // test knob
+  const uint32_t tpw = kMultiTile<K> ? static_cast<uint32_t>(std::max<size_t>(1, std::min<size_t>(tiles, want))) : 1u;
+  const size_t blocks = a.batch * ((tiles + tpw - 1) / tpw);
+  if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
   k_reconstruct_fast<K, NQ, 2><<<static_cast<uint32_t>(blocks), Geo<K>::kThreads, reconstruct_lds_bytes<K, NQ>(), s>>>(
-      T, a, static_cast<uint32_t>(nsyms), tiles);
+      T, a, static_cast<uint32_t>(nsyms), tiles, tpw);
   if constexpr (NQ == 4)
     k_reconstruct_fast<K, NQ, 4><<<static_cast<uint32_t>(blocks), Geo<K>::kThreads, reconstruct_lds_bytes<K, NQ>(), s>>>(
-        T, a, static_cast<uint32_t>(nsyms), tiles);
+        T, a, static_cast<uint32_t>(nsyms), tiles, tpw);
   return hipGetLastError();
 }
 

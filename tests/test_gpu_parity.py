@@ -409,6 +409,43 @@ def test_reconstruct_prefix_modes(gpu, oracle, nw, kw, plen):
         assert want[:plen] == pls[b].tobytes()
 
 
+@pytest.mark.parametrize("tpw,batch", [(2, 8), (3, 8), (4, 5), (8, 8)])
+def test_reconstruct_multi_tile_workgroups(gpu, oracle, monkeypatch, tpw, batch):
+    """k = 256: one workgroup decodes `tpw` consecutive 256-column tiles of a
+    payload (kernels_fast.hip rec_tiles; NP_REC_TPW pins the count the launcher
+    derives from the batch size).  771 symbol columns = 3 full tiles and one of
+    3 columns, so workgroups end on partial tiles and on tile counts that tpw
+    does not divide; every prefix mode, XCD-major and plain workgroup order."""
+    import torch
+
+    monkeypatch.setenv("NP_REC_TPW", str(tpw))
+    p = npa.CodeParams.derive_parameters(1024, 342)
+    n, k = p.n(), p.k()
+    plen = 512 * (3 * 256 + 3) - 5
+    rng = np.random.default_rng(tpw * 31 + batch)
+    pats = _prefix_patterns(n, k, rng)
+    sl = p.make_encoder(gpu).shard_len(plen)
+    assert sl // 2 == 771
+    pls = np.stack([np.frombuffer(synth.payload(7000 + b, plen), dtype=np.uint8) for b in range(batch)])
+    dp = dev(pls)
+    ds = torch.empty((batch, n, sl), dtype=torch.uint8, device="cuda")
+    npa.encode_batch_dev(p, dp.data_ptr(), plen, plen, batch, ds.data_ptr(), n * sl, ctx=gpu, stream=stream())
+    pres = np.stack([pats[b % len(pats)] for b in range(batch)])
+    dpres = dev(pres)
+    olen = (sl // 2) * 2 * k
+    out = torch.empty((batch, olen), dtype=torch.uint8, device="cuda")
+    npa.reconstruct_batch_dev2(p, ds.data_ptr(), sl, n * sl, dpres.data_ptr(), 0, batch, out.data_ptr(), olen,
+                               ctx=gpu, stream=stream())
+    o = host(out)
+    hs = host(ds)
+    for b in range(batch):
+        recv = [hs[b, i].tobytes() if pres[b, i] else None for i in range(n)]
+        st, want = oracle.reconstruct(recv, n, k)
+        assert st == 0
+        assert o[b].tobytes() == want, (b, b % len(pats))
+        assert want[:plen] == pls[b].tobytes()
+
+
 @pytest.mark.parametrize("nw,kw,plen,batch", [(1024, 342, 512 * 300 + 7, 3), (16, 8, 4096, 2), (256, 86, 99, 5),
                                               (4096, 1366, 2048 * 70, 2), (2, 1, 3, 4), (300, 100, 64 * 129, 2)])
 def test_reconstruct_from_systematic_batch_dev(gpu, oracle, nw, kw, plen, batch):
