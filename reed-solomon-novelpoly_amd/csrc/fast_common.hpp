@@ -292,6 +292,22 @@ __device__ __forceinline__ T fresh(T v) {
   return v;
 }
 
+// The table pointers as new values (see fresh): inside a loop over tiles,
+// keeps the compiler from hoisting loads and addresses derived from them
+// (staged tables, pool addresses) out of the loop into live registers.
+__device__ __forceinline__ DevTables fresh_tables(const DevTables& T) {
+  DevTables t = T;
+  t.log = fresh(t.log);
+  t.exp = fresh(t.exp);
+  t.skew = fresh(t.skew);
+  t.skew_add = fresh(t.skew_add);
+  t.log_walsh = fresh(t.log_walsh);
+  t.lw_fold = fresh(t.lw_fold);
+  t.perm_pools = fresh(t.perm_pools);
+  t.zeros = fresh(t.zeros);
+  return t;
+}
+
 // ------------------------------------------------------ byte reshuffles ----
 // 8-byte block (4 big-endian symbols) <-> byte-planar quad.
 __device__ __forceinline__ void blk_to_quad(uint2 d, uint32_t& l, uint32_t& h) {

@@ -136,6 +136,181 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
   }
 }
 
+// ----------------------------------------------------- multi-tile encode ----
+// k = 256: a workgroup encodes `tpw` consecutive tiles of one payload, and the
+// payload blocks of the next tile flow into the LDS tile by LDS-DMA while the
+// last shift's cq levels and row stores of this tile run (the tile is free
+// once every wave has read it back for that last cq pass).  The launch record
+// is re-read from the kernarg segment at every tile, so that none of it stays
+// live in registers across the tile loop.
+template <int K>
+constexpr bool kMultiTile = K == 256;
+
+struct EncLaunch {
+  DevTables T;
+  EncodeArgs a;
+  uint32_t nchunks, tiles, tpw;
+};
+typedef const __attribute__((address_space(4))) EncLaunch* enc_launch_ptr;
+
+// The tile's payload blocks by LDS-DMA, 4 bytes per lane: wave w fills LDS
+// bytes [8 KiB w, 8 KiB (w + 1)) = columns 16w..16w+15, in LDS order; each
+// lane reads the payload dword that the swizzled LDS image holds there
+// (col_base: block m of column c at byte 512c + 8 (m ^ swz(c)) for K = 256).
+template <int K>
+__device__ __forceinline__ void dma_tile(const uint8_t* pay, uint32_t ch0, uint8_t* tile, uint32_t w, uint32_t lane) {
+  static_assert(Geo<K>::P == 1 && Geo<K>::W == Geo<K>::Q, "one swizzle row per column");
+  constexpr uint32_t kColBytes = 2 * K, kPieces = 2 * K / 256;  // 256-byte pieces per column
+  const uint32_t sw0 = swz<K>(16u * w);
+#pragma unroll
+  for (uint32_t j = 0; j < 16 * kPieces; ++j) {
+    const uint32_t c = 16u * w + j / kPieces;                   // column (wave-uniform)
+    const uint32_t sw = sw0 ^ swz<K>(j / kPieces);              // swz(c): linear in c
+    const uint32_t b = (j % kPieces) * 32u + (lane >> 1);       // LDS block of this lane
+    const uint8_t* src = pay + static_cast<size_t>(ch0 + c) * kColBytes + 8u * (b ^ sw) + 4u * (lane & 1u);
+    uint8_t* dst = tile + static_cast<size_t>(c) * kColBytes + 256u * (j % kPieces);
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                     (__attribute__((address_space(3))) void*)(dst), 4, 0, 0);
+  }
+}
+
+// One shift of the encode (rows sK .. sK+K-1).  With `dma_pay`, the last cq
+// pass starts the next tile's payload DMA once every wave has read the tile.
+template <int K>
+__device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArgs& a, uint8_t* tile, uint32_t* VP,
+                                             uint8_t* out, uint32_t sh, uint32_t nshift, uint32_t g, uint32_t lane,
+                                             uint32_t ncols, bool full, uint32_t cqb, uint32_t hb,
+                                             const uint32_t (&ML)[16], const uint32_t (&MH)[16], uint32_t (&PL)[8],
+                                             uint32_t (&PH)[8], const uint8_t* dma_pay, uint32_t dma_ch0) {
+  using G = Geo<K>;
+  const uint32_t index = sh * K;
+  uint32_t XL[16], XH[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    XL[q] = ML[q];
+    XH[q] = MH[q];
+  }
+  const uint32_t* vp = VP + (sh & 1u) * G::kVPWords;
+  if (sh == 1) {
+    fwd_top<K, 1>(T, vp, index, XL, XH, PL, PH);
+  } else if (sh == 2) {
+    fwd_top<K, 2>(T, vp, index, XL, XH, PL, PH);
+  } else if (sh == 3) {
+    fwd_top<K, 3>(T, vp, index, XL, XH, PL, PH);
+  } else {
+    fwd_top<K, 0>(T, vp, index, XL, XH, PL, PH);
+  }
+  hi_levels<K, false, false, 1>(T, vp, index, XL, XH);
+  __syncthreads();  // the previous cq pass is done with the tile and with the other table buffer
+  if (sh + 1 < nshift && (sh + 1) * K < a.wanted_n)
+    stage_vpools<K, G::kThreads>(T, (sh + 1) * K, VP + ((sh + 1) & 1u) * G::kVPWords);
+  hi_write<K>(tile, fresh_v(hb), XL, XH);
+  __syncthreads();
+  cq_read<K>(tile, fresh_v(cqb), XL, XH);
+  if (dma_pay) {
+    __syncthreads();  // every wave has its cq registers: the tile is free
+    dma_tile<K>(dma_pay, dma_ch0, tile, g, lane);
+  }
+  cq_levels<K, false, false>(T, vp, index, g, XL, XH);
+  store_rows(out, a.shard_len, index + 16 * g, a.wanted_n, XL, XH, lane, ncols, full);
+}
+
+// One tile; returns whether the next tile's payload is on its way by DMA.
+template <int K>
+__device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const EncodeArgs& a, uint8_t* smem, uint32_t pb,
+                                                  uint32_t tl, uint32_t nchunks, bool have_dma, uint32_t next_tl) {
+  using G = Geo<K>;
+  uint8_t* tile = smem;
+  uint32_t* VP = reinterpret_cast<uint32_t*>(smem + G::kTileBytes);  // 2 staged transforms
+  const uint32_t ch0 = tl * kTile;
+  const uint32_t ncols = min(static_cast<uint32_t>(kTile), nchunks - ch0);
+  const uint8_t* pay = a.payloads + static_cast<size_t>(pb) * a.payload_stride;
+  uint8_t* out = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(ch0);
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, g = uniform(tid >> 6);
+  const bool full =
+      ncols == kTile && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
+  const bool aligned_pay = (reinterpret_cast<uintptr_t>(pay) & 7u) == 0;
+  auto tile_fast = [&](uint32_t t) __attribute__((always_inline)) {
+    return aligned_pay && static_cast<size_t>(t * kTile + kTile) * 2 * K <= a.payload_len;
+  };
+  if (have_dma) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces have landed
+  } else {
+    const uint32_t c0 = tid / G::Q, m0 = tid % G::Q;
+    const uint32_t base = col_base<K>(c0) ^ (8u * m0);
+    const size_t gbase = static_cast<size_t>(ch0 + c0) * 2 * K + 8u * m0;
+    if (tile_fast(tl)) {
+      uint2 v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = *reinterpret_cast<const uint2*>(pay + gbase + static_cast<size_t>(i) * 32 * K);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) *reinterpret_cast<uint2*>(tile + (base ^ col_base_c<K>(16u * i))) = v[i];
+    } else {
+#pragma unroll 1
+      for (uint32_t i = 0; i < 16; ++i) {
+        const size_t g0 = gbase + static_cast<size_t>(i) * 32 * K;
+        uint32_t w[2] = {0, 0};
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (g0 + e < a.payload_len) w[e >> 2] |= static_cast<uint32_t>(pay[g0 + e]) << (8 * (e & 3));
+        *reinterpret_cast<uint2*>(tile + (base ^ col_base_c<K>(16u * i))) = make_uint2(w[0], w[1]);
+      }
+    }
+  }
+  const uint32_t nshift = a.n / K;
+  const uint32_t last = min(nshift, (a.wanted_n + K - 1) / K) - 1;  // last shift with wanted rows
+  stage_vpools<K, G::kThreads>(T, 0, VP);                              // inverse transform, index 0
+  if (nshift > 1) stage_vpools<K, G::kThreads>(T, K, VP + G::kVPWords);  // first shift
+  __syncthreads();
+
+  const uint32_t cqb = col_base<K>(4 * lane) ^ (32u * g);
+  {
+    uint32_t CL[16], CH[16];
+    cq_read<K>(tile, cqb, CL, CH);
+    store_rows(out, a.shard_len, 16 * g, a.wanted_n, CL, CH, lane, ncols, full);
+    cq_levels<K, true, true>(T, VP, 0, g, CL, CH);
+    cq_write<K>(tile, cqb, CL, CH);
+  }
+  __syncthreads();
+  const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
+  uint32_t ML[16], MH[16];
+  hi_read<K>(tile, hb, ML, MH);
+  hi_levels<K, true, true>(T, VP, 0, ML, MH);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) asm volatile("" : "+v"(ML[q]), "+v"(MH[q]));  // materialise M once
+  uint32_t PL[8], PH[8];
+#pragma unroll 1
+  for (uint32_t sh = 1; sh < last; ++sh)
+    encode_shift<K>(T, a, tile, VP, out, sh, nshift, g, lane, ncols, full, cqb, hb, ML, MH, PL, PH, nullptr, 0);
+  const bool dma = last >= 1 && next_tl != ~0u && tile_fast(next_tl);
+  if (last >= 1)
+    encode_shift<K>(T, a, tile, VP, out, last, nshift, g, lane, ncols, full, cqb, hb, ML, MH, PL, PH,
+                    dma ? pay : nullptr, next_tl * kTile);
+  return dma;
+}
+
+template <int K>
+__global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_multi(EncLaunch L) {
+#if defined(__HIP_DEVICE_COMPILE__)  // (the host pass cannot bind the kernarg-segment record to references)
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t groups = (L.tiles + L.tpw - 1) / L.tpw;  // workgroups per batch entry
+  const TileRef tr = tile_of(blockIdx.x, groups, (L.a.batch & 7u) == 0);
+  const uint32_t pb = tr.pb, tl0 = tr.tl * L.tpw;
+  const uint32_t ntl = min(L.tpw, L.tiles - tl0);
+  const uint64_t kp = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());
+  bool dma = false;
+#pragma unroll 1
+  for (uint32_t t = 0; t < ntl; ++t) {
+    if (t > 0) __syncthreads();  // the previous tile's last cq pass is done with the tables
+    const enc_launch_ptr lp = reinterpret_cast<enc_launch_ptr>(fresh(kp));
+    const DevTables T = lp->T;
+    const EncodeArgs a = lp->a;
+    dma = encode_tile_multi<K>(T, a, smem, fresh(pb), fresh(tl0) + t, lp->nchunks, dma,
+                               t + 1 < ntl ? tl0 + t + 1 : ~0u);
+  }
+#endif
+}
+
 // ------------------------------------------------------------ reconstruct ----
 struct RecCtx {
   const DevTables& T;
@@ -187,11 +362,23 @@ __device__ __forceinline__ void issue_rows(uint2 (&raw)[16], const uint8_t* sh, 
   }
 }
 
-// Workgroups that decode several tiles of a payload (k_reconstruct_fast
-// `tpw`): K = 256 only; for smaller K the tile loop costs register spills
-// that outweigh the staging it saves.
+// Copy-out straight from the cq registers: lane l holds columns 4l..4l+3 at
+// positions 16g..16g+15, i.e. bytes [32g, 32g + 32) of each of those four
+// 2K-byte output columns (two 16-byte stores per column).  Full tiles with
+// 16-byte aligned output only; saves the LDS round trip and its two barriers.
 template <int K>
-constexpr bool kMultiTile = K == 256;
+__device__ __forceinline__ void copy_out_cq(uint8_t* out_tile, uint32_t lane, uint32_t g, const uint32_t (&L)[16],
+                                            const uint32_t (&H)[16]) {
+  uint2 d[4][4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) cq_to_blks(&L[4 * u], &H[4 * u], d[u]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    uint8_t* o = out_tile + static_cast<size_t>(4u * lane + i) * 2 * K + 32u * g;
+    *reinterpret_cast<uint4*>(o) = make_uint4(d[0][i].x, d[0][i].y, d[1][i].x, d[1][i].y);
+    *reinterpret_cast<uint4*>(o + 16) = make_uint4(d[2][i].x, d[2][i].y, d[3][i].x, d[3][i].y);
+  }
+}
 
 // Row loads run one step ahead of their use where the registers allow it
 // (prefixes of up to 2 segments); the 4-segment decode, which keeps more
@@ -392,6 +579,11 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
         });
   }
   stamp(dbg, 30);
+  if (full && ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 15u) == 0) {
+    copy_out_cq<K>(a.out + static_cast<size_t>(pb) * a.out_stride + static_cast<size_t>(col0) * 2 * K, lane, g, XL, XH);
+    stamp(dbg, 31);
+    return;
+  }
   __syncthreads();
   cq_write<K>(tile, cqbf, XL, XH);
   __syncthreads();
@@ -559,6 +751,12 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
                    nc == kTile && aligned);
       }
     }
+    if (full && ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 15u) == 0) {
+      copy_out_cq<K>(a.out + static_cast<size_t>(pb) * a.out_stride + static_cast<size_t>(col0) * 2 * K, lane, g, XL,
+                     XH);
+      stamp(dbg, 31);
+      continue;
+    }
     __syncthreads();
     cq_write<K>(tile, cqbf, XL, XH);
     __syncthreads();
@@ -686,15 +884,35 @@ size_t reconstruct_lds_bytes() {
   return static_cast<size_t>(Geo<K>::kTileBytes) + 2u * 4u * Geo<K>::kVPWords + 2u * 4 * K;
 }
 
+// Tiles per workgroup (kMultiTile): as many as keep >= kWorkgroups
+// workgroups (4 per CU on 256 CUs) in the grid.  `knob` names an environment
+// variable that pins the count (tests).
+constexpr size_t kWorkgroups = 1024;
+
+template <int K>
+uint32_t tiles_per_workgroup(size_t batch, uint32_t tiles, const char* knob) {
+  if (!kMultiTile<K>) return 1;
+  size_t want = batch * tiles / kWorkgroups;
+  if (const char* e = std::getenv(knob)) want = std::strtoul(e, nullptr, 10);
+  return static_cast<uint32_t>(std::max<size_t>(1, std::min<size_t>(tiles, want)));
+}
+
 template <int K>
 hipError_t launch_encode_k(const DevTables& T, const EncodeArgs& a, hipStream_t s) {
   const size_t nchunks = (a.payload_len + 2 * a.k - 1) / (2 * a.k);
   if (nchunks == 0 || a.batch == 0) return hipSuccess;
+  if (nchunks > 0xffffffffu) return hipErrorInvalidValue;
   const uint32_t tiles = static_cast<uint32_t>((nchunks + kTile - 1) / kTile);
-  const size_t blocks = a.batch * tiles;
-  if (blocks > 0x7fffffffu || nchunks > 0xffffffffu) return hipErrorInvalidValue;
-  k_encode_fast<K><<<static_cast<uint32_t>(blocks), Geo<K>::kThreads, encode_lds_bytes<K>(), s>>>(
-      T, a, static_cast<uint32_t>(nchunks), tiles);
+  const uint32_t tpw = tiles_per_workgroup<K>(a.batch, tiles, "NP_ENC_TPW");
+  const size_t blocks = a.batch * ((tiles + tpw - 1) / tpw);
+  if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
+  if constexpr (kMultiTile<K>) {
+    k_encode_multi<K><<<static_cast<uint32_t>(blocks), Geo<K>::kThreads, encode_lds_bytes<K>(), s>>>(
+        EncLaunch{T, a, static_cast<uint32_t>(nchunks), tiles, tpw});
+  } else {
+    k_encode_fast<K><<<static_cast<uint32_t>(blocks), Geo<K>::kThreads, encode_lds_bytes<K>(), s>>>(
+        T, a, static_cast<uint32_t>(nchunks), tiles);
+  }
   return hipGetLastError();
 }
 
@@ -706,21 +924,13 @@ hipError_t launch_prefix_k(const DevTables& T, const ReconstructArgs& a, uint8_t
   return hipGetLastError();
 }
 
-// Reconstruct workgroups to keep in flight (4 per CU on 256 CUs) before
-// tiles are merged into one workgroup.
-constexpr size_t kRecWorkgroups = 1024;
-
 template <int K, int NQ>
 hipError_t launch_reconstruct_k(const DevTables& T, const ReconstructArgs& a, hipStream_t s) {
   const size_t nsyms = a.shard_len / 2;
   if (nsyms == 0 || a.batch == 0) return hipSuccess;
   if (nsyms > 0xffffffffu) return hipErrorInvalidValue;
   const uint32_t tiles = static_cast<uint32_t>((nsyms + kTile - 1) / kTile);
-  // tiles per workgroup: as many as keep >= kRecWorkgroups workgroups in flight
-  const size_t all = a.batch * tiles;
-  size_t want = all / kRecWorkgroups;
-  if (const char* e = std::getenv("NP_REC_TPW")) want = std::strtoul(e, nullptr, 10);  // test knob
-  const uint32_t tpw = kMultiTile<K> ? static_cast<uint32_t>(std::max<size_t>(1, std::min<size_t>(tiles, want))) : 1u;
+  const uint32_t tpw = tiles_per_workgroup<K>(a.batch, tiles, "NP_REC_TPW");
   const size_t blocks = a.batch * ((tiles + tpw - 1) / tpw);
   if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
   k_reconstruct_fast<K, NQ, 2><<<static_cast<uint32_t>(blocks), Geo<K>::kThreads, reconstruct_lds_bytes<K, NQ>(), s>>>(
@@ -780,7 +990,7 @@ hipError_t configure_fast_kernels() {
   };
   set(reinterpret_cast<const void*>(&k_encode_fast<64>), encode_lds_bytes<64>());
   set(reinterpret_cast<const void*>(&k_encode_fast<128>), encode_lds_bytes<128>());
-  set(reinterpret_cast<const void*>(&k_encode_fast<256>), encode_lds_bytes<256>());
+  set(reinterpret_cast<const void*>(&k_encode_multi<256>), encode_lds_bytes<256>());
   set(reinterpret_cast<const void*>(&k_reconstruct_fast<64, 2, 2>), reconstruct_lds_bytes<64, 2>());
   set(reinterpret_cast<const void*>(&k_reconstruct_fast<64, 4, 2>), reconstruct_lds_bytes<64, 4>());
   set(reinterpret_cast<const void*>(&k_reconstruct_fast<64, 4, 4>), reconstruct_lds_bytes<64, 4>());

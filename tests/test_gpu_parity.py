@@ -409,6 +409,38 @@ def test_reconstruct_prefix_modes(gpu, oracle, nw, kw, plen):
         assert want[:plen] == pls[b].tobytes()
 
 
+@pytest.mark.parametrize("nw,tpw,batch,stride_pad", [(1024, 2, 8, 0), (1024, 3, 8, 0), (1024, 4, 5, 0),
+                                                     (700, 4, 8, 0), (1024, 4, 8, 1), (2048, 3, 3, 0)])
+def test_encode_multi_tile_workgroups(gpu, oracle, monkeypatch, nw, tpw, batch, stride_pad):
+    """k = 256: one workgroup encodes `tpw` consecutive tiles of a payload and
+    the next tile's payload arrives by LDS-DMA during the last shift
+    (kernels_fast.hip k_encode_multi; NP_ENC_TPW pins the tile count).  771
+    chunks = 3 full tiles and a partial one (loaded without DMA); wanted_n < n
+    ends on an earlier shift; an odd payload stride takes the byte path; n = 8k
+    runs shifts past the shared top-level products."""
+    import torch
+
+    monkeypatch.setenv("NP_ENC_TPW", str(tpw))
+    p = npa.CodeParams.derive_parameters(nw, 342)
+    n, k = p.n(), p.k()
+    assert k == 256
+    plen = 512 * (3 * 256 + 3) - 5
+    stride = plen + stride_pad
+    sl = p.make_encoder(gpu).shard_len(plen)
+    pls = np.zeros((batch, stride), np.uint8)
+    for b in range(batch):
+        pls[b, :plen] = np.frombuffer(synth.payload(9000 + b, plen), dtype=np.uint8)
+    dp = dev(pls)
+    ds = torch.zeros((batch, n, sl), dtype=torch.uint8, device="cuda")
+    npa.encode_batch_dev(p, dp.data_ptr(), plen, stride, batch, ds.data_ptr(), n * sl, ctx=gpu, stream=stream())
+    hs = host(ds)
+    for b in range(batch):
+        st, want = oracle.encode(pls[b, :plen].tobytes(), n, k, nw)
+        assert st == 0
+        bad = [v for v in range(nw) if hs[b, v].tobytes() != want[v]]
+        assert not bad, (b, len(bad), bad[:5])
+
+
 @pytest.mark.parametrize("tpw,batch", [(2, 8), (3, 8), (4, 5), (8, 8)])
 def test_reconstruct_multi_tile_workgroups(gpu, oracle, monkeypatch, tpw, batch):
     """k = 256: one workgroup decodes `tpw` consecutive 256-column tiles of a
