@@ -146,6 +146,12 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
 template <int K>
 constexpr bool kMultiTile = K == 256;
 
+// Table buffers of the multi-tile encode: the inverse transform's and one per
+// shift, staged once per workgroup (n <= 4K); with the 128 KiB tile they fill
+// the 160 KiB of LDS.  Table loads inside the tile loop would wait (vmcnt
+// counts in order) for the row stores issued before them.
+constexpr int kEncBuffers = 4;
+
 struct EncLaunch {
   DevTables T;
   EncodeArgs a;
@@ -157,20 +163,29 @@ typedef const __attribute__((address_space(4))) EncLaunch* enc_launch_ptr;
 // bytes [8 KiB w, 8 KiB (w + 1)) = columns 16w..16w+15, in LDS order; each
 // lane reads the payload dword that the swizzled LDS image holds there
 // (col_base: block m of column c at byte 512c + 8 (m ^ swz(c)) for K = 256).
+// Written as asm (M0 = the piece's LDS address, set in the same statement,
+// cdna_hip_programming.md §5.7): hipcc then adds no vmcnt(0) of its own
+// before the next LDS reads, which would also wait for the row stores issued
+// after these loads; encode_tile_multi waits with a counted vmcnt instead.
 template <int K>
 __device__ __forceinline__ void dma_tile(const uint8_t* pay, uint32_t ch0, uint8_t* tile, uint32_t w, uint32_t lane) {
   static_assert(Geo<K>::P == 1 && Geo<K>::W == Geo<K>::Q, "one swizzle row per column");
   constexpr uint32_t kColBytes = 2 * K, kPieces = 2 * K / 256;  // 256-byte pieces per column
   const uint32_t sw0 = swz<K>(16u * w);
+  const uint32_t lds0 = static_cast<uint32_t>(
+      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)(tile)));
 #pragma unroll
   for (uint32_t j = 0; j < 16 * kPieces; ++j) {
     const uint32_t c = 16u * w + j / kPieces;                   // column (wave-uniform)
     const uint32_t sw = sw0 ^ swz<K>(j / kPieces);              // swz(c): linear in c
     const uint32_t b = (j % kPieces) * 32u + (lane >> 1);       // LDS block of this lane
     const uint8_t* src = pay + static_cast<size_t>(ch0 + c) * kColBytes + 8u * (b ^ sw) + 4u * (lane & 1u);
-    uint8_t* dst = tile + static_cast<size_t>(c) * kColBytes + 256u * (j % kPieces);
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
-                                     (__attribute__((address_space(3))) void*)(dst), 4, 0, 0);
+    const uint32_t dst = uniform(lds0 + c * kColBytes + 256u * (j % kPieces));
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(dst)
+                 : "memory");
   }
 }
 
@@ -190,7 +205,7 @@ __device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArg
     XL[q] = ML[q];
     XH[q] = MH[q];
   }
-  const uint32_t* vp = VP + (sh & 1u) * G::kVPWords;
+  const uint32_t* vp = VP + sh * G::kVPWords;  // the tables of every shift stay staged (kEncBuffers)
   if (sh == 1) {
     fwd_top<K, 1>(T, vp, index, XL, XH, PL, PH);
   } else if (sh == 2) {
@@ -201,24 +216,23 @@ __device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArg
     fwd_top<K, 0>(T, vp, index, XL, XH, PL, PH);
   }
   hi_levels<K, false, false, 1>(T, vp, index, XL, XH);
-  __syncthreads();  // the previous cq pass is done with the tile and with the other table buffer
-  if (sh + 1 < nshift && (sh + 1) * K < a.wanted_n)
-    stage_vpools<K, G::kThreads>(T, (sh + 1) * K, VP + ((sh + 1) & 1u) * G::kVPWords);
+  __syncthreads();  // the previous cq pass is done with the tile
   hi_write<K>(tile, fresh_v(hb), XL, XH);
   __syncthreads();
   cq_read<K>(tile, fresh_v(cqb), XL, XH);
   if (dma_pay) {
     __syncthreads();  // every wave has its cq registers: the tile is free
-    dma_tile<K>(dma_pay, dma_ch0, tile, g, lane);
+    if constexpr (!(kExp & 4)) dma_tile<K>(dma_pay, dma_ch0, tile, g, lane);
   }
   cq_levels<K, false, false>(T, vp, index, g, XL, XH);
-  store_rows(out, a.shard_len, index + 16 * g, a.wanted_n, XL, XH, lane, ncols, full);
+  store_rows(out, a.shard_len, index + 16 * g, (kExp & 2) ? 0u : a.wanted_n, XL, XH, lane, ncols, full);
 }
 
 // One tile; returns whether the next tile's payload is on its way by DMA.
 template <int K>
 __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const EncodeArgs& a, uint8_t* smem, uint32_t pb,
-                                                  uint32_t tl, uint32_t nchunks, bool have_dma, uint32_t next_tl) {
+                                                  uint32_t tl, uint32_t nchunks, bool first, bool have_dma,
+                                                  bool stored16, uint32_t next_tl) {
   using G = Geo<K>;
   uint8_t* tile = smem;
   uint32_t* VP = reinterpret_cast<uint32_t*>(smem + G::kTileBytes);  // 2 staged transforms
@@ -234,7 +248,12 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
     return aligned_pay && static_cast<size_t>(t * kTile + kTile) * 2 * K <= a.payload_len;
   };
   if (have_dma) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces have landed
+    // this wave's DMA pieces have landed; the previous tile's last 16 row
+    // stores, issued after them, may still be in flight
+    if (stored16)
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else {
     const uint32_t c0 = tid / G::Q, m0 = tid % G::Q;
     const uint32_t base = col_base<K>(c0) ^ (8u * m0);
@@ -242,7 +261,8 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
     if (tile_fast(tl)) {
       uint2 v[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = *reinterpret_cast<const uint2*>(pay + gbase + static_cast<size_t>(i) * 32 * K);
+      for (int i = 0; i < 16; ++i)
+        v[i] = (kExp & 4) ? make_uint2(i, tid) : *reinterpret_cast<const uint2*>(pay + gbase + static_cast<size_t>(i) * 32 * K);
 #pragma unroll
       for (int i = 0; i < 16; ++i) *reinterpret_cast<uint2*>(tile + (base ^ col_base_c<K>(16u * i))) = v[i];
     } else {
@@ -259,15 +279,16 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
   }
   const uint32_t nshift = a.n / K;
   const uint32_t last = min(nshift, (a.wanted_n + K - 1) / K) - 1;  // last shift with wanted rows
-  stage_vpools<K, G::kThreads>(T, 0, VP);                              // inverse transform, index 0
-  if (nshift > 1) stage_vpools<K, G::kThreads>(T, K, VP + G::kVPWords);  // first shift
+  if (first) {  // tables of the inverse transform (index 0) and of every shift, kept for all tiles
+    for (uint32_t sh = 0; sh <= last; ++sh) stage_vpools<K, G::kThreads>(T, sh * K, VP + sh * G::kVPWords);
+  }
   __syncthreads();
 
   const uint32_t cqb = col_base<K>(4 * lane) ^ (32u * g);
   {
     uint32_t CL[16], CH[16];
     cq_read<K>(tile, cqb, CL, CH);
-    store_rows(out, a.shard_len, 16 * g, a.wanted_n, CL, CH, lane, ncols, full);
+    store_rows(out, a.shard_len, 16 * g, (kExp & 2) ? 0u : a.wanted_n, CL, CH, lane, ncols, full);
     cq_levels<K, true, true>(T, VP, 0, g, CL, CH);
     cq_write<K>(tile, cqb, CL, CH);
   }
@@ -305,7 +326,12 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     const enc_launch_ptr lp = reinterpret_cast<enc_launch_ptr>(fresh(kp));
     const DevTables T = lp->T;
     const EncodeArgs a = lp->a;
-    dma = encode_tile_multi<K>(T, a, smem, fresh(pb), fresh(tl0) + t, lp->nchunks, dma,
+    // the previous tile's last shift stored 16 rows per wave (store_rows' full path)
+    const uint32_t pch0 = (tl0 + t - 1) * kTile;
+    const bool stored16 = t > 0 && pch0 + kTile <= lp->nchunks &&
+                          ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0 &&
+                          (min(a.n / K, (a.wanted_n + K - 1) / K) - 1) * K + 16 * 16 <= a.wanted_n;
+    dma = encode_tile_multi<K>(T, a, smem, fresh(pb), fresh(tl0) + t, lp->nchunks, t == 0, dma, stored16,
                                t + 1 < ntl ? tl0 + t + 1 : ~0u);
   }
 #endif
@@ -878,6 +904,11 @@ size_t encode_lds_bytes() {
   return static_cast<size_t>(Geo<K>::kTileBytes) + 2u * 4u * Geo<K>::kVPWords;
 }
 
+template <int K>
+size_t encode_multi_lds_bytes() {
+  return static_cast<size_t>(Geo<K>::kTileBytes) + kEncBuffers * 4u * Geo<K>::kVPWords;
+}
+
 
 template <int K, int NQ>
 size_t reconstruct_lds_bytes() {
@@ -903,16 +934,18 @@ hipError_t launch_encode_k(const DevTables& T, const EncodeArgs& a, hipStream_t 
   if (nchunks == 0 || a.batch == 0) return hipSuccess;
   if (nchunks > 0xffffffffu) return hipErrorInvalidValue;
   const uint32_t tiles = static_cast<uint32_t>((nchunks + kTile - 1) / kTile);
-  const uint32_t tpw = tiles_per_workgroup<K>(a.batch, tiles, "NP_ENC_TPW");
+  const uint32_t tpw = a.n <= kEncBuffers * K ? tiles_per_workgroup<K>(a.batch, tiles, "NP_ENC_TPW") : 1u;
   const size_t blocks = a.batch * ((tiles + tpw - 1) / tpw);
   if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
   if constexpr (kMultiTile<K>) {
-    k_encode_multi<K><<<static_cast<uint32_t>(blocks), Geo<K>::kThreads, encode_lds_bytes<K>(), s>>>(
-        EncLaunch{T, a, static_cast<uint32_t>(nchunks), tiles, tpw});
-  } else {
-    k_encode_fast<K><<<static_cast<uint32_t>(blocks), Geo<K>::kThreads, encode_lds_bytes<K>(), s>>>(
-        T, a, static_cast<uint32_t>(nchunks), tiles);
+    if (a.n <= kEncBuffers * K) {
+      k_encode_multi<K><<<static_cast<uint32_t>(blocks), Geo<K>::kThreads, encode_multi_lds_bytes<K>(), s>>>(
+          EncLaunch{T, a, static_cast<uint32_t>(nchunks), tiles, tpw});
+      return hipGetLastError();
+    }
   }
+  k_encode_fast<K><<<static_cast<uint32_t>(blocks), Geo<K>::kThreads, encode_lds_bytes<K>(), s>>>(
+      T, a, static_cast<uint32_t>(nchunks), tiles);
   return hipGetLastError();
 }
 
@@ -990,7 +1023,8 @@ hipError_t configure_fast_kernels() {
   };
   set(reinterpret_cast<const void*>(&k_encode_fast<64>), encode_lds_bytes<64>());
   set(reinterpret_cast<const void*>(&k_encode_fast<128>), encode_lds_bytes<128>());
-  set(reinterpret_cast<const void*>(&k_encode_multi<256>), encode_lds_bytes<256>());
+  set(reinterpret_cast<const void*>(&k_encode_fast<256>), encode_lds_bytes<256>());
+  set(reinterpret_cast<const void*>(&k_encode_multi<256>), encode_multi_lds_bytes<256>());
   set(reinterpret_cast<const void*>(&k_reconstruct_fast<64, 2, 2>), reconstruct_lds_bytes<64, 2>());
   set(reinterpret_cast<const void*>(&k_reconstruct_fast<64, 4, 2>), reconstruct_lds_bytes<64, 4>());
   set(reinterpret_cast<const void*>(&k_reconstruct_fast<64, 4, 4>), reconstruct_lds_bytes<64, 4>());
