@@ -330,7 +330,8 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     const uint32_t pch0 = (tl0 + t - 1) * kTile;
     const bool stored16 = t > 0 && pch0 + kTile <= lp->nchunks &&
                           ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0 &&
-                          (min(a.n / K, (a.wanted_n + K - 1) / K) - 1) * K + 16 * 16 <= a.wanted_n;
+                          (min(a.n / K, (a.wanted_n + K - 1) / K) - 1) * K + 16 * 16 <= a.wanted_n &&
+                          16 * a.shard_len < 0x7fffffffu;
     dma = encode_tile_multi<K>(T, a, smem, fresh(pb), fresh(tl0) + t, lp->nchunks, t == 0, dma, stored16,
                                t + 1 < ntl ? tl0 + t + 1 : ~0u);
   }
