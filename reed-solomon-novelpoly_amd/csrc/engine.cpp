@@ -201,9 +201,9 @@ hipError_t launch_encode(np_ctx* c, const np::EncodeArgs& a, hipStream_t s) {
 // context lock.
 hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream_t s) {
   if (np::fast_reconstruct_supported(a.n, a.k)) {
-    if (a.locators) return np::launch_reconstruct_fast(c->T, a, s);
-    // per-payload decode prefix + row multipliers, then the decode; batches
-    // larger than the scratch cap go in slices
+    // per-payload decode prefix + row multipliers and their tables (from the
+    // caller's locators when given), then the decode; batches larger than the
+    // scratch cap go in slices
     const size_t stride = np::prefix_stride(a.n, a.k);
     const size_t per = std::max<size_t>(1, kBigScratchCap / stride);
     for (size_t b0 = 0; b0 < a.batch; b0 += per) {
@@ -211,6 +211,7 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
       sub.batch = std::min(per, a.batch - b0);
       sub.shards = a.shards + b0 * a.batch_stride;
       sub.present = a.present + b0 * a.n;
+      if (a.locators) sub.locators = a.locators + b0 * a.n;
       sub.out = a.out + b0 * a.out_stride;
       uint8_t* scr = nullptr;
       size_t bytes = 0;

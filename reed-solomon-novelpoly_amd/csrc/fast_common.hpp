@@ -31,12 +31,19 @@ __device__ __forceinline__ void stamp(uint64_t* dbg, int slot) {
 }
 constexpr int kPoolWords = 20;
 
-// Prefix-locator record of one payload (k_prefix_locator): header (byte 0 =
-// prefix segments) then one u16 row multiplier per row of the prefix.
+// Prefix-locator record of one payload (k_prefix_locator, k_locator_records):
+// header (byte 0 = prefix segments), one u16 row multiplier per row, then the
+// v_perm tables (kPoolWords dwords, field_tables.cpp) of every row's
+// multiplier, contiguous: the decode reads one 80-byte record per row and
+// tile from a 40-80 KiB block instead of from the 5 MiB pool table, where the
+// tiles of a payload would fetch the same scattered records again from HBM.
 constexpr uint32_t kPrefixHeader = 16;
+__host__ __device__ constexpr size_t prefix_pools_offset(uint32_t n) {
+  return (kPrefixHeader + 2u * static_cast<size_t>(n) + 15u) & ~static_cast<size_t>(15);
+}
 __host__ __device__ constexpr size_t prefix_stride_c(uint32_t n, uint32_t k) {
   (void)k;
-  return (kPrefixHeader + 2u * static_cast<size_t>(n) + 15u) & ~static_cast<size_t>(15);
+  return prefix_pools_offset(n) + 4u * kPoolWords * static_cast<size_t>(n);
 }
 
 __host__ __device__ constexpr int ilog2(int v) {
@@ -449,6 +456,34 @@ __device__ __forceinline__ void pipelined(const DevTables& T, CF cval, GF group)
   uint32_t pa[20], pb[20];
   pool_of(T, cval(Int<0>{}), pa);
   pipe_step<0, NG>(T, cval, group, pa, pb);
+}
+
+// Same with group f's tables at rec(Int<f>) (a wave-uniform global address).
+__device__ __forceinline__ void pool_at(cpool_t q, uint32_t (&p)[20]) {
+#pragma unroll
+  for (int i = 0; i < 20; ++i) p[i] = q[i];
+}
+
+// need(f) (wave-uniform): group f multiplies; the tables of the others are
+// not fetched (their group must not use the multiplier).
+template <int F, int NG, typename RF, typename NF, typename GF>
+__device__ __forceinline__ void rpipe_step(RF& rec, NF& need, GF& group, uint32_t (&cur)[20], uint32_t (&nxt)[20]) {
+  if constexpr (F < NG) {
+    if constexpr (F + 1 < NG) {
+      if (need(Int<F + 1>{})) pool_at(rec(Int<F + 1>{}), nxt);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    group(Int<F>{}, make_mult(cur));
+    __builtin_amdgcn_sched_barrier(0);
+    rpipe_step<F + 1, NG>(rec, need, group, nxt, cur);
+  }
+}
+
+template <int NG, typename RF, typename NF, typename GF>
+__device__ __forceinline__ void pipelined_rec(RF rec, NF need, GF group) {
+  uint32_t pa[20], pb[20];
+  if (need(Int<0>{})) pool_at(rec(Int<0>{}), pa);
+  rpipe_step<0, NG>(rec, need, group, pa, pb);
 }
 
 // Same for a transform whose VGPR table halves are staged in LDS (VP, see

@@ -343,7 +343,7 @@ struct RecCtx {
   const DevTables& T;
   size_t shard_len;
   uint8_t* tile;
-  const uint16_t* E;
+  const uint32_t* R;  // row table records of the payload (prefix record)
   const uint8_t* sh;
   uint32_t* VP;  // 2 staged transforms
   uint32_t g, lane, tid, ncols;
@@ -429,7 +429,7 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
     __builtin_amdgcn_sched_barrier(0);
     const uint32_t g = fresh(c.g);
     const uint8_t* sh = fresh(c.sh);
-    const uint16_t* E = fresh(c.E);
+    const uint32_t* R = fresh(c.R);
     const size_t shard_len = fresh(c.shard_len);
     const uint32_t cqb = fresh_v(c.cqb), hb = fresh_v(c.hb);
     uint32_t m = msk[0];
@@ -441,8 +441,11 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
                  c.ncols, c.full);
     uint32_t XL[16], XH[16];
     stamp(c.dbg, 2 + 6 * step);
-    pipelined<16>(
-        T, [&](auto pc) __attribute__((always_inline)) { return uniform(E[index + 16 * g + decltype(pc)::value]); },
+    pipelined_rec<16>(
+        [&](auto pc) __attribute__((always_inline)) {
+          return (cpool_t)(R) + (index + 16 * g + decltype(pc)::value) * kPoolWords;
+        },
+        [&](auto pc) __attribute__((always_inline)) { return ((m >> decltype(pc)::value) & 1u) != 0; },  // present
         [&](auto pc, const Mult& pool) __attribute__((always_inline)) {
           constexpr int x = decltype(pc)::value;
           XL[x] = 0;  // absent rows contribute zero
@@ -532,13 +535,11 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
 // Decode of one tile (K < 256: see kMultiTile), as rec_tiles with ntl = 1.
 template <int K, int NQ>
 __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructArgs& a, const uint8_t* sh,
-                                         const uint8_t* pres, const uint16_t* loc, const uint16_t* pre_e, uint8_t* smem,
+                                         const uint8_t* pres, const uint32_t* rows, uint8_t* smem,
                                          uint32_t pb, uint32_t col0, uint32_t ncols, bool full, uint64_t* dbg) {
   using G = Geo<K>;
-  constexpr int N = NQ * K;
   uint8_t* tile = smem;
   uint32_t* VP = reinterpret_cast<uint32_t*>(smem + G::kTileBytes);  // 2 staged transforms
-  uint16_t* E = reinterpret_cast<uint16_t*>(smem + G::kTileBytes + 8 * G::kVPWords);  // multiplier of every row
   const uint32_t tid = threadIdx.x, lane = tid & 63u, g = uniform(tid >> 6);
   const uint32_t cqb = col_base<K>(4 * lane) ^ (32u * g);
 
@@ -555,11 +556,6 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
 
   uint32_t XL[16], XH[16];
   if constexpr (NQ > 1) {
-    for (uint32_t v = tid; v < static_cast<uint32_t>(N); v += G::kThreads) {
-      // mul(x, log m) == x * EXP[m] (inc_log_mul.rs:42-49); the prefix
-      // locator already holds the multipliers (launch_prefix_locator)
-      E[v] = loc ? T.exp[loc[v]] : pre_e[v];
-    }
     // multiplier tables of the first two segment transforms (indices 2K, 3K or K, 0)
     stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(0)) * K, VP);
     stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(1)) * K, VP + G::kVPWords);
@@ -568,7 +564,7 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
 
     const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
     uint32_t AL[16], AH[16];
-    RecCtx c{T, a.shard_len, tile, E, sh, VP, g, lane, tid, ncols, full, cqb, hb, dbg};
+    RecCtx c{T, a.shard_len, tile, rows, sh, VP, g, lane, tid, ncols, full, cqb, hb, dbg};
     rec_segments<K, NQ>(c, msk, raw, AL, AH, false);
     // ---- forward transform of size K at index 0
     const uint32_t* vp0 = VP + ((NQ - 1) & 1) * G::kVPWords;  // segment 0's tables = FFT(K, 0)'s
@@ -591,8 +587,11 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
 #pragma unroll
     for (int p = 0; p < 16; ++p) blk_to_quad(raw[p], XL[p], XH[p]);
   } else {
-    pipelined<16>(
-        T, [&](auto pc) __attribute__((always_inline)) { return uniform(E[16 * g + decltype(pc)::value]); },
+    pipelined_rec<16>(
+        [&](auto pc) __attribute__((always_inline)) {
+          return (cpool_t)(fresh(rows)) + (16 * g + decltype(pc)::value) * kPoolWords;
+        },
+        [&](auto pc) __attribute__((always_inline)) { return ((m0 >> decltype(pc)::value) & 1u) == 0; },  // erased
         [&](auto pc, const Mult& pool) __attribute__((always_inline)) {
           constexpr int x = decltype(pc)::value;
           // present: the received symbol (mod.rs:225-235); erased: the
@@ -658,13 +657,11 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
 // output whenever the prefix holds at least K present rows.
 template <int K, int NQ>
 __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructArgs& a, const uint8_t* pres,
-                                          const uint16_t* loc, const uint16_t* pre_e, uint8_t* smem, uint32_t pb,
+                                          const uint32_t* rows, uint8_t* smem, uint32_t pb,
                                           uint32_t tl0, uint32_t ntl, uint32_t nsyms) {
   using G = Geo<K>;
-  constexpr int N = NQ * K;
   uint8_t* tile = smem;
   uint32_t* VP = reinterpret_cast<uint32_t*>(smem + G::kTileBytes);  // 2 staged transforms
-  uint16_t* E = reinterpret_cast<uint16_t*>(smem + G::kTileBytes + 8 * G::kVPWords);  // multiplier of every row
   const uint32_t tid0 = threadIdx.x, g0 = uniform(tid0 >> 6);
   const bool aligned = ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
   const uint8_t* shp = a.shards + static_cast<size_t>(pb) * a.batch_stride;
@@ -678,20 +675,23 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
   auto tile_cols = [&](uint32_t tl) __attribute__((always_inline)) {
     return min(static_cast<uint32_t>(kTile), nsyms - tl * kTile);
   };
+  // Tile order rotated by the batch entry: the workgroups running at the same
+  // time then read different 512-byte pieces of their rows, instead of every
+  // one the same offset of 4 KiB-strided rows (L2 conflict misses).
+  const uint32_t rot = pb % ntl;
+  auto tile_at = [&](uint32_t t) __attribute__((always_inline)) {
+    const uint32_t i = t + rot;
+    return tl0 + (i >= ntl ? i - ntl : i);
+  };
   uint2 raw[16];
   if constexpr (kRowPrefetch<NQ>) {
-    const uint32_t nc = tile_cols(tl0);
-    issue_rows(raw, (NQ > 1 && (kExp & 32)) ? T.zeros : shp + 2u * static_cast<size_t>(tl0) * kTile,
+    const uint32_t nc = tile_cols(tile_at(0));
+    issue_rows(raw, (NQ > 1 && (kExp & 32)) ? T.zeros : shp + 2u * static_cast<size_t>(tile_at(0)) * kTile,
                (NQ > 1 && (kExp & 32)) ? 0 : a.shard_len, msk0[0],
                static_cast<uint32_t>(NQ == 1 ? 0 : seg_of<NQ>(0)) * K + 16 * g0, T.zeros, tid0 & 63u, nc,
                nc == kTile && aligned);
   }
   if constexpr (NQ > 1) {
-    for (uint32_t v = tid0; v < static_cast<uint32_t>(N); v += G::kThreads) {
-      // mul(x, log m) == x * EXP[m] (inc_log_mul.rs:42-49); the prefix
-      // locator already holds the multipliers (launch_prefix_locator)
-      E[v] = loc ? T.exp[loc[v]] : pre_e[v];
-    }
     // multiplier tables of the first two segment transforms (indices 2K, 3K or
     // K, 0): for NQ = 2 these are all the tables, kept for every tile
     stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(0)) * K, VP);
@@ -711,7 +711,7 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
     uint32_t msk[NQ];
 #pragma unroll
     for (int i = 0; i < NQ; ++i) msk[i] = fresh(msk0[i]);
-    const uint32_t tl = tl0 + t, col0 = tl * kTile, ncols = tile_cols(tl);
+    const uint32_t tl = tile_at(t), col0 = tl * kTile, ncols = tile_cols(tl);
     const bool full = ncols == kTile && aligned;
     const uint8_t* sh = shp + 2u * static_cast<size_t>(col0);
     uint64_t* dbg = (kExp & 64) ? reinterpret_cast<uint64_t*>(a.out + static_cast<size_t>(pb) * a.out_stride +
@@ -731,7 +731,7 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
     if constexpr (NQ > 1) {
       const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
       uint32_t AL[16], AH[16];
-      RecCtx c{T, shard_len, tile, E, sh, VP, g, lane, tid, ncols, full, cqb, hb, dbg};
+      RecCtx c{T, shard_len, tile, rows, sh, VP, g, lane, tid, ncols, full, cqb, hb, dbg};
       rec_segments<K, NQ>(c, msk, raw, AL, AH, t > 0 && NQ == 2);
       // ---- forward transform of size K at index 0
       const uint32_t* vp0 = VP + ((NQ - 1) & 1) * G::kVPWords;  // segment 0's tables = FFT(K, 0)'s
@@ -754,8 +754,11 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
 #pragma unroll
       for (int p = 0; p < 16; ++p) blk_to_quad(raw[p], XL[p], XH[p]);
     } else {
-      pipelined<16>(
-          T, [&](auto pc) __attribute__((always_inline)) { return uniform(E[16 * g + decltype(pc)::value]); },
+      pipelined_rec<16>(
+          [&](auto pc) __attribute__((always_inline)) {
+            return (cpool_t)(fresh(rows)) + (16 * g + decltype(pc)::value) * kPoolWords;
+          },
+          [&](auto pc) __attribute__((always_inline)) { return ((m0 >> decltype(pc)::value) & 1u) == 0; },  // erased
           [&](auto pc, const Mult& pool) __attribute__((always_inline)) {
             constexpr int x = decltype(pc)::value;
             // present: the received symbol (mod.rs:225-235); erased: the
@@ -772,8 +775,9 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
     // the next tile's first-step rows load during this tile's copy-out
     if constexpr (kRowPrefetch<NQ>) {
       if (t + 1 < ntl) {
-        const uint32_t nc = tile_cols(tl + 1);
-        issue_rows(raw, (NQ > 1 && (kExp & 32)) ? T.zeros : sh + 2u * kTile, (NQ > 1 && (kExp & 32)) ? 0 : shard_len,
+        const uint32_t tn = tile_at(t + 1), nc = tile_cols(tn);
+        issue_rows(raw, (NQ > 1 && (kExp & 32)) ? T.zeros : shp + 2u * static_cast<size_t>(tn) * kTile,
+                   (NQ > 1 && (kExp & 32)) ? 0 : shard_len,
                    msk[0], static_cast<uint32_t>(NQ == 1 ? 0 : seg_of<NQ>(0)) * K + 16 * g, T.zeros, lane, nc,
                    nc == kTile && aligned);
       }
@@ -831,22 +835,18 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
   const uint32_t pb = tr.pb, tl0 = tr.tl * tpw;
   const uint32_t ntl = min(tpw, tiles - tl0);
   const uint8_t* pres = a.present + static_cast<size_t>(pb) * N;
-  const uint16_t* loc = a.locators ? a.locators + static_cast<size_t>(pb) * N : nullptr;
-
-  int nq = NQ;
-  const uint16_t* pre_e = nullptr;
-  if (!loc) {
-    const uint8_t* rec = a.prefix + static_cast<size_t>(pb) * prefix_stride_c(N, K);
-    nq = uniform(rec[0]);
-    pre_e = reinterpret_cast<const uint16_t*>(rec + kPrefixHeader);
-  }
+  // the payload's decode prefix and row tables (k_prefix_locator, or
+  // k_locator_records for caller locators)
+  const uint8_t* rec = a.prefix + static_cast<size_t>(pb) * prefix_stride_c(N, K);
+  const int nq = uniform(rec[0]);
+  const uint32_t* rows = reinterpret_cast<const uint32_t*>(rec + prefix_pools_offset(N));
   if constexpr (kMultiTile<K>) {
     if constexpr (SERVE == 4) {
-      if (nq == 4) rec_tiles<K, 4>(T, a, pres, loc, pre_e, smem, pb, tl0, ntl, nsyms);
+      if (nq == 4) rec_tiles<K, 4>(T, a, pres, rows, smem, pb, tl0, ntl, nsyms);
     } else if (nq == 1) {
-      rec_tiles<K, 1>(T, a, pres, loc, pre_e, smem, pb, tl0, ntl, nsyms);
+      rec_tiles<K, 1>(T, a, pres, rows, smem, pb, tl0, ntl, nsyms);
     } else if (nq == 2) {
-      rec_tiles<K, 2>(T, a, pres, loc, pre_e, smem, pb, tl0, ntl, nsyms);
+      rec_tiles<K, 2>(T, a, pres, rows, smem, pb, tl0, ntl, nsyms);
     }
   } else {  // tpw == 1
     const uint32_t col0 = tl0 * kTile;
@@ -858,16 +858,28 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
                                                                static_cast<size_t>(nsyms) * 2 * K + 256u * tl0)
                                  : nullptr;
     if constexpr (SERVE == 4) {
-      if (nq == 4) rec_tile<K, 4>(T, a, sh, pres, loc, pre_e, smem, pb, col0, ncols, full, dbg);
+      if (nq == 4) rec_tile<K, 4>(T, a, sh, pres, rows, smem, pb, col0, ncols, full, dbg);
     } else if (nq == 1) {
-      rec_tile<K, 1>(T, a, sh, pres, loc, pre_e, smem, pb, col0, ncols, full, dbg);
+      rec_tile<K, 1>(T, a, sh, pres, rows, smem, pb, col0, ncols, full, dbg);
     } else if (nq == 2) {
-      rec_tile<K, 2>(T, a, sh, pres, loc, pre_e, smem, pb, col0, ncols, full, dbg);
+      rec_tile<K, 2>(T, a, sh, pres, rows, smem, pb, col0, ncols, full, dbg);
     }
   }
 }
 
 // ---------------------------------------------------------- prefix locator ----
+// The v_perm tables of row multipliers E[0..rows) into the record (thread
+// tid copies the rows it wrote E for: no barrier).
+__device__ __forceinline__ void write_row_pools(const DevTables& T, const uint16_t* E, uint32_t rows, uint8_t* dst) {
+  for (uint32_t v = threadIdx.x; v < rows; v += 256) {
+    const uint4* src = reinterpret_cast<const uint4*>(T.perm_pools + static_cast<size_t>(E[v]) * kPoolWords);
+    uint4* d = reinterpret_cast<uint4*>(dst + static_cast<size_t>(v) * 4 * kPoolWords);
+#pragma unroll
+    for (int i = 0; i < kPoolWords / 4; ++i) d[i] = src[i];
+  }
+}
+
+
 // One workgroup per payload: the decode prefix (rec_tile) and the erasure
 // locator folded to it (fused_locator, SURVEY F8: eval_error_polynomial
 // inc_reconstruct.rs:90-113 over [0, NQ' * K)), as row multipliers EXP[loc]
@@ -897,6 +909,23 @@ __global__ __launch_bounds__(256) void k_prefix_locator(DevTables T, Reconstruct
   } else {
     fused_locator<N, 256>(T, pres, W, E, PR);
   }
+  write_row_pools(T, E, static_cast<uint32_t>(nq) * K, rec + prefix_pools_offset(N));
+}
+
+// The record for caller locators (log form, all n rows: the full decode,
+// NQ' = NQ): row multipliers EXP[loc] and their tables.  One workgroup per
+// payload.
+template <int K, int NQ>
+__global__ __launch_bounds__(256) void k_locator_records(DevTables T, ReconstructArgs a, uint8_t* out) {
+  constexpr int N = NQ * K;
+  const uint32_t pb = blockIdx.x, tid = threadIdx.x;
+  const uint16_t* loc = a.locators + static_cast<size_t>(pb) * N;
+  uint8_t* rec = out + static_cast<size_t>(pb) * prefix_stride_c(N, K);
+  uint16_t* E = reinterpret_cast<uint16_t*>(rec + kPrefixHeader);
+  if (tid == 0) rec[0] = static_cast<uint8_t>(NQ);
+  // mul(x, log m) == x * EXP[m] (inc_log_mul.rs:42-49)
+  for (uint32_t v = tid; v < static_cast<uint32_t>(N); v += 256) E[v] = T.exp[loc[v]];
+  write_row_pools(T, E, N, rec + prefix_pools_offset(N));
 }
 
 // ------------------------------------------------------------- launchers ----
@@ -913,7 +942,7 @@ size_t encode_multi_lds_bytes() {
 
 template <int K, int NQ>
 size_t reconstruct_lds_bytes() {
-  return static_cast<size_t>(Geo<K>::kTileBytes) + 2u * 4u * Geo<K>::kVPWords + 2u * 4 * K;
+  return static_cast<size_t>(Geo<K>::kTileBytes) + 2u * 4u * Geo<K>::kVPWords;
 }
 
 // Tiles per workgroup (kMultiTile): as many as keep >= kWorkgroups
@@ -954,7 +983,10 @@ template <int K, int NQ>
 hipError_t launch_prefix_k(const DevTables& T, const ReconstructArgs& a, uint8_t* out, hipStream_t s) {
   if (a.batch == 0) return hipSuccess;
   if (a.batch > 0x7fffffffu) return hipErrorInvalidValue;
-  k_prefix_locator<K, NQ><<<static_cast<uint32_t>(a.batch), 256, 0, s>>>(T, a, out);
+  if (a.locators)
+    k_locator_records<K, NQ><<<static_cast<uint32_t>(a.batch), 256, 0, s>>>(T, a, out);
+  else
+    k_prefix_locator<K, NQ><<<static_cast<uint32_t>(a.batch), 256, 0, s>>>(T, a, out);
   return hipGetLastError();
 }
 

@@ -24,8 +24,8 @@ struct ReconstructArgs {
   size_t shard_len, batch_stride;
   const uint8_t* present;    // device, batch x n
   const uint16_t* locators;  // device, batch x n (log form)
-  // fast path, locators == nullptr: per-payload decode prefix and row
-  // multipliers from launch_prefix_locator (stride prefix_stride(n) bytes)
+  // fast path: per-payload decode prefix, row multipliers and their tables
+  // from launch_prefix_locator (stride prefix_stride(n) bytes)
   const uint8_t* prefix;
   size_t batch;
   uint32_t n, k;
@@ -61,8 +61,10 @@ bool fast_reconstruct_supported(uint32_t n, uint32_t k);
 hipError_t launch_encode_fast(const DevTables& T, const EncodeArgs& a, hipStream_t s);
 hipError_t launch_reconstruct_fast(const DevTables& T, const ReconstructArgs& a, hipStream_t s);
 // Per payload: the shortest row prefix (k, 2k or n rows) holding k present rows
-// and the folded erasure locator over it as row multipliers, for the fast
-// reconstruct kernel (a.prefix).  `out` holds batch * prefix_stride(n, k) bytes.
+// and the folded erasure locator over it as row multipliers, with their v_perm
+// tables, for the fast reconstruct kernel (a.prefix); with a.locators set, the
+// caller's locators over all n rows instead (the full decode).  `out` holds
+// batch * prefix_stride(n, k) bytes.
 size_t prefix_stride(uint32_t n, uint32_t k);
 hipError_t launch_prefix_locator(const DevTables& T, const ReconstructArgs& a, uint8_t* out, hipStream_t s);
 

@@ -20,7 +20,7 @@ os.makedirs(dst, exist_ok=True)
 # The bench's "reconstruct" span is the prefix-locator launch plus both fast
 # reconstruct instances (prefixes of <= 2 and of 4 segments); their per-launch
 # traffic and durations add up.  Each instance is also reported on its own.
-KINDS = {"encode": ("k_encode_fast",), "reconstruct": ("k_reconstruct_fast", "k_prefix_locator"),
+KINDS = {"encode": ("k_encode_fast", "k_encode_multi"), "reconstruct": ("k_reconstruct_fast", "k_prefix_locator"),
          "locator": ("k_error_locator",), "encode_big": ("k_encode_big",), "reconstruct_big": ("k_reconstruct_big",),
          "calib_read8": ("read8",), "calib_copy8": ("copy8",)}
 
