@@ -871,11 +871,27 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
 // The v_perm tables of row multipliers E[0..rows) into the record (thread
 // tid copies the rows it wrote E for: no barrier).
 __device__ __forceinline__ void write_row_pools(const DevTables& T, const uint16_t* E, uint32_t rows, uint8_t* dst) {
-  for (uint32_t v = threadIdx.x; v < rows; v += 256) {
-    const uint4* src = reinterpret_cast<const uint4*>(T.perm_pools + static_cast<size_t>(E[v]) * kPoolWords);
-    uint4* d = reinterpret_cast<uint4*>(dst + static_cast<size_t>(v) * 4 * kPoolWords);
+  constexpr int kQ = kPoolWords / 4;  // 16-byte pieces per row
+  for (uint32_t v0 = threadIdx.x; v0 < rows; v0 += 4 * 256) {
+    uint4 t[4][kQ];  // four rows in flight per thread
 #pragma unroll
-    for (int i = 0; i < kPoolWords / 4; ++i) d[i] = src[i];
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t v = v0 + 256u * r;
+      if (v < rows) {
+        const uint4* src = reinterpret_cast<const uint4*>(T.perm_pools + static_cast<size_t>(E[v]) * kPoolWords);
+#pragma unroll
+        for (int i = 0; i < kQ; ++i) t[r][i] = src[i];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t v = v0 + 256u * r;
+      if (v < rows) {
+        uint4* d = reinterpret_cast<uint4*>(dst + static_cast<size_t>(v) * 4 * kPoolWords);
+#pragma unroll
+        for (int i = 0; i < kQ; ++i) d[i] = t[r][i];
+      }
+    }
   }
 }
 
