@@ -565,10 +565,13 @@ __host__ __device__ constexpr int hi_groups() {
 }
 
 // Levels 0..3 in the cq layout: CL/CH[p] = position 16g + p.  Group t of level
-// b is g * (8 >> b) + (p >> (b + 1)).
+// b is g * (8 >> b) + (p >> (b + 1)).  `rows` (wave-uniform bit p = position
+// 16g + p): inverse transforms skip the groups none of whose input rows is
+// set (all-zero inputs stay zero), forward ones the groups none of whose
+// output rows is set (outputs nobody reads); ~0u runs every group.
 template <int K, bool INVERSE, bool INDEX0>
 __device__ __forceinline__ void cq_levels(const DevTables& T, const uint32_t* VP, uint32_t index, uint32_t g,
-                                          uint32_t (&L)[16], uint32_t (&H)[16]) {
+                                          uint32_t (&L)[16], uint32_t (&H)[16], uint32_t rows = ~0u) {
   if constexpr (kExp & 1) return;
   auto cval = [&](auto fc) __attribute__((always_inline)) {
     constexpr GroupRef r = cq_group<INVERSE>(decltype(fc)::value);
@@ -582,6 +585,8 @@ __device__ __forceinline__ void cq_levels(const DevTables& T, const uint32_t* VP
     constexpr GroupRef r = cq_group<INVERSE>(decltype(fc)::value);
     constexpr int d = 1 << r.b;
     const bool live = !INDEX0 || r.t != 0 || g != 0;  // c == 0: the skew sentinel, no product
+    constexpr uint32_t span = ((1u << (2 * d)) - 1u) << (r.t * 2 * d);  // the group's rows
+    if ((rows & span) == 0) return;
 #pragma unroll
     for (int u = 0; u < d; ++u) {
       const int x = r.t * 2 * d + u, y = x + d;

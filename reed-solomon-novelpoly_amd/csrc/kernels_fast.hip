@@ -463,7 +463,7 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
         });
     const uint32_t* vp = c.VP + (step & 1) * Geo<K>::kVPWords;
     stamp(c.dbg, 3 + 6 * step);
-    cq_levels<K, true, false>(T, vp, index, g, XL, XH);
+    cq_levels<K, true, false>(T, vp, index, g, XL, XH, m);  // absent rows are zero
     stamp(c.dbg, 4 + 6 * step);
     if (step > 0 || after_tile) {
       __syncthreads();  // the previous high pass (or tile's copy-out) is done with the tile and the other table buffer
@@ -576,7 +576,7 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
     __syncthreads();
     stamp(dbg, 28);
     cq_read<K>(tile, fresh_v(cqb), XL, XH);
-    cq_levels<K, false, true>(T, vp0, 0, g, XL, XH);
+    cq_levels<K, false, true>(T, vp0, 0, g, XL, XH, ~uniform(msk[NQ - 1]));  // erased rows only
     stamp(dbg, 29);
   }
   // ---- merge: received systematic rows, postmultiplied recovered ones
@@ -743,7 +743,7 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
       __syncthreads();
       stamp(dbg, 28);
       cq_read<K>(tile, fresh_v(cqb), XL, XH);
-      cq_levels<K, false, true>(T, vp0, 0, g, XL, XH);
+      cq_levels<K, false, true>(T, vp0, 0, g, XL, XH, ~uniform(msk[NQ - 1]));  // erased rows only
       stamp(dbg, 29);
     }
     // ---- merge: received systematic rows, postmultiplied recovered ones
@@ -871,27 +871,11 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
 // The v_perm tables of row multipliers E[0..rows) into the record (thread
 // tid copies the rows it wrote E for: no barrier).
 __device__ __forceinline__ void write_row_pools(const DevTables& T, const uint16_t* E, uint32_t rows, uint8_t* dst) {
-  constexpr int kQ = kPoolWords / 4;  // 16-byte pieces per row
-  for (uint32_t v0 = threadIdx.x; v0 < rows; v0 += 4 * 256) {
-    uint4 t[4][kQ];  // four rows in flight per thread
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const uint32_t v = v0 + 256u * r;
-      if (v < rows) {
-        const uint4* src = reinterpret_cast<const uint4*>(T.perm_pools + static_cast<size_t>(E[v]) * kPoolWords);
-#pragma unroll
-        for (int i = 0; i < kQ; ++i) t[r][i] = src[i];
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const uint32_t v = v0 + 256u * r;
-      if (v < rows) {
-        uint4* d = reinterpret_cast<uint4*>(dst + static_cast<size_t>(v) * 4 * kPoolWords);
-#pragma unroll
-        for (int i = 0; i < kQ; ++i) d[i] = t[r][i];
-      }
-    }
+  for (uint32_t v = threadIdx.x; v < rows; v += 256) {
+    const uint4* src = reinterpret_cast<const uint4*>(T.perm_pools + static_cast<size_t>(E[v]) * kPoolWords);
+    uint4* d = reinterpret_cast<uint4*>(dst + static_cast<size_t>(v) * 4 * kPoolWords);
+    const uint4 a0 = src[0], a1 = src[1], a2 = src[2], a3 = src[3], a4 = src[4];
+    d[0] = a0, d[1] = a1, d[2] = a2, d[3] = a3, d[4] = a4;
   }
 }
 
