@@ -82,8 +82,17 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
   }
   const uint32_t nshift = a.n / K;
   const uint32_t wanted_store = ((kExp & 2) && a.k != 12345u) ? 0u : a.wanted_n;  // experiment: no stores
-  stage_vpools<K, G::kThreads>(T, 0, VP);                              // inverse transform, index 0
-  if (nshift > 1) stage_vpools<K, G::kThreads>(T, K, VP + G::kVPWords);  // first shift
+  // n <= 4K: the tables of every transform stay staged (one buffer each, as
+  // k_encode_multi: no table load inside the shift loop, where it would wait
+  // for the row stores issued before it); otherwise two buffers alternate
+  const bool resident = nshift <= 4;
+  if (resident) {
+    for (uint32_t sh = 0; sh < nshift && sh * K < a.wanted_n; ++sh)
+      stage_vpools<K, G::kThreads>(T, sh * K, VP + sh * G::kVPWords);
+  } else {
+    stage_vpools<K, G::kThreads>(T, 0, VP);                              // inverse transform, index 0
+    if (nshift > 1) stage_vpools<K, G::kThreads>(T, K, VP + G::kVPWords);  // first shift
+  }
   __syncthreads();
 
   const uint32_t cqb = col_base<K>(4 * lane) ^ (32u * g);  // blocks 4g..4g+3 of columns 4l..4l+3
@@ -114,7 +123,7 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
       XL[q] = ML[q];
       XH[q] = MH[q];
     }
-    const uint32_t* vp = VP + (sh & 1u) * G::kVPWords;
+    const uint32_t* vp = VP + (resident ? sh : (sh & 1u)) * G::kVPWords;
     if (sh == 1) {
       fwd_top<K, 1>(T, vp, index, XL, XH, PL, PH);
     } else if (sh == 2) {
@@ -126,7 +135,7 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     }
     hi_levels<K, false, false, 1>(T, vp, index, XL, XH);
     __syncthreads();  // the previous cq pass is done with the tile and with the other table buffer
-    if (sh + 1 < nshift && (sh + 1) * K < a.wanted_n)
+    if (!resident && sh + 1 < nshift && (sh + 1) * K < a.wanted_n)
       stage_vpools<K, G::kThreads>(T, (sh + 1) * K, VP + ((sh + 1) & 1u) * G::kVPWords);
     hi_write<K>(tile, fresh_v(hb), XL, XH);
     __syncthreads();
@@ -931,7 +940,7 @@ __global__ __launch_bounds__(256) void k_locator_records(DevTables T, Reconstruc
 // ------------------------------------------------------------- launchers ----
 template <int K>
 size_t encode_lds_bytes() {
-  return static_cast<size_t>(Geo<K>::kTileBytes) + 2u * 4u * Geo<K>::kVPWords;
+  return static_cast<size_t>(Geo<K>::kTileBytes) + 4u * 4u * Geo<K>::kVPWords;  // up to 4 resident tables
 }
 
 template <int K>
