@@ -739,6 +739,64 @@ __device__ __forceinline__ void hi_write(uint8_t* tile, uint32_t base, const uin
     *reinterpret_cast<uint2*>(tile + (base ^ (8u * Geo<K>::R * j))) = quad_to_blk(L[j], H[j]);
 }
 
+// Planar exchange between the two layouts (the transforms' own LDS round
+// trips; the payload tile and the output copy-out keep the natural block
+// format above): a block holds (low bytes, high bytes) of 4 positions of one
+// column, so the high layout moves its quads with no byte shuffle and the cq
+// side does only the 4 x 4 byte transpose (positions x columns) of each plane.
+__device__ __forceinline__ void tr4x4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t* o) {
+  const uint32_t t01 = vperm(a1, a0, 0x05010400u), u01 = vperm(a1, a0, 0x07030602u);
+  const uint32_t t23 = vperm(a3, a2, 0x05010400u), u23 = vperm(a3, a2, 0x07030602u);
+  o[0] = vperm(t23, t01, 0x05040100u);
+  o[1] = vperm(t23, t01, 0x07060302u);
+  o[2] = vperm(u23, u01, 0x05040100u);
+  o[3] = vperm(u23, u01, 0x07060302u);
+}
+
+template <int K>
+__device__ __forceinline__ void cq_read_p(const uint8_t* tile, uint32_t base, uint32_t (&L)[16], uint32_t (&H)[16]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    uint2 d[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      d[i] = *reinterpret_cast<const uint2*>(tile + (base ^ (col_base_c<K>(i) ^ (8u * u))));
+    tr4x4(d[0].x, d[1].x, d[2].x, d[3].x, &L[4 * u]);
+    tr4x4(d[0].y, d[1].y, d[2].y, d[3].y, &H[4 * u]);
+  }
+}
+
+template <int K>
+__device__ __forceinline__ void cq_write_p(uint8_t* tile, uint32_t base, const uint32_t (&L)[16],
+                                           const uint32_t (&H)[16]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    uint32_t l[4], h[4];
+    tr4x4(L[4 * u], L[4 * u + 1], L[4 * u + 2], L[4 * u + 3], l);
+    tr4x4(H[4 * u], H[4 * u + 1], H[4 * u + 2], H[4 * u + 3], h);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *reinterpret_cast<uint2*>(tile + (base ^ (col_base_c<K>(i) ^ (8u * u)))) = make_uint2(l[i], h[i]);
+  }
+}
+
+template <int K>
+__device__ __forceinline__ void hi_read_p(const uint8_t* tile, uint32_t base, uint32_t (&L)[16], uint32_t (&H)[16]) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint2 d = *reinterpret_cast<const uint2*>(tile + (base ^ (8u * Geo<K>::R * j)));
+    L[j] = d.x;
+    H[j] = d.y;
+  }
+}
+
+template <int K>
+__device__ __forceinline__ void hi_write_p(uint8_t* tile, uint32_t base, const uint32_t (&L)[16],
+                                           const uint32_t (&H)[16]) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) *reinterpret_cast<uint2*>(tile + (base ^ (8u * Geo<K>::R * j))) = make_uint2(L[j], H[j]);
+}
+
 // ---------------------------------------------------------------- locator ----
 // eval_error_polynomial (inc_reconstruct.rs:90-113, called over the whole field
 // by mod.rs:217-218) for an erasure set inside [0, N), folded to N points

@@ -102,13 +102,13 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     cq_read<K>(tile, cqb, CL, CH);
     store_rows(out, a.shard_len, 16 * g, wanted_store, CL, CH, lane, ncols, full);
     cq_levels<K, true, true>(T, VP, 0, g, CL, CH);
-    cq_write<K>(tile, cqb, CL, CH);
+    cq_write_p<K>(tile, cqb, CL, CH);
   }
   __syncthreads();
   // ---- high layout: inverse levels 4.. -> coefficients M
   const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
   uint32_t ML[16], MH[16];
-  hi_read<K>(tile, hb, ML, MH);
+  hi_read_p<K>(tile, hb, ML, MH);
   hi_levels<K, true, true>(T, VP, 0, ML, MH);
 #pragma unroll
   for (int q = 0; q < 16; ++q) asm volatile("" : "+v"(ML[q]), "+v"(MH[q]));  // materialise M once
@@ -137,9 +137,9 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     __syncthreads();  // the previous cq pass is done with the tile and with the other table buffer
     if (!resident && sh + 1 < nshift && (sh + 1) * K < a.wanted_n)
       stage_vpools<K, G::kThreads>(T, (sh + 1) * K, VP + ((sh + 1) & 1u) * G::kVPWords);
-    hi_write<K>(tile, fresh_v(hb), XL, XH);
+    hi_write_p<K>(tile, fresh_v(hb), XL, XH);
     __syncthreads();
-    cq_read<K>(tile, fresh_v(cqb), XL, XH);
+    cq_read_p<K>(tile, fresh_v(cqb), XL, XH);
     cq_levels<K, false, false>(T, vp, index, g, XL, XH);
     store_rows(out, a.shard_len, index + 16 * g, wanted_store, XL, XH, lane, ncols, full);
   }
@@ -226,9 +226,9 @@ __device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArg
   }
   hi_levels<K, false, false, 1>(T, vp, index, XL, XH);
   __syncthreads();  // the previous cq pass is done with the tile
-  hi_write<K>(tile, fresh_v(hb), XL, XH);
+  hi_write_p<K>(tile, fresh_v(hb), XL, XH);
   __syncthreads();
-  cq_read<K>(tile, fresh_v(cqb), XL, XH);
+  cq_read_p<K>(tile, fresh_v(cqb), XL, XH);
   if (dma_pay) {
     __syncthreads();  // every wave has its cq registers: the tile is free
     if constexpr (!(kExp & 4)) dma_tile<K>(dma_pay, dma_ch0, tile, g, lane);
@@ -299,12 +299,12 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
     cq_read<K>(tile, cqb, CL, CH);
     store_rows(out, a.shard_len, 16 * g, (kExp & 2) ? 0u : a.wanted_n, CL, CH, lane, ncols, full);
     cq_levels<K, true, true>(T, VP, 0, g, CL, CH);
-    cq_write<K>(tile, cqb, CL, CH);
+    cq_write_p<K>(tile, cqb, CL, CH);
   }
   __syncthreads();
   const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
   uint32_t ML[16], MH[16];
-  hi_read<K>(tile, hb, ML, MH);
+  hi_read_p<K>(tile, hb, ML, MH);
   hi_levels<K, true, true>(T, VP, 0, ML, MH);
 #pragma unroll
   for (int q = 0; q < 16; ++q) asm volatile("" : "+v"(ML[q]), "+v"(MH[q]));  // materialise M once
