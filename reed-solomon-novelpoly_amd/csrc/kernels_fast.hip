@@ -481,7 +481,7 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
         stage_vpools<K, Geo<K>::kThreads>(T, static_cast<uint32_t>(qn) * K, c.VP + ((step + 1) & 1) * Geo<K>::kVPWords);
       }
     }
-    cq_write<K>(c.tile, cqb, XL, XH);
+    cq_write_p<K>(c.tile, cqb, XL, XH);
     // next step's rows (the systematic rows after the last step) load during
     // this step's high pass
     if constexpr (kRowPrefetch<NQ>) {
@@ -500,7 +500,7 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
     }
     __syncthreads();
     stamp(c.dbg, 5 + 6 * step);
-    hi_read<K>(c.tile, hb, XL, XH);
+    hi_read_p<K>(c.tile, hb, XL, XH);
     hi_levels<K, true, false>(T, vp, index, XL, XH);
     stamp(c.dbg, 6 + 6 * step);
     __builtin_amdgcn_sched_barrier(0);
