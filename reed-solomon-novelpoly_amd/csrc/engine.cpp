@@ -181,6 +181,9 @@ hipError_t big_done(np_ctx* c, hipStream_t s, hipError_t e) {
   return hipEventRecord(c->big_done, s);
 }
 
+// Scratch slots of a k = 1024 launch over `tiles` tiles: one per resident workgroup.
+size_t big_slots(size_t tiles) { return std::min((tiles + 7) / 8 * 8, np::big_resident_slots()); }
+
 // Caller holds the context lock.
 hipError_t launch_encode(np_ctx* c, const np::EncodeArgs& a, hipStream_t s) {
   if (np::fast_encode_supported(a.n, a.k)) return np::launch_encode_fast(c->T, a, s);
@@ -188,7 +191,7 @@ hipError_t launch_encode(np_ctx* c, const np::EncodeArgs& a, hipStream_t s) {
     const size_t tiles = ((a.payload_len + 2 * a.k - 1) / (2 * a.k) + 255) / 256;
     uint8_t* scr = nullptr;
     size_t bytes = 0;
-    hipError_t e = big_scratch(c, std::max<size_t>(a.batch * tiles, 8) * np::big_encode_scratch_per_tile(), s, &scr, &bytes);
+    hipError_t e = big_scratch(c, big_slots(a.batch * tiles) * np::big_encode_scratch_per_tile(), s, &scr, &bytes);
     if (e == hipSuccess) e = np::launch_encode_big(c->T, a, scr, bytes, s);
     return big_done(c, s, e);
   }
@@ -228,7 +231,7 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
     const size_t tiles = (a.shard_len / 2 + 255) / 256;
     uint8_t* scr = nullptr;
     size_t bytes = 0;
-    hipError_t e = big_scratch(c, std::max<size_t>(a.batch * tiles, 8) * np::big_reconstruct_scratch_per_tile(a.n), s, &scr,
+    hipError_t e = big_scratch(c, big_slots(a.batch * tiles) * np::big_reconstruct_scratch_per_tile(a.n), s, &scr,
                                 &bytes);
     if (e == hipSuccess) e = np::launch_reconstruct_big(c->T, a, scr, bytes, s);
     return big_done(c, s, e);

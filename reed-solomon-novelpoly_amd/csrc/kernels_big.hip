@@ -450,13 +450,35 @@ bool big_reconstruct_supported(uint32_t n, uint32_t k) {
 size_t big_encode_scratch_per_tile() { return kEncScratch; }
 size_t big_reconstruct_scratch_per_tile(uint32_t n) { return (4u * (n / kKB) + 4u) * kSegScr; }
 
+// Workgroups of the k = 1024 kernels resident on the device at once (one per
+// CU: 1024 threads and ~150 KiB of LDS each), rounded down to a multiple of 8.
+// Each launch covers at most that many tiles, so a launch is one full round of
+// workgroups on the CUs (no partial last round) and its scratch stays that of
+// the resident workgroups.
+size_t big_resident_slots() {
+  static size_t slots = 0;  // same for every context: the pool holds one GPU type
+  if (slots == 0) {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&k_reconstruct_big<4>), kTB,
+                                                     rec_big_lds<4>()) != hipSuccess ||
+        per <= 0)
+      per = 1;
+    slots = std::max<size_t>(8, static_cast<size_t>(cus) * per / 8 * 8);
+  }
+  return slots;
+}
+
 hipError_t launch_encode_big(const DevTables& T, const EncodeArgs& a, uint8_t* scratch, size_t scratch_bytes,
                              hipStream_t s) {
   const size_t nchunks = (a.payload_len + 2 * a.k - 1) / (2 * a.k);
   if (nchunks == 0 || a.batch == 0) return hipSuccess;
   const uint32_t tiles = static_cast<uint32_t>((nchunks + kTile - 1) / kTile);
   const size_t total = a.batch * tiles;
-  const size_t per_launch = scratch_bytes / kEncScratch / 8 * 8;  // keeps tile0 % 8 == 0 (tile_of)
+  // multiple of 8 keeps tile0 % 8 == 0 (tile_of)
+  const size_t per_launch = std::min(big_resident_slots(), scratch_bytes / kEncScratch / 8 * 8);
   if (per_launch == 0 || total > 0xffffffffu) return hipErrorInvalidValue;
   for (size_t t0 = 0; t0 < total; t0 += per_launch) {
     const uint32_t blocks = static_cast<uint32_t>(std::min(per_launch, total - t0));
@@ -475,7 +497,7 @@ hipError_t launch_reconstruct_big(const DevTables& T, const ReconstructArgs& a, 
   const uint32_t tiles = static_cast<uint32_t>((nsyms + kTile - 1) / kTile);
   const size_t total = a.batch * tiles;
   const size_t per_tile = big_reconstruct_scratch_per_tile(a.n);
-  const size_t per_launch = scratch_bytes / per_tile / 8 * 8;  // keeps tile0 % 8 == 0 (tile_of)
+  const size_t per_launch = std::min(big_resident_slots(), scratch_bytes / per_tile / 8 * 8);
   if (per_launch == 0 || total > 0xffffffffu) return hipErrorInvalidValue;
   for (size_t t0 = 0; t0 < total; t0 += per_launch) {
     const uint32_t blocks = static_cast<uint32_t>(std::min(per_launch, total - t0));

@@ -72,6 +72,7 @@ hipError_t launch_prefix_locator(const DevTables& T, const ReconstructArgs& a, u
 bool big_encode_supported(uint32_t n, uint32_t k);
 bool big_reconstruct_supported(uint32_t n, uint32_t k);
 size_t big_encode_scratch_per_tile();
+size_t big_resident_slots();  // scratch slots a launch uses at most (multiple of 8)
 size_t big_reconstruct_scratch_per_tile(uint32_t n);
 hipError_t launch_encode_big(const DevTables& T, const EncodeArgs& a, uint8_t* scratch, size_t scratch_bytes,
                              hipStream_t s);

@@ -266,6 +266,34 @@ def test_full_size_batch_properties(gpu, oracle, cid):
         assert ho[b, :plen].tobytes() == pls[b].tobytes(), b
 
 
+@pytest.mark.parametrize("batch,plen", [(40, 4 << 20), (33, 2048 * 256 * 9 - 5)])
+def test_big_path_launch_rounds(gpu, oracle, batch, plen):
+    """k = 1024 kernels over more tiles than one launch holds (launches of one
+    resident round each, kernels_big.hip): 320 tiles with an XCD-major batch and
+    297 tiles with a ragged last tile and batch % 8 != 0.  The last payload (in
+    the last, partial launch) against the oracle; every payload round-trips."""
+    import torch
+
+    p = npa.CodeParams.derive_parameters(4096, 1366)
+    n, k = p.n(), p.k()
+    assert (n, k) == (4096, 1024)
+    pls = np.stack([np.frombuffer(synth.payload(300 + b, plen), dtype=np.uint8) for b in range(batch)])
+    sl = p.make_encoder(gpu).shard_len(plen)
+    dp = dev(pls)
+    ds = torch.empty((batch, n, sl), dtype=torch.uint8, device="cuda")
+    npa.encode_batch_dev(p, dp.data_ptr(), plen, plen, batch, ds.data_ptr(), n * sl, ctx=gpu, stream=stream())
+    hs = host(ds)
+    st, want = oracle.encode(pls[-1].tobytes(), n, k, n)
+    assert st == 0 and hs[-1].tobytes() == b"".join(want)
+    pres = np.stack([synth.present_mask(500 + b, n, 2730) for b in range(batch)])
+    out = torch.empty((batch, (sl // 2) * 2 * k), dtype=torch.uint8, device="cuda")
+    npa.reconstruct_batch_dev(p, ds.data_ptr(), sl, n * sl, pres.tobytes(), batch, out.data_ptr(),
+                              out.shape[1], ctx=gpu, stream=stream())
+    ho = host(out)
+    bad = [b for b in range(batch) if ho[b, :plen].tobytes() != pls[b].tobytes()]
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("nw,kw,plen", [(256, 86, 128 * 256), (256, 86, 128 * 300 + 5), (256, 86, 1280),
                                         (512, 100, 128 * 700), (1024, 342, 512 * 256), (1024, 342, 5121),
                                         (1024, 342, 512 * 512 + 77), (300, 100, 77777), (512, 128, 256 * 600),
