@@ -327,11 +327,14 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
           for (int s = 0; s < 4; ++s) qx(d[s], x0[s]);
         }
       }
-#pragma unroll 1
-      for (uint32_t q = 1; q < static_cast<uint32_t>(NQ); ++q) {
-        uint2 y[4];
+      uint2 yq[NQ - 1][4];  // every segment's quads in flight at once (one latency per j)
 #pragma unroll
-        for (int s = 0; s < 4; ++s) y[s] = scr_q(scrY + (4 * q + s) * kSegScr, j, tid);
+      for (int q = 1; q < NQ; ++q)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) yq[q - 1][s] = scr_q(scrY + (4 * q + s) * kSegScr, j, tid);
+#pragma unroll
+      for (uint32_t q = 1; q < static_cast<uint32_t>(NQ); ++q) {
+        uint2 (&y)[4] = yq[q - 1];
         // levels 8 (t = 0: Cantor(4q), t = 1: Cantor(4q + 2)) and 9 (Cantor(2q)): hi ^= lo; lo ^= c hi
         {
           const Mult m80 = mult_of(T, 4u * q), m81 = mult_of(T, 4u * q + 2u);
@@ -352,15 +355,11 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
           for (int s = 0; s < 4; ++s) qx(d[s], y[s]);  // ^ x1 (and for NQ = 4: x1)
         } else if (q == 2) {
 #pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            qx(d[s], y[s]);                                // ^ x2
-            scr_q_store(scrY + s * kSegScr, j, tid, y[s].x, y[s].y);  // keep x2 (y_0s slots are consumed)
-          }
+          for (int s = 0; s < 4; ++s) qx(d[s], y[s]);  // ^ x2 (kept in yq[1] for q = 3)
         } else {  // q == 3: ^ beta (x2 ^ x3)
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
-            const uint2 x2 = scr_q(scrY + s * kSegScr, j, tid);
-            qx(y[s], x2);
+            qx(y[s], yq[1][s]);
             qm(d[s], y[s], beta);
           }
         }

@@ -1,6 +1,6 @@
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/ab4
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "big_path or shapes or full_size or digests" > gpurun_out/ab4/pytest.log 2>&1; rc=$?
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "big_path or reconstruct_shapes or full_size" > gpurun_out/ab4/pytest.log 2>&1; rc=$?
 tail -3 gpurun_out/ab4/pytest.log
 [ $rc -ne 0 ] && { grep -E "FAILED|Error" gpurun_out/ab4/pytest.log | head; exit $rc; }
 for r in 1 2; do for t in A B; do
