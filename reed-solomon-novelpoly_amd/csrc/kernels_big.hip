@@ -244,19 +244,24 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   }
 
   // ---- phase 1: y_qs for every segment q and sub-segment s
+  __syncthreads();  // E, PR ready
 #pragma unroll 1
   for (uint32_t qs = 0; qs < 4u * NQ; ++qs) {
     const uint32_t index = 256u * qs;  // = 1024 q + 256 s
-    __syncthreads();                   // tile / tables free (and E, PR ready)
+    const uint32_t gg = fresh(g);
+    // the sub-segment's present rows load while the tables are staged
+    uint2 rows[2][8];
+#pragma unroll
+    for (int half = 0; half < 2; ++half)
+      load_rows<8>(rows[half], sh, a.shard_len, PR, index + 16 * gg + 8 * half, T.zeros, lane, ncols, full);
+    __syncthreads();  // tile / tables free
     stage_vpools<kS, kTB>(T, index, VP);
     __syncthreads();
     uint32_t XL[16], XH[16];
     {
-      const uint32_t gg = fresh(g);
 #pragma unroll
       for (int half = 0; half < 2; ++half) {
-        uint2 raw[8];
-        load_rows<8>(raw, sh, a.shard_len, PR, index + 16 * gg + 8 * half, T.zeros, lane, ncols, full);
+        const uint2 (&raw)[8] = rows[half];
         pipelined<8>(
             T, [&](auto pc) __attribute__((always_inline)) { return uniform(E[index + 16 * gg + 8 * half + decltype(pc)::value]); },
             [&](auto pc, const Mult& pool) __attribute__((always_inline)) {
