@@ -817,7 +817,7 @@ __device__ __forceinline__ void fused_locator(const DevTables& T, const uint8_t*
   __syncthreads();
   for (uint32_t h = 1; h < N; h <<= 1) {  // integer WHT of the 0/1 erasure vector
     for (uint32_t b = tid; b < N / 2; b += NT) {
-      const uint32_t i = (b / h) * 2 * h + (b % h), j = i + h;
+      const uint32_t i = ((b & ~(h - 1u)) << 1) | (b & (h - 1u)), j = i + h;  // h is a power of 2
       const int32_t x = static_cast<int32_t>(W[i]), y = static_cast<int32_t>(W[j]);
       W[i] = static_cast<uint32_t>(x + y);
       W[j] = static_cast<uint32_t>(x - y);
@@ -833,7 +833,7 @@ __device__ __forceinline__ void fused_locator(const DevTables& T, const uint8_t*
   __syncthreads();
   for (uint32_t h = 1; h < N; h <<= 1) {  // WHT mod 65535
     for (uint32_t b = tid; b < N / 2; b += NT) {
-      const uint32_t i = (b / h) * 2 * h + (b % h), j = i + h;
+      const uint32_t i = ((b & ~(h - 1u)) << 1) | (b & (h - 1u)), j = i + h;  // h is a power of 2
       const uint32_t x = W[i], y = W[j];
       uint32_t s = x + y, d = x + 65535u - y;
       s -= s >= 65535u ? 65535u : 0u;
