@@ -1,3 +1,8 @@
+#!/bin/bash
+# A/B of two builds on config 4 (k = 1024 path) on the GPU box: the big-path
+# parity tests on the in-tree build, then config-4 benches alternating
+# ab_libs/libA.so and ab_libs/libB.so (built in this container with
+# `make -C reed-solomon-novelpoly_amd OUT=$PWD/ab_libs/libX.so OBJDIR=/tmp/objX`).
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/ab4
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "big_path or reconstruct_shapes or full_size" > gpurun_out/ab4/pytest.log 2>&1; rc=$?
