@@ -31,27 +31,51 @@ constexpr int kTB = Geo<kS>::kThreads;    // 1024 threads
 constexpr size_t kSegScr = 16u * kTB * 8; // one sub-segment of a tile in thread order: 128 KiB
 
 // Scratch of one sub-segment slot: quad j of thread t at ((j * kTB) + t) * 8 bytes.
+// NT: nontemporal (streaming) accesses.  The reconstruct writes every scratch
+// word once and reads it back once, far beyond what L2 holds in between (the
+// resident workgroups' scratch is 640 MiB): streaming is -7 % there.  The
+// encode re-reads its coefficients M once per shift and keeps plain accesses
+// (streaming them cost it +5 %).
+__device__ __forceinline__ uint64_t* scr_at(uint8_t* seg, uint32_t j, uint32_t tid) {
+  return reinterpret_cast<uint64_t*>(seg + static_cast<uint32_t>((j * kTB + tid) * 8));
+}
+__device__ __forceinline__ const uint64_t* scr_at(const uint8_t* seg, uint32_t j, uint32_t tid) {
+  return reinterpret_cast<const uint64_t*>(seg + static_cast<uint32_t>((j * kTB + tid) * 8));
+}
+
+template <bool NT>
+__device__ __forceinline__ void scr_q_store(uint8_t* seg, uint32_t j, uint32_t tid, uint32_t l, uint32_t h) {
+  const uint64_t v = static_cast<uint64_t>(l) | (static_cast<uint64_t>(h) << 32);
+  if constexpr (NT)
+    __builtin_nontemporal_store(v, scr_at(seg, j, tid));
+  else
+    *scr_at(seg, j, tid) = v;
+}
+template <bool NT>
+__device__ __forceinline__ uint2 scr_q(const uint8_t* seg, uint32_t j, uint32_t tid) {
+  uint64_t v;
+  if constexpr (NT)
+    v = __builtin_nontemporal_load(scr_at(seg, j, tid));
+  else
+    v = *scr_at(seg, j, tid);
+  return make_uint2(static_cast<uint32_t>(v), static_cast<uint32_t>(v >> 32));
+}
+
+template <bool NT>
 __device__ __forceinline__ void scr_store(uint8_t* seg, uint32_t tid, const uint32_t (&L)[16],
                                           const uint32_t (&H)[16]) {
 #pragma unroll
-  for (int j = 0; j < 16; ++j)
-    *reinterpret_cast<uint2*>(seg + static_cast<uint32_t>((j * kTB + tid) * 8)) = make_uint2(L[j], H[j]);
+  for (int j = 0; j < 16; ++j) scr_q_store<NT>(seg, j, tid, L[j], H[j]);
 }
 
+template <bool NT>
 __device__ __forceinline__ void scr_load(const uint8_t* seg, uint32_t tid, uint32_t (&L)[16], uint32_t (&H)[16]) {
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    const uint2 v = *reinterpret_cast<const uint2*>(seg + static_cast<uint32_t>((j * kTB + tid) * 8));
+    const uint2 v = scr_q<NT>(seg, j, tid);
     L[j] = v.x;
     H[j] = v.y;
   }
-}
-
-__device__ __forceinline__ uint2 scr_q(const uint8_t* seg, uint32_t j, uint32_t tid) {
-  return *reinterpret_cast<const uint2*>(seg + static_cast<uint32_t>((j * kTB + tid) * 8));
-}
-__device__ __forceinline__ void scr_q_store(uint8_t* seg, uint32_t j, uint32_t tid, uint32_t l, uint32_t h) {
-  *reinterpret_cast<uint2*>(seg + static_cast<uint32_t>((j * kTB + tid) * 8)) = make_uint2(l, h);
 }
 
 __device__ __forceinline__ Mult mult_of(const DevTables& T, uint32_t c) {
@@ -135,7 +159,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
     uint32_t XL[16], XH[16];
     hi_read<kS>(tile, fresh_v(hb), XL, XH);
     hi_levels<kS, true, false>(T, VP, index, XL, XH);
-    scr_store(scrM + s * kSegScr, tid, XL, XH);
+    scr_store<false>(scrM + s * kSegScr, tid, XL, XH);
   }
 
   // ---- phase 2: top inverse levels at index 0 -> coefficients M (in place)
@@ -143,16 +167,16 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
     const Mult beta = mult_of(T, 2u);  // level 8, t = 1; the t = 0 skews at index 0 are zero
 #pragma unroll 1
     for (uint32_t j = 0; j < 16; ++j) {
-      uint2 x0 = scr_q(scrM, j, tid), x1 = scr_q(scrM + kSegScr, j, tid);
-      uint2 x2 = scr_q(scrM + 2 * kSegScr, j, tid), x3 = scr_q(scrM + 3 * kSegScr, j, tid);
+      uint2 x0 = scr_q<false>(scrM, j, tid), x1 = scr_q<false>(scrM + kSegScr, j, tid);
+      uint2 x2 = scr_q<false>(scrM + 2 * kSegScr, j, tid), x3 = scr_q<false>(scrM + 3 * kSegScr, j, tid);
       qx(x1, x0);     // level 8, t = 0: hi ^= lo
       qx(x3, x2);     // level 8, t = 1
       qm(x2, x3, beta);
       qx(x2, x0);     // level 9, t = 0
       qx(x3, x1);
-      scr_q_store(scrM + kSegScr, j, tid, x1.x, x1.y);
-      scr_q_store(scrM + 2 * kSegScr, j, tid, x2.x, x2.y);
-      scr_q_store(scrM + 3 * kSegScr, j, tid, x3.x, x3.y);
+      scr_q_store<false>(scrM + kSegScr, j, tid, x1.x, x1.y);
+      scr_q_store<false>(scrM + 2 * kSegScr, j, tid, x2.x, x2.y);
+      scr_q_store<false>(scrM + 3 * kSegScr, j, tid, x3.x, x3.y);
     }
   }
 
@@ -165,8 +189,8 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       const Mult m9 = mult_of(T, 2u * c), m80 = mult_of(T, 4u * c), m81 = mult_of(T, 4u * c + 2u);
 #pragma unroll 1
       for (uint32_t j = 0; j < 16; ++j) {
-        uint2 w0 = scr_q(scrM, j, tid), w1 = scr_q(scrM + kSegScr, j, tid);
-        uint2 w2 = scr_q(scrM + 2 * kSegScr, j, tid), w3 = scr_q(scrM + 3 * kSegScr, j, tid);
+        uint2 w0 = scr_q<false>(scrM, j, tid), w1 = scr_q<false>(scrM + kSegScr, j, tid);
+        uint2 w2 = scr_q<false>(scrM + 2 * kSegScr, j, tid), w3 = scr_q<false>(scrM + 3 * kSegScr, j, tid);
         qm(w0, w2, m9);  // level 9: lo ^= c9 * hi; hi ^= lo
         qx(w2, w0);
         qm(w1, w3, m9);
@@ -175,10 +199,10 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
         qx(w1, w0);
         qm(w2, w3, m81);  // level 8, t = 1
         qx(w3, w2);
-        scr_q_store(scrW, j, tid, w0.x, w0.y);
-        scr_q_store(scrW + kSegScr, j, tid, w1.x, w1.y);
-        scr_q_store(scrW + 2 * kSegScr, j, tid, w2.x, w2.y);
-        scr_q_store(scrW + 3 * kSegScr, j, tid, w3.x, w3.y);
+        scr_q_store<false>(scrW, j, tid, w0.x, w0.y);
+        scr_q_store<false>(scrW + kSegScr, j, tid, w1.x, w1.y);
+        scr_q_store<false>(scrW + 2 * kSegScr, j, tid, w2.x, w2.y);
+        scr_q_store<false>(scrW + 3 * kSegScr, j, tid, w3.x, w3.y);
       }
     }
 #pragma unroll 1
@@ -189,7 +213,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       stage_vpools<kS, kTB>(T, index, VP);
       __syncthreads();
       uint32_t XL[16], XH[16];
-      scr_load(scrW + s * kSegScr, tid, XL, XH);
+      scr_load<false>(scrW + s * kSegScr, tid, XL, XH);
       hi_levels<kS, false, false>(T, VP, index, XL, XH);
       hi_write<kS>(tile, fresh_v(hb), XL, XH);
       __syncthreads();
@@ -282,12 +306,12 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
     __syncthreads();
     hi_read<kS>(tile, fresh_v(hb), XL, XH);
     hi_levels<kS, true, false>(T, VP, index, XL, XH);
-    scr_store(scrY + qs * kSegScr, tid, XL, XH);
+    scr_store<true>(scrY + qs * kSegScr, tid, XL, XH);
     if (qs < 4) {  // segment 0: also D_256(y_0s)
       uint32_t DL[16] = {0}, DH[16] = {0};
       add_derivative<kS>(DL, XL, tid % G::R);
       add_derivative<kS>(DH, XH, tid % G::R);
-      scr_store(scrD + qs * kSegScr, tid, DL, DH);
+      scr_store<true>(scrD + qs * kSegScr, tid, DL, DH);
     }
   }
 
@@ -303,8 +327,8 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
         uint2 y[4], z[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          y[s] = scr_q(scrY + s * kSegScr, j, tid);
-          z[s] = scr_q(scrD + s * kSegScr, j, tid);
+          y[s] = scr_q<true>(scrY + s * kSegScr, j, tid);
+          z[s] = scr_q<true>(scrD + s * kSegScr, j, tid);
         }
         qx(y[1], y[0]);
         qx(y[3], y[2]);
@@ -336,7 +360,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
       for (int q = 1; q < NQ; ++q)
 #pragma unroll
-        for (int s = 0; s < 4; ++s) yq[q - 1][s] = scr_q(scrY + (4 * q + s) * kSegScr, j, tid);
+        for (int s = 0; s < 4; ++s) yq[q - 1][s] = scr_q<true>(scrY + (4 * q + s) * kSegScr, j, tid);
 #pragma unroll
       for (uint32_t q = 1; q < static_cast<uint32_t>(NQ); ++q) {
         uint2 (&y)[4] = yq[q - 1];
@@ -376,7 +400,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       qm(d[2], d[3], beta);
       qx(d[3], d[2]);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) scr_q_store(scrD + s * kSegScr, j, tid, d[s].x, d[s].y);
+      for (int s = 0; s < 4; ++s) scr_q_store<true>(scrD + s * kSegScr, j, tid, d[s].x, d[s].y);
     }
   }
 
@@ -388,7 +412,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
     stage_vpools<kS, kTB>(T, index, VP);
     __syncthreads();
     uint32_t XL[16], XH[16];
-    scr_load(scrD + s * kSegScr, tid, XL, XH);
+    scr_load<true>(scrD + s * kSegScr, tid, XL, XH);
     hi_levels<kS, false, false>(T, VP, index, XL, XH);
     hi_write<kS>(tile, fresh_v(hb), XL, XH);
     __syncthreads();
