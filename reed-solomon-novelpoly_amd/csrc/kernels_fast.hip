@@ -32,6 +32,11 @@
 #include <cstdlib>
 
 #include "fast_common.hpp"
+// The next tile's payload is read once: streaming (nt) LDS-DMA loads keep L2
+// for the tables and the row stores; config 3 encode -4 %.
+#ifndef NP_DMA_MOD
+#define NP_DMA_MOD " nt"
+#endif
 
 namespace np {
 namespace {
@@ -191,7 +196,7 @@ __device__ __forceinline__ void dma_tile(const uint8_t* pay, uint32_t ch0, uint8
     const uint8_t* src = pay + static_cast<size_t>(ch0 + c) * kColBytes + 8u * (b ^ sw) + 4u * (lane & 1u);
     const uint32_t dst = uniform(lds0 + c * kColBytes + 256u * (j % kPieces));
     uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" NP_DMA_MOD "\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "v"(src), "s"(dst)
                  : "memory");
@@ -375,6 +380,11 @@ __device__ __forceinline__ uint32_t row_mask16(const uint8_t* pres, uint32_t row
   return static_cast<uint32_t>(__ballot(p));
 }
 
+// Row loads keep the default policy: the merge re-reads the systematic rows
+// (streaming loads measured +0.5 % on the decode).
+#ifndef NP_ROW_LOAD_CPOL
+#define NP_ROW_LOAD_CPOL 0
+#endif
 // Issues the loads of the lane's pieces of rows row0..row0+15; the data is
 // consumed later.  Full tiles: one buffer descriptor per row whose size is 0
 // for an absent row, so that load returns zeros with no HBM traffic and no
@@ -386,7 +396,7 @@ __device__ __forceinline__ void issue_rows(uint2 (&raw)[16], const uint8_t* sh, 
 #pragma unroll
     for (int p = 0; p < 16; ++p) {
       const __amdgpu_buffer_rsrc_t r = buf_rsrc(sh + static_cast<size_t>(row0 + p) * shard_len, ((mask >> p) & 1u) ? 512u : 0u);
-      const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, 8u * lane, 0, 0);
+      const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, 8u * lane, 0, NP_ROW_LOAD_CPOL);
       raw[p] = make_uint2(v.x, v.y);
     }
   } else {
@@ -402,6 +412,7 @@ __device__ __forceinline__ void issue_rows(uint2 (&raw)[16], const uint8_t* sh, 
 // positions 16g..16g+15, i.e. bytes [32g, 32g + 32) of each of those four
 // 2K-byte output columns (two 16-byte stores per column).  Full tiles with
 // 16-byte aligned output only; saves the LDS round trip and its two barriers.
+// (Streaming stores here cost +26 %: each wave writes a quarter of a line.)
 template <int K>
 __device__ __forceinline__ void copy_out_cq(uint8_t* out_tile, uint32_t lane, uint32_t g, const uint32_t (&L)[16],
                                             const uint32_t (&H)[16]) {
