@@ -403,6 +403,32 @@ __device__ __forceinline__ void load_rows(uint2 (&raw)[NR], const uint8_t* sh, s
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
+// 8-byte accesses of data touched exactly once, with streaming (nt) cache
+// policy: payload loads of the single-tile and k = 1024 encodes (config 4
+// encode -5 %, config 2 neutral) and the k = 1024 reconstruct's output
+// (whole lines; -1 %).
+#ifndef NP_PAYLOAD_NT
+#define NP_PAYLOAD_NT 1
+#endif
+#ifndef NP_OUT8_NT
+#define NP_OUT8_NT 1
+#endif
+__device__ __forceinline__ uint2 load_once(const uint8_t* p) {
+#if NP_PAYLOAD_NT
+  const uint64_t v = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p));
+  return make_uint2(static_cast<uint32_t>(v), static_cast<uint32_t>(v >> 32));
+#else
+  return *reinterpret_cast<const uint2*>(p);
+#endif
+}
+__device__ __forceinline__ void store_once(uint8_t* p, uint2 v) {
+#if NP_OUT8_NT
+  __builtin_nontemporal_store(static_cast<uint64_t>(v.x) | (static_cast<uint64_t>(v.y) << 32), reinterpret_cast<uint64_t*>(p));
+#else
+  *reinterpret_cast<uint2*>(p) = v;
+#endif
+}
+
 // Raw buffer descriptor (V#) over [base, base + bytes): buffer loads and
 // stores take the wave-uniform part of an address from SGPRs (base, soffset)
 // and only the lane part from a VGPR, so row addressing costs no VALU.  A load

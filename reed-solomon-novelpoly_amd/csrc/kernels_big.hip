@@ -131,7 +131,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
         uint2 v[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i)
-          v[i] = *reinterpret_cast<const uint2*>(pay + gbase + static_cast<size_t>(i) * 16 * 2 * kKB);
+          v[i] = load_once(pay + gbase + static_cast<size_t>(i) * 16 * 2 * kKB);
 #pragma unroll
         for (int i = 0; i < 16; ++i) *reinterpret_cast<uint2*>(tile + (base ^ col_base_c<kS>(16u * i))) = v[i];
       } else {
@@ -453,7 +453,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
         const uint2 v = *reinterpret_cast<const uint2*>(tile + (base ^ col_base_c<kS>(16u * i)));
         uint8_t* o = outp + static_cast<size_t>(c) * 2 * kKB + 8u * m0;
         if (al_o) {
-          *reinterpret_cast<uint2*>(o) = v;
+          store_once(o, v);
         } else {
 #pragma unroll
           for (int e = 0; e < 8; ++e) o[e] = static_cast<uint8_t>((e < 4 ? v.x : v.y) >> (8 * (e & 3)));

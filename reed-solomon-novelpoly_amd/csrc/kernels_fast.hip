@@ -70,7 +70,7 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
       uint2 v[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i)
-        v[i] = (kExp & 4) ? make_uint2(i, tid) : *reinterpret_cast<const uint2*>(pay + gbase + static_cast<size_t>(i) * 32 * K);
+        v[i] = (kExp & 4) ? make_uint2(i, tid) : load_once(pay + gbase + static_cast<size_t>(i) * 32 * K);
 #pragma unroll
       for (int i = 0; i < 16; ++i) *reinterpret_cast<uint2*>(tile + (base ^ col_base_c<K>(16u * i))) = v[i];
     } else {
@@ -276,7 +276,7 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
       uint2 v[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i)
-        v[i] = (kExp & 4) ? make_uint2(i, tid) : *reinterpret_cast<const uint2*>(pay + gbase + static_cast<size_t>(i) * 32 * K);
+        v[i] = (kExp & 4) ? make_uint2(i, tid) : load_once(pay + gbase + static_cast<size_t>(i) * 32 * K);
 #pragma unroll
       for (int i = 0; i < 16; ++i) *reinterpret_cast<uint2*>(tile + (base ^ col_base_c<K>(16u * i))) = v[i];
     } else {
