@@ -35,7 +35,7 @@ constexpr size_t kSegScr = 16u * kTB * 8; // one sub-segment of a tile in thread
 // word once and reads it back once, far beyond what L2 holds in between (the
 // resident workgroups' scratch is 640 MiB): streaming is -7 % there.  The
 // encode re-reads its coefficients M once per shift and keeps plain accesses
-// (streaming them cost it +5 %).
+// for them (streaming them cost it +5 %).
 __device__ __forceinline__ uint64_t* scr_at(uint8_t* seg, uint32_t j, uint32_t tid) {
   return reinterpret_cast<uint64_t*>(seg + static_cast<uint32_t>((j * kTB + tid) * 8));
 }
@@ -92,6 +92,11 @@ __device__ __forceinline__ void qx(uint2& x, const uint2& y) {
 }
 
 // ------------------------------------------------------------------ encode ----
+// The shift's top-level outputs W are written once and read once: streaming
+// (-6 % on the encode); the coefficients M keep the default policy.
+#ifndef NP_W_NT
+#define NP_W_NT true
+#endif
 constexpr size_t kEncScratch = 8 * kSegScr;  // M (4 sub-segments) + W (4 sub-segments)
 
 __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_big(
@@ -199,10 +204,10 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
         qx(w1, w0);
         qm(w2, w3, m81);  // level 8, t = 1
         qx(w3, w2);
-        scr_q_store<false>(scrW, j, tid, w0.x, w0.y);
-        scr_q_store<false>(scrW + kSegScr, j, tid, w1.x, w1.y);
-        scr_q_store<false>(scrW + 2 * kSegScr, j, tid, w2.x, w2.y);
-        scr_q_store<false>(scrW + 3 * kSegScr, j, tid, w3.x, w3.y);
+        scr_q_store<NP_W_NT>(scrW, j, tid, w0.x, w0.y);
+        scr_q_store<NP_W_NT>(scrW + kSegScr, j, tid, w1.x, w1.y);
+        scr_q_store<NP_W_NT>(scrW + 2 * kSegScr, j, tid, w2.x, w2.y);
+        scr_q_store<NP_W_NT>(scrW + 3 * kSegScr, j, tid, w3.x, w3.y);
       }
     }
 #pragma unroll 1
@@ -213,7 +218,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       stage_vpools<kS, kTB>(T, index, VP);
       __syncthreads();
       uint32_t XL[16], XH[16];
-      scr_load<false>(scrW + s * kSegScr, tid, XL, XH);
+      scr_load<NP_W_NT>(scrW + s * kSegScr, tid, XL, XH);
       hi_levels<kS, false, false>(T, VP, index, XL, XH);
       hi_write<kS>(tile, fresh_v(hb), XL, XH);
       __syncthreads();
