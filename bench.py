@@ -119,8 +119,29 @@ def cpu_baseline(cfg, params, seconds):
     }
 
 
+def launch_replicas(args) -> int:
+    """`python bench.py --gpus N` (N > 1) outside torchrun: start N ranks under
+    torch.distributed.run as a child process -- before this process touches the
+    GPU -- and return its exit code.  Each rank then runs main() below."""
+    import socket
+    import subprocess
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch_replicas(args))
+    if world_env is not None and int(world_env) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}; launch one rank per GPU")
     import torch
     import torch.distributed as dist
 
@@ -150,9 +171,10 @@ def main():
     out_len = (sl // 2) * 2 * k
     lo, hi = partition(batch, world, rank)
 
-    g = torch.Generator(device=dev)
-    g.manual_seed(0x5EED0000 + rank)
-    payloads = torch.randint(0, 256, (batch, plen), dtype=torch.uint8, device=dev, generator=g)
+    # SURVEY.md §8(d) synthetic inputs: payload i = splitmix64 stream with seed
+    # 0x5EED_0000 + i (global payload index), erasures by partial Fisher-Yates
+    # with seed 0xE7A5_0000 + i
+    payloads = synth.payload_batch_dev(lo, hi, plen, dev)
     shards = torch.empty((batch, n, sl), dtype=torch.uint8, device=dev)
     present_h = torch.from_numpy(
         __import__("numpy").stack([synth.present_mask(i, n, erase) for i in range(lo, hi)]))
@@ -203,13 +225,13 @@ def main():
 
     kt = {name: sum(a.elapsed_time(b) for a, b in pairs) / len(pairs) for name, pairs in ev.items()}
     nshard = n  # wanted_n == n for the BASELINE configs
-    # reconstruct: the present rows the kernel decodes from (the shortest row
-    # prefix holding k present rows on the fast path, all present rows otherwise)
-    nq = (1, 2, 4) if k in (64, 128, 256) and n in (2 * k, 4 * k) else (n // k,)
-    rows = sum(synth.decode_rows(present_h[i].numpy(), n, k, nq) for i in range(batch))
+    # SURVEY.md §8(d) algorithmic bytes per payload: encode = P + n * shard_len;
+    # reconstruct = present * shard_len + (shard_len / 2) * 2k (every present
+    # row is read: the reference decodes from all of them)
+    present_rows = int(present_h.sum())
     algo = {
         "encode": batch * (plen + nshard * sl),
-        "reconstruct": batch * n + rows * sl + batch * out_len,
+        "reconstruct": present_rows * sl + batch * out_len,
     }
     # the committed PMC summary was measured on the default workload (config 3
     # at its BASELINE batch): other configs and batches report traffic null

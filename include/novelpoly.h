@@ -127,16 +127,40 @@ int np_encode_batch_dev(np_ctx* ctx, const np_code_params* params, const uint8_t
 int np_reconstruct_batch_dev(np_ctx* ctx, const np_code_params* params, const uint8_t* d_shards,
                              size_t shard_len, size_t batch_stride, const uint8_t* present, size_t batch,
                              uint8_t* d_out, size_t out_stride, void* stream);
+/* Per-payload outcome of a device batch reconstruct (device memory, one entry
+ * per payload): status = NP_OK, or NP_ERR_NEED_MORE_SHARDS when the payload
+ * has fewer than k present shards (mod.rs:178-180; the error's fields are
+ * {have, min = k, all = n}); have = its present-shard count.  A payload marked
+ * NeedMoreShards is not decoded: its output bytes are left untouched. */
+typedef struct np_payload_status {
+  int32_t status;
+  uint32_t have;
+} np_payload_status;
+
 /* Same as np_reconstruct_batch_dev with the present mask on the device
  * (d_present: batch rows of n bytes) and optionally the erasure locators already
  * computed (d_locators: batch rows of n uint16, see np_error_locator_dev).
- * d_locators == NULL: the locators are computed on the device (on the fast path
- * by a per-payload kernel that also picks the shortest row prefix holding k
- * present rows).  No host-side NeedMoreShards check. */
+ * d_locators == NULL: the locators are computed on the device by a per-payload
+ * kernel.  Every payload is decoded from all its present shards, as the
+ * reference (inc_reconstruct.rs:61-85), or copied when its k systematic shards
+ * are all present (inc_reconstruct.rs:46-50) -- bit-exact for any received
+ * bytes.  d_status (device, batch entries, may be NULL) receives each
+ * payload's np_payload_status; the NeedMoreShards check runs on the device. */
 int np_reconstruct_batch_dev2(np_ctx* ctx, const np_code_params* params, const uint8_t* d_shards,
                               size_t shard_len, size_t batch_stride, const uint8_t* d_present,
                               const uint16_t* d_locators, size_t batch, uint8_t* d_out, size_t out_stride,
-                              void* stream);
+                              np_payload_status* d_status, void* stream);
+/* OPT-IN, not crate-equivalent: for callers whose received shards are known
+ * to be an unmodified codeword (e.g. verified by a Merkle proof upstream).
+ * Like np_reconstruct_batch_dev2 with d_locators = NULL, but a payload whose
+ * first 2k shards hold k present ones may be decoded from those 2k rows only
+ * (n = 4k shapes of the fast path).  That equals the reference's output only
+ * when the shards form a codeword; for other bytes the reference's decode
+ * (a linear map of every present shard) differs. */
+int np_reconstruct_codewords_batch_dev(np_ctx* ctx, const np_code_params* params, const uint8_t* d_shards,
+                                       size_t shard_len, size_t batch_stride, const uint8_t* d_present,
+                                       size_t batch, uint8_t* d_out, size_t out_stride,
+                                       np_payload_status* d_status, void* stream);
 /* mod.rs:247-285 ReedSolomon::reconstruct_from_systematic for `batch` payloads
  * whose first k shards are all present: d_shards as for np_encode_batch_dev
  * (batch_stride >= k*shard_len, only rows 0..k-1 are read), d_out as for
@@ -154,8 +178,9 @@ int np_error_locator_dev(np_ctx* ctx, size_t n, const uint8_t* d_present, size_t
  * Same layouts as the device batch API, host pointers.  The batch is
  * pipelined over several streams in sub-batches (H2D, kernel, D2H overlap);
  * pinned host memory (hipHostMalloc / hipHostRegister) gives full overlap.
- * Reconstruct copies only the shard rows the kernels read.  Both calls return
- * when the outputs are in host memory. */
+ * Reconstruct copies only the shard rows the kernels read (the k systematic
+ * rows when every payload of the batch has them all, else all n rows).  Both
+ * calls return when the outputs are in host memory. */
 int np_encode_batch_host(np_ctx* ctx, const np_code_params* params, const uint8_t* payloads, size_t payload_len,
                          size_t payload_stride, size_t batch, uint8_t* shards, size_t batch_stride);
 int np_reconstruct_batch_host(np_ctx* ctx, const np_code_params* params, const uint8_t* shards, size_t shard_len,

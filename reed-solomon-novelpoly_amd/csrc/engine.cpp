@@ -182,7 +182,9 @@ hipError_t big_done(np_ctx* c, hipStream_t s, hipError_t e) {
 }
 
 // Scratch slots of a k = 1024 launch over `tiles` tiles: one per resident workgroup.
-size_t big_slots(size_t tiles) { return std::min((tiles + 7) / 8 * 8, np::big_resident_slots()); }
+size_t big_slots(const np_ctx* c, size_t tiles) {
+  return std::min((tiles + 7) / 8 * 8, np::big_resident_slots(c->device));
+}
 
 // Caller holds the context lock.
 hipError_t launch_encode(np_ctx* c, const np::EncodeArgs& a, hipStream_t s) {
@@ -191,34 +193,46 @@ hipError_t launch_encode(np_ctx* c, const np::EncodeArgs& a, hipStream_t s) {
     const size_t tiles = ((a.payload_len + 2 * a.k - 1) / (2 * a.k) + 255) / 256;
     uint8_t* scr = nullptr;
     size_t bytes = 0;
-    hipError_t e = big_scratch(c, big_slots(a.batch * tiles) * np::big_encode_scratch_per_tile(), s, &scr, &bytes);
+    hipError_t e = big_scratch(c, big_slots(c, a.batch * tiles) * np::big_encode_scratch_per_tile(), s, &scr, &bytes);
     if (e == hipSuccess) e = np::launch_encode_big(c->T, a, scr, bytes, s);
     return big_done(c, s, e);
   }
   return np::launch_encode_generic(c->T, a, s);
 }
 
+// Payload `b0` onward of a (a slice of the batch; status follows when set).
+np::ReconstructArgs slice(const np::ReconstructArgs& a, size_t b0, size_t cnt) {
+  np::ReconstructArgs sub = a;
+  sub.batch = cnt;
+  sub.shards = a.shards + b0 * a.batch_stride;
+  sub.present = a.present + b0 * a.n;
+  if (a.locators) sub.locators = a.locators + b0 * a.n;
+  if (a.status) sub.status = a.status + 2 * b0;
+  sub.out = a.out + b0 * a.out_stride;
+  return sub;
+}
+
+constexpr size_t kStatusBytes = 2 * sizeof(uint32_t);  // per payload (launchers.hpp ReconstructArgs::status)
+
 // a.locators == nullptr: the locators are computed on the device, into the
 // ordered context scratch (prefix locators on the fast path, full locators on
-// the generic path; fused into the k = 1024 kernels).  Caller holds the
-// context lock.
+// the generic path; fused into the k = 1024 kernels).  a.status == nullptr:
+// the per-payload status goes to the context scratch too (payloads with fewer
+// than k present rows are still skipped).  Batches larger than the scratch cap
+// go in slices.  Caller holds the context lock.
 hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream_t s) {
+  const size_t own_status = a.status ? 0 : kStatusBytes;  // scratch bytes per payload for the status
   if (np::fast_reconstruct_supported(a.n, a.k)) {
-    // per-payload decode prefix + row multipliers and their tables (from the
-    // caller's locators when given), then the decode; batches larger than the
-    // scratch cap go in slices
+    // per-payload decode rows + row multipliers and their tables (from the
+    // caller's locators when given) and the status, then the decode
     const size_t stride = np::prefix_stride(a.n, a.k);
-    const size_t per = std::max<size_t>(1, kBigScratchCap / stride);
+    const size_t per = std::max<size_t>(1, kBigScratchCap / (stride + own_status));
     for (size_t b0 = 0; b0 < a.batch; b0 += per) {
-      np::ReconstructArgs sub = a;
-      sub.batch = std::min(per, a.batch - b0);
-      sub.shards = a.shards + b0 * a.batch_stride;
-      sub.present = a.present + b0 * a.n;
-      if (a.locators) sub.locators = a.locators + b0 * a.n;
-      sub.out = a.out + b0 * a.out_stride;
+      np::ReconstructArgs sub = slice(a, b0, std::min(per, a.batch - b0));
       uint8_t* scr = nullptr;
       size_t bytes = 0;
-      hipError_t e = big_scratch(c, sub.batch * stride, s, &scr, &bytes);
+      hipError_t e = big_scratch(c, sub.batch * (stride + own_status), s, &scr, &bytes);
+      if (!a.status) sub.status = reinterpret_cast<uint32_t*>(scr + sub.batch * stride);
       if (e == hipSuccess) e = np::launch_prefix_locator(c->T, sub, scr, s);
       sub.prefix = scr;
       if (e == hipSuccess) e = np::launch_reconstruct_fast(c->T, sub, s);
@@ -229,27 +243,33 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
   }
   if (np::big_reconstruct_supported(a.n, a.k)) {
     const size_t tiles = (a.shard_len / 2 + 255) / 256;
+    const size_t per_tile = np::big_reconstruct_scratch_per_tile(a.n);
+    const size_t status_bytes = (a.batch * own_status + 255) / 256 * 256;
+    if (status_bytes + 8 * per_tile > kBigScratchCap) return hipErrorInvalidValue;  // > 13M payloads
     uint8_t* scr = nullptr;
     size_t bytes = 0;
-    hipError_t e = big_scratch(c, big_slots(a.batch * tiles) * np::big_reconstruct_scratch_per_tile(a.n), s, &scr,
-                                &bytes);
-    if (e == hipSuccess) e = np::launch_reconstruct_big(c->T, a, scr, bytes, s);
+    hipError_t e = big_scratch(c, status_bytes + big_slots(c, a.batch * tiles) * per_tile, s, &scr, &bytes);
+    np::ReconstructArgs b = a;
+    if (!a.status) b.status = reinterpret_cast<uint32_t*>(scr);
+    if (e == hipSuccess) e = np::launch_payload_status(b, s);
+    if (e == hipSuccess) e = np::launch_reconstruct_big(c->T, b, scr + status_bytes, bytes - status_bytes, s);
     return big_done(c, s, e);
   }
-  if (a.locators) return np::launch_reconstruct_generic(c->T, a, s);
-  // locators into the ordered context scratch, in slices of at most its cap
-  const size_t per = std::max<size_t>(1, kBigScratchCap / (a.n * sizeof(uint16_t)));
+  // generic path: the status, and the locators unless the caller gave them,
+  // into the ordered context scratch
+  const size_t loc_bytes = a.locators ? 0 : a.n * sizeof(uint16_t);
+  const size_t per = std::max<size_t>(1, kBigScratchCap / (loc_bytes + own_status + 1));
   for (size_t b0 = 0; b0 < a.batch; b0 += per) {
-    np::ReconstructArgs b = a;
-    b.batch = std::min(per, a.batch - b0);
-    b.shards = a.shards + b0 * a.batch_stride;
-    b.present = a.present + b0 * a.n;
-    b.out = a.out + b0 * a.out_stride;
+    np::ReconstructArgs b = slice(a, b0, std::min(per, a.batch - b0));
     uint8_t* scr = nullptr;
     size_t bytes = 0;
-    hipError_t e = big_scratch(c, b.batch * a.n * sizeof(uint16_t), s, &scr, &bytes);
-    if (e == hipSuccess) e = np::launch_error_locator(c->T, a.n, b.present, b.batch, reinterpret_cast<uint16_t*>(scr), s);
-    b.locators = reinterpret_cast<uint16_t*>(scr);
+    hipError_t e = big_scratch(c, std::max<size_t>(1, b.batch * (loc_bytes + own_status)), s, &scr, &bytes);
+    if (!a.status) b.status = reinterpret_cast<uint32_t*>(scr + b.batch * loc_bytes);
+    if (e == hipSuccess) e = np::launch_payload_status(b, s);
+    if (!a.locators) {
+      b.locators = reinterpret_cast<uint16_t*>(scr);
+      if (e == hipSuccess) e = np::launch_error_locator(c->T, a.n, b.present, b.batch, reinterpret_cast<uint16_t*>(scr), s);
+    }
     if (e == hipSuccess) e = np::launch_reconstruct_generic(c->T, b, s);
     e = big_done(c, s, e);
     if (e != hipSuccess) return e;
@@ -479,23 +499,19 @@ hipError_t pipe_sync(np_ctx* c, hipError_t e) {
   return e;
 }
 
-// Rows of each payload the reconstruct kernels read: the fast path decodes
-// from the shortest prefix of k, 2k or n rows holding k present rows
-// (kernels_fast.hip rec_tile), every other path reads all n rows.
+// Rows of each payload the reconstruct kernels read: on the fast path only the
+// k systematic rows when all of them are present (the output is those rows,
+// kernels_fast.hip k_prefix_locator), otherwise -- and on every other path --
+// all n rows: the reference decodes from every present row
+// (inc_reconstruct.rs:61-85).
 size_t rows_needed(const np_code_params* p, const uint8_t* present, size_t batch) {
   if (!np::fast_reconstruct_supported(static_cast<uint32_t>(p->n), static_cast<uint32_t>(p->k))) return p->n;
-  size_t rows = p->k;
-  for (size_t b = 0; b < batch && rows < p->n; ++b) {
+  for (size_t b = 0; b < batch; ++b) {
     const uint8_t* pr = present + b * p->n;
-    size_t have1 = 0, have2 = 0;
-    for (size_t v = 0; v < 2 * p->k; ++v) {
-      have1 += (v < p->k && pr[v]) ? 1 : 0;
-      have2 += pr[v] ? 1 : 0;
-    }
-    const size_t need = have1 == p->k ? p->k : (p->n == 4 * p->k && have2 >= p->k) ? 2 * p->k : p->n;
-    rows = std::max(rows, need);
+    for (size_t v = 0; v < p->k; ++v)
+      if (!pr[v]) return p->n;
   }
-  return rows;
+  return p->k;
 }
 
 }  // namespace
@@ -594,16 +610,19 @@ int np_error_locator_dev(np_ctx* c, size_t n, const uint8_t* d_present, size_t b
   return dev_err(np::launch_error_locator(c->T, static_cast<uint32_t>(n), d_present, batch, d_loc, pick(c, stream)));
 }
 
-int np_reconstruct_batch_dev2(np_ctx* c, const np_code_params* p, const uint8_t* d_shards, size_t shard_len,
-                              size_t bstride, const uint8_t* d_present, const uint16_t* d_loc, size_t batch,
-                              uint8_t* d_out, size_t out_stride, void* stream) {
+namespace {
+
+int reconstruct_dev2(np_ctx* c, const np_code_params* p, const uint8_t* d_shards, size_t shard_len, size_t bstride,
+                     const uint8_t* d_present, const uint16_t* d_loc, size_t batch, uint8_t* d_out,
+                     size_t out_stride, np_payload_status* d_status, void* stream, bool trusted) {
   if (!c) return fail(NP_ERR_INVALID_ARGUMENT);
   int st = check_params(p);
   if (st) return st;
   if (shard_len == 0 || (shard_len & 1)) return fail(NP_ERR_EMPTY_SHARD);
   if (!d_shards || !d_present || !d_out || bstride < p->n * shard_len || out_stride < (shard_len / 2) * 2 * p->k)
     return fail(NP_ERR_INVALID_ARGUMENT);
-  std::lock_guard<std::mutex> g(c->mu);  // scratch of the generic / k = 1024 paths
+  static_assert(sizeof(np_payload_status) == 2 * sizeof(uint32_t), "status layout of ReconstructArgs::status");
+  std::lock_guard<std::mutex> g(c->mu);  // context scratch
   (void)hipSetDevice(c->device);
   np::ReconstructArgs a{};
   a.shards = d_shards;
@@ -616,7 +635,26 @@ int np_reconstruct_batch_dev2(np_ctx* c, const np_code_params* p, const uint8_t*
   a.k = static_cast<uint32_t>(p->k);
   a.out = d_out;
   a.out_stride = out_stride;
+  a.status = reinterpret_cast<uint32_t*>(d_status);
+  a.trusted = trusted;
   return dev_err(launch_reconstruct(c, a, pick(c, stream)));
+}
+
+}  // namespace
+
+int np_reconstruct_batch_dev2(np_ctx* c, const np_code_params* p, const uint8_t* d_shards, size_t shard_len,
+                              size_t bstride, const uint8_t* d_present, const uint16_t* d_loc, size_t batch,
+                              uint8_t* d_out, size_t out_stride, np_payload_status* d_status, void* stream) {
+  return reconstruct_dev2(c, p, d_shards, shard_len, bstride, d_present, d_loc, batch, d_out, out_stride, d_status,
+                          stream, false);
+}
+
+int np_reconstruct_codewords_batch_dev(np_ctx* c, const np_code_params* p, const uint8_t* d_shards,
+                                       size_t shard_len, size_t bstride, const uint8_t* d_present, size_t batch,
+                                       uint8_t* d_out, size_t out_stride, np_payload_status* d_status,
+                                       void* stream) {
+  return reconstruct_dev2(c, p, d_shards, shard_len, bstride, d_present, nullptr, batch, d_out, out_stride,
+                          d_status, stream, true);
 }
 
 int np_reconstruct_batch_dev(np_ctx* c, const np_code_params* p, const uint8_t* d_shards, size_t shard_len,

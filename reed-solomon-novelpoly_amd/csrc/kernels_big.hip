@@ -20,6 +20,9 @@
 //
 // Reference: inc_afft.rs:139-214 / :267-332, inc_encode.rs:15-48,
 // inc_reconstruct.rs:1-113, mod.rs:117-239.
+#include <map>
+#include <mutex>
+
 #include "fast_common.hpp"
 
 namespace np {
@@ -250,6 +253,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   const uint32_t blk = tile0 + blockIdx.x;
   const TileRef tr = tile_of(blk, tiles, (a.batch & 7u) == 0);
   const uint32_t pb = tr.pb, tl = tr.tl;
+  if (a.status && uniform(a.status[2 * pb]) != 0) return;  // fewer than k present rows (k_payload_status)
   const uint32_t col0 = tl * kTile;
   const uint32_t ncols = min(static_cast<uint32_t>(kTile), nsyms - col0);
   const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);
@@ -488,19 +492,29 @@ size_t big_reconstruct_scratch_per_tile(uint32_t n) { return (4u * (n / kKB) + 4
 // Each launch covers at most that many tiles, so a launch is one full round of
 // workgroups on the CUs (no partial last round) and its scratch stays that of
 // the resident workgroups.
-size_t big_resident_slots() {
-  static size_t slots = 0;  // same for every context: the pool holds one GPU type
-  if (slots == 0) {
-    int dev = 0, cus = 0, per = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&k_reconstruct_big<4>), kTB,
-                                                     rec_big_lds<4>()) != hipSuccess ||
-        per <= 0)
-      per = 1;
-    slots = std::max<size_t>(8, static_cast<size_t>(cus) * per / 8 * 8);
-  }
+int current_device() {
+  int d = 0;
+  return hipGetDevice(&d) == hipSuccess ? d : 0;
+}
+
+// Cached per device under a lock (contexts on different threads may ask at once).
+size_t big_resident_slots(int device) {
+  static std::mutex mu;
+  static std::map<int, size_t> cache;
+  std::lock_guard<std::mutex> g(mu);
+  const auto it = cache.find(device);
+  if (it != cache.end()) return it->second;
+  int cus = 0, per = 0, prev = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+  // the occupancy query runs on the current device: switch to `device` for it
+  const bool sw = hipGetDevice(&prev) == hipSuccess && prev != device && hipSetDevice(device) == hipSuccess;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&k_reconstruct_big<4>), kTB,
+                                                   rec_big_lds<4>()) != hipSuccess ||
+      per <= 0)
+    per = 1;
+  if (sw) (void)hipSetDevice(prev);
+  const size_t slots = std::max<size_t>(8, static_cast<size_t>(cus) * per / 8 * 8);
+  cache[device] = slots;
   return slots;
 }
 
@@ -511,7 +525,7 @@ hipError_t launch_encode_big(const DevTables& T, const EncodeArgs& a, uint8_t* s
   const uint32_t tiles = static_cast<uint32_t>((nchunks + kTile - 1) / kTile);
   const size_t total = a.batch * tiles;
   // multiple of 8 keeps tile0 % 8 == 0 (tile_of)
-  const size_t per_launch = std::min(big_resident_slots(), scratch_bytes / kEncScratch / 8 * 8);
+  const size_t per_launch = std::min(big_resident_slots(current_device()), scratch_bytes / kEncScratch / 8 * 8);
   if (per_launch == 0 || total > 0xffffffffu) return hipErrorInvalidValue;
   for (size_t t0 = 0; t0 < total; t0 += per_launch) {
     const uint32_t blocks = static_cast<uint32_t>(std::min(per_launch, total - t0));
@@ -530,7 +544,7 @@ hipError_t launch_reconstruct_big(const DevTables& T, const ReconstructArgs& a, 
   const uint32_t tiles = static_cast<uint32_t>((nsyms + kTile - 1) / kTile);
   const size_t total = a.batch * tiles;
   const size_t per_tile = big_reconstruct_scratch_per_tile(a.n);
-  const size_t per_launch = std::min(big_resident_slots(), scratch_bytes / per_tile / 8 * 8);
+  const size_t per_launch = std::min(big_resident_slots(current_device()), scratch_bytes / per_tile / 8 * 8);
   if (per_launch == 0 || total > 0xffffffffu) return hipErrorInvalidValue;
   for (size_t t0 = 0; t0 < total; t0 += per_launch) {
     const uint32_t blocks = static_cast<uint32_t>(std::min(per_launch, total - t0));

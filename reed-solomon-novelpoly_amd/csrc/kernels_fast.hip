@@ -667,14 +667,17 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
 // restricted to its first K outputs is FFT(K, 0): its t = 0 skews are 0).
 // NQ = 1: every systematic row is present, the output is those rows.
 //
-// Decoding from a prefix.  The first NQ * K codeword symbols are the
-// codeword of the same message under the (NQ * K, K) code: the size-n forward
-// transform of the zero-padded coefficients copies its lower half into the
-// upper half at every top level (inc_afft.rs:267-332 with x[i + d] = 0), so its
-// first NQ * K outputs are FFT(NQ * K, 0) of the same coefficients.  A message
-// of K symbols is determined by any K of its codeword symbols, so decoding the
-// prefix with the rows beyond it treated as erased yields the reference's
-// output whenever the prefix holds at least K present rows.
+// Decoding from a prefix (trusted codewords only, ReconstructArgs::trusted).
+// The first NQ * K codeword symbols are the codeword of the same message
+// under the (NQ * K, K) code: the size-n forward transform of the zero-padded
+// coefficients copies its lower half into the upper half at every top level
+// (inc_afft.rs:267-332 with x[i + d] = 0), so its first NQ * K outputs are
+// FFT(NQ * K, 0) of the same coefficients.  A message of K symbols is
+// determined by any K of its codeword symbols, so when the received shards
+// ARE a codeword, decoding the prefix with the rows beyond it treated as
+// erased yields the reference's output.  For any other input the reference's
+// decode (a linear map of every present row) differs, so the crate-equivalent
+// entry points always decode from all n rows (or copy, NQ = 1).
 template <int K, int NQ>
 __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructArgs& a, const uint8_t* pres,
                                           const uint32_t* rows, uint8_t* smem, uint32_t pb,
@@ -838,10 +841,12 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
 // One workgroup: `tpw` consecutive 256-column tiles of one batch entry (the
 // row multipliers and the staged tables of a payload serve all of them, and
 // the next tile's rows load during a tile's copy-out), n = NQ * K.  Without
-// caller locators (a.locators == nullptr) the workgroup decodes from the
-// prefix that k_prefix_locator chose (K, 2K or n rows holding K present rows,
-// rec_tiles) with its row multipliers.  Caller locators are over all n rows, so
-// they pin the full decode.  An instance serves the payloads whose prefix has
+// caller locators (a.locators == nullptr) the workgroup decodes from the rows
+// that k_prefix_locator chose (NQ' = 1: the K systematic rows, all present;
+// NQ' = NQ: all n rows; NQ' = 2 for trusted codewords only; NQ' = 0: fewer
+// than K present rows, no decode) with its row multipliers.  Caller locators
+// are over all n rows, so they pin the full decode.  An instance serves the
+// payloads whose prefix has
 // at most SERVE segments (SERVE = 2: prefixes of 1 and 2 segments; SERVE = 4:
 // the 4-segment ones only), so each code path gets its own register allocation;
 // for n = 4K the host launches both over the same grid.
@@ -906,6 +911,31 @@ __device__ __forceinline__ void write_row_pools(const DevTables& T, const uint16
 // (present) / EXP[-loc] (erased).  Record: byte 0 = NQ' in {1, 2, NQ}, u16
 // multipliers from kPrefixHeader.  Computed once per payload instead of once
 // per column tile.
+// Present rows of payload pb in [0, K), [0, 2K) and [0, N) (256 threads).
+template <int K, int N>
+__device__ __forceinline__ void count_present(const uint8_t* pres, int& have1, int& have2, int& have) {
+  have1 = have2 = have = 0;
+  for (int r = 0; r < N; r += 256) {
+    const int v = static_cast<int>(threadIdx.x) + r;
+    const bool p = v < N && pres[v] != 0;
+    if (r < K) have1 += __syncthreads_count(v < K && p);
+    if (r < 2 * K) have2 += __syncthreads_count(v < 2 * K && p);
+    have += __syncthreads_count(p);
+  }
+}
+
+// Status of payload pb (launchers.hpp ReconstructArgs::status); true if it
+// decodes.
+__device__ __forceinline__ bool write_status(const ReconstructArgs& a, uint32_t pb, int have) {
+  const bool ok = have >= static_cast<int>(a.k);  // mod.rs:178-180
+  if (threadIdx.x == 0 && a.status) {
+    a.status[2 * pb] = ok ? 0u : kStatusNeedMoreShards;
+    a.status[2 * pb + 1] = static_cast<uint32_t>(have);
+  }
+  return ok;
+}
+
+// NQ' = 0 marks a payload with fewer than K present rows: no decode.
 template <int K, int NQ>
 __global__ __launch_bounds__(256) void k_prefix_locator(DevTables T, ReconstructArgs a, uint8_t* out) {
   constexpr int N = NQ * K;
@@ -915,15 +945,15 @@ __global__ __launch_bounds__(256) void k_prefix_locator(DevTables T, Reconstruct
   const uint8_t* pres = a.present + static_cast<size_t>(pb) * N;
   uint8_t* rec = out + static_cast<size_t>(pb) * prefix_stride_c(N, K);
   uint16_t* E = reinterpret_cast<uint16_t*>(rec + kPrefixHeader);
-  int have1 = 0, have2 = 0;  // present rows in [0, K) and [0, 2K)
-  for (int r = 0; r < 2 * K; r += 256) {
-    const int v = static_cast<int>(tid) + r;
-    have1 += __syncthreads_count(v < K && pres[v] != 0);
-    have2 += __syncthreads_count(v < 2 * K && pres[v] != 0);
-  }
-  const int nq = have1 == K ? 1 : (NQ == 4 && have2 >= K) ? 2 : NQ;
+  int have1, have2, have;  // present rows in [0, K), [0, 2K), [0, N)
+  count_present<K, N>(pres, have1, have2, have);
+  // All K systematic rows present: the output is those rows (the reference
+  // copies received rows < k, inc_reconstruct.rs:46-50), exact for any input.
+  // Otherwise the full decode from every present row, as the reference
+  // (inc_reconstruct.rs:61-85); the 2K-row prefix only for trusted codewords.
+  const int nq = !write_status(a, pb, have) ? 0 : have1 == K ? 1 : (a.trusted && NQ == 4 && have2 >= K) ? 2 : NQ;
   if (tid == 0) rec[0] = static_cast<uint8_t>(nq);
-  if (nq == 1) return;
+  if (nq <= 1) return;
   if (NQ == 4 && nq == 2) {
     fused_locator<2 * K, 256>(T, pres, W, E, PR);
   } else {
@@ -942,7 +972,11 @@ __global__ __launch_bounds__(256) void k_locator_records(DevTables T, Reconstruc
   const uint16_t* loc = a.locators + static_cast<size_t>(pb) * N;
   uint8_t* rec = out + static_cast<size_t>(pb) * prefix_stride_c(N, K);
   uint16_t* E = reinterpret_cast<uint16_t*>(rec + kPrefixHeader);
-  if (tid == 0) rec[0] = static_cast<uint8_t>(NQ);
+  int have1, have2, have;
+  count_present<K, N>(a.present + static_cast<size_t>(pb) * N, have1, have2, have);
+  const bool ok = write_status(a, pb, have);
+  if (tid == 0) rec[0] = static_cast<uint8_t>(ok ? NQ : 0);
+  if (!ok) return;
   // mul(x, log m) == x * EXP[m] (inc_log_mul.rs:42-49)
   for (uint32_t v = tid; v < static_cast<uint32_t>(N); v += 256) E[v] = T.exp[loc[v]];
   write_row_pools(T, E, N, rec + prefix_pools_offset(N));

@@ -141,6 +141,7 @@ __global__ __launch_bounds__(kThreads) void k_reconstruct_generic(DevTables T, R
   const uint32_t s0 = blockIdx.x * cols;
   const uint32_t ncol = min(cols, nsyms - s0);
   const uint32_t n = a.n, k = a.k;
+  if (a.status && a.status[2 * b] != 0) return;  // fewer than k present rows (k_payload_status)
   const uint8_t* sh = a.shards + b * a.batch_stride;
   const uint8_t* pres = a.present + b * n;
   const uint16_t* loc = a.locators + b * n;
@@ -205,6 +206,22 @@ __global__ __launch_bounds__(1024) void k_error_locator(DevTables T, uint32_t n,
   lds_walsh(lw, 65536u);
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
     locators[b * n + i] = pres[i] ? lw[i] : static_cast<uint16_t>(kQ - lw[i]);
+}
+
+// mod.rs:171-180: a payload with fewer than k present rows is NeedMoreShards
+// {have, min: k, all: n}; one 256-thread workgroup per payload.
+__global__ __launch_bounds__(256) void k_payload_status(ReconstructArgs a) {
+  const size_t b = blockIdx.x;
+  const uint8_t* pres = a.present + b * a.n;
+  int have = 0;
+  for (uint32_t r = 0; r < a.n; r += 256) {
+    const uint32_t v = r + threadIdx.x;
+    have += __syncthreads_count(v < a.n && pres[v] != 0);
+  }
+  if (threadIdx.x == 0) {
+    a.status[2 * b] = have >= static_cast<int>(a.k) ? 0u : kStatusNeedMoreShards;
+    a.status[2 * b + 1] = static_cast<uint32_t>(have);
+  }
 }
 
 // ------------------------------------------------------------ parity hooks ----
@@ -328,6 +345,13 @@ hipError_t launch_error_locator(const DevTables& T, uint32_t n, const uint8_t* p
                                 uint16_t* locators, hipStream_t s) {
   if (batch == 0) return hipSuccess;
   k_error_locator<<<static_cast<uint32_t>(batch), 1024, 65536 * sizeof(uint16_t), s>>>(T, n, present, locators);
+  return hipGetLastError();
+}
+
+hipError_t launch_payload_status(const ReconstructArgs& a, hipStream_t s) {
+  if (a.batch == 0 || !a.status) return hipSuccess;
+  if (a.batch > 0x7fffffffu) return hipErrorInvalidValue;
+  k_payload_status<<<static_cast<uint32_t>(a.batch), 256, 0, s>>>(a);
   return hipGetLastError();
 }
 

@@ -31,13 +31,29 @@ struct ReconstructArgs {
   uint32_t n, k;
   uint8_t* out;
   size_t out_stride;
+  // device, batch x {status, have}: NP_ERR_NEED_MORE_SHARDS (mod.rs:178-180)
+  // and the present-row count of a payload with fewer than k present rows
+  // (its output is left untouched), {0, have} otherwise.  Written by
+  // launch_payload_status or, on the fast path, by launch_prefix_locator;
+  // the decode kernels skip the payloads it marks.
+  uint32_t* status;
+  // Codeword-only callers (np_reconstruct_codewords_batch_dev): the fast path
+  // may decode from the shortest row prefix holding k present rows, which
+  // equals the reference's output only when the received shards form a
+  // codeword.  Never set by the crate-equivalent entry points.
+  bool trusted;
 };
+
+// Status code of a payload with fewer than k present rows (include/novelpoly.h).
+constexpr uint32_t kStatusNeedMoreShards = 5;
 
 // ---- generic path: any power-of-two n <= 65536, k <= n/2 (kernels_generic.hip) ----
 hipError_t launch_encode_generic(const DevTables& T, const EncodeArgs& a, hipStream_t s);
 hipError_t launch_reconstruct_generic(const DevTables& T, const ReconstructArgs& a, hipStream_t s);
 hipError_t launch_error_locator(const DevTables& T, uint32_t n, const uint8_t* present, size_t batch,
                                 uint16_t* locators, hipStream_t s);
+// a.status of every payload from its present rows (generic and k = 1024 paths).
+hipError_t launch_payload_status(const ReconstructArgs& a, hipStream_t s);
 // parity hooks
 hipError_t launch_afft(const DevTables& T, uint16_t* data, uint32_t size, uint32_t index, size_t cols,
                        bool inverse, hipStream_t s);
@@ -60,11 +76,12 @@ bool fast_encode_supported(uint32_t n, uint32_t k);
 bool fast_reconstruct_supported(uint32_t n, uint32_t k);
 hipError_t launch_encode_fast(const DevTables& T, const EncodeArgs& a, hipStream_t s);
 hipError_t launch_reconstruct_fast(const DevTables& T, const ReconstructArgs& a, hipStream_t s);
-// Per payload: the shortest row prefix (k, 2k or n rows) holding k present rows
-// and the folded erasure locator over it as row multipliers, with their v_perm
-// tables, for the fast reconstruct kernel (a.prefix); with a.locators set, the
-// caller's locators over all n rows instead (the full decode).  `out` holds
-// batch * prefix_stride(n, k) bytes.
+// Per payload: the rows to decode from (k rows when all k systematic rows are
+// present -- a copy --, otherwise all n; with a.trusted also the 2k-row
+// prefix when it holds k present rows), the folded erasure locator over them
+// as row multipliers with their v_perm tables for the fast reconstruct kernel
+// (a.prefix), and a.status; with a.locators set, the caller's locators over
+// all n rows instead.  `out` holds batch * prefix_stride(n, k) bytes.
 size_t prefix_stride(uint32_t n, uint32_t k);
 hipError_t launch_prefix_locator(const DevTables& T, const ReconstructArgs& a, uint8_t* out, hipStream_t s);
 
@@ -72,7 +89,7 @@ hipError_t launch_prefix_locator(const DevTables& T, const ReconstructArgs& a, u
 bool big_encode_supported(uint32_t n, uint32_t k);
 bool big_reconstruct_supported(uint32_t n, uint32_t k);
 size_t big_encode_scratch_per_tile();
-size_t big_resident_slots();  // scratch slots a launch uses at most (multiple of 8)
+size_t big_resident_slots(int device);  // scratch slots a launch uses at most (multiple of 8)
 size_t big_reconstruct_scratch_per_tile(uint32_t n);
 hipError_t launch_encode_big(const DevTables& T, const EncodeArgs& a, uint8_t* scratch, size_t scratch_bytes,
                              hipStream_t s);

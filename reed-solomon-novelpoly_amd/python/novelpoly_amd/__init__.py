@@ -68,7 +68,8 @@ def lib() -> C.CDLL:
                 C.c_int, [vp, P, C.POINTER(vp), C.POINTER(_sz), _sz, vp, _sz, C.POINTER(_sz)]),
             "np_encode_batch_dev": (C.c_int, [vp, P, vp, _sz, _sz, _sz, vp, _sz, vp]),
             "np_reconstruct_batch_dev": (C.c_int, [vp, P, vp, _sz, _sz, vp, _sz, vp, _sz, vp]),
-            "np_reconstruct_batch_dev2": (C.c_int, [vp, P, vp, _sz, _sz, vp, vp, _sz, vp, _sz, vp]),
+            "np_reconstruct_batch_dev2": (C.c_int, [vp, P, vp, _sz, _sz, vp, vp, _sz, vp, _sz, vp, vp]),
+            "np_reconstruct_codewords_batch_dev": (C.c_int, [vp, P, vp, _sz, _sz, vp, _sz, vp, _sz, vp, vp]),
             "np_error_locator_dev": (C.c_int, [vp, _sz, vp, _sz, vp, vp]),
             "np_reconstruct_from_systematic_batch_dev": (C.c_int, [vp, P, vp, _sz, _sz, _sz, vp, _sz, vp]),
             "np_encode_batch_host": (C.c_int, [vp, P, vp, _sz, _sz, _sz, vp, _sz]),
@@ -409,11 +410,43 @@ def error_locator_dev(n: int, d_present: int, batch: int, d_locators: int, ctx: 
 
 def reconstruct_batch_dev2(params: CodeParams, d_shards: int, shard_len: int, batch_stride: int, d_present: int,
                            d_locators: int, batch: int, d_out: int, out_stride: int,
-                           ctx: Optional[Context] = None, stream: int = 0) -> None:
+                           ctx: Optional[Context] = None, stream: int = 0, d_status: int = 0) -> None:
+    """Device batch reconstruct, bit-exact with the crate for any received bytes.
+
+    d_status: device address of ``batch`` np_payload_status entries (int32 status,
+    uint32 have; see :func:`payload_errors`) or 0."""
     ctx = ctx or default_context()
     _raise(lib().np_reconstruct_batch_dev2(ctx.handle, C.byref(params._c()), d_shards, shard_len, batch_stride,
                                            d_present, d_locators or None, batch, d_out, out_stride,
-                                           stream or None))
+                                           d_status or None, stream or None))
+
+
+def reconstruct_codewords_batch_dev(params: CodeParams, d_shards: int, shard_len: int, batch_stride: int,
+                                    d_present: int, batch: int, d_out: int, out_stride: int,
+                                    ctx: Optional[Context] = None, stream: int = 0, d_status: int = 0) -> None:
+    """OPT-IN prefix decode for shards known to form a codeword (include/novelpoly.h);
+    not crate-equivalent for other bytes."""
+    ctx = ctx or default_context()
+    _raise(lib().np_reconstruct_codewords_batch_dev(ctx.handle, C.byref(params._c()), d_shards, shard_len,
+                                                    batch_stride, d_present, batch, d_out, out_stride,
+                                                    d_status or None, stream or None))
+
+
+def payload_errors(params: CodeParams, status_pairs) -> List[Optional[Error]]:
+    """np_payload_status entries (a sequence of (status, have) pairs, e.g. a
+    ``batch x 2`` int array copied to the host) as the crate's per-call result:
+    None for a decoded payload, ``NeedMoreShards(have, k, n)`` (mod.rs:178-180)
+    otherwise."""
+    out: List[Optional[Error]] = []
+    for st, have in status_pairs:
+        st = int(st)
+        if st == 0:
+            out.append(None)
+        elif st == NeedMoreShards.code:
+            out.append(NeedMoreShards(int(have), params.k(), params.n()))
+        else:
+            out.append(DeviceError(st, "unexpected payload status"))
+    return out
 
 
 def encode_batch_host(params: CodeParams, payloads: int, payload_len: int, payload_stride: int, batch: int,

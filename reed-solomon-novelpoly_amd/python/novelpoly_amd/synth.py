@@ -77,13 +77,31 @@ def present_mask(index: int, n: int, count: int) -> np.ndarray:
     return m
 
 
-def decode_rows(present: np.ndarray, n: int, k: int, fast_nq: tuple = (1, 2, 4)) -> int:
-    """Shard rows the fused-locator reconstruct kernel reads for one payload: it
-    decodes from the shortest prefix of q*k rows (q in ``fast_nq``, q*k <= n)
-    that holds k present rows (kernels_fast.hip, rec_tile), reading only the
-    present rows of that prefix.  Used for the algorithmic byte count."""
-    present = np.asarray(present).astype(bool)
-    for q in fast_nq:
-        if q * k <= n and int(present[: q * k].sum()) >= k:
-            return int(present[: q * k].sum())
-    return int(present[:n].sum())
+def _s64(x: int) -> int:
+    """A u64 constant as the int64 with the same bits (torch has no uint64 math)."""
+    return x - (1 << 64) if x >= 1 << 63 else x
+
+
+def payload_batch_dev(lo: int, hi: int, nbytes: int, device):
+    """Payloads lo..hi-1 as a (hi - lo) x nbytes uint8 torch tensor on `device`,
+    bit-identical to :func:`payload` (splitmix64 in int64 arithmetic: products
+    wrap mod 2^64, logical shifts by masking).  Generates the bench's 1 GiB
+    batches in milliseconds instead of seconds of host work."""
+    import torch
+
+    words = (nbytes + 7) // 8
+    seeds = torch.arange(lo, hi, dtype=torch.int64, device=device) + 0x5EED0000
+    idx = torch.arange(1, words + 1, dtype=torch.int64, device=device)
+    out = torch.empty((hi - lo, words), dtype=torch.int64, device=device)
+    gamma, m1, m2 = _s64(0x9E3779B97F4A7C15), _s64(0xBF58476D1CE4E5B9), _s64(0x94D049BB133111EB)
+
+    def lsr(z, s):
+        return (z >> s) & ((1 << (64 - s)) - 1)
+
+    step = max(1, (1 << 24) // max(1, words))  # bound the temporaries to ~16M words
+    for b0 in range(0, hi - lo, step):
+        z = seeds[b0:b0 + step, None] + idx[None, :] * gamma
+        z = (z ^ lsr(z, 30)) * m1
+        z = (z ^ lsr(z, 27)) * m2
+        out[b0:b0 + step] = z ^ lsr(z, 31)
+    return out.view(torch.uint8)[:, :nbytes].contiguous() if nbytes % 8 else out.view(torch.uint8)

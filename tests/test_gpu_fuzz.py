@@ -4,7 +4,9 @@ batch sizes, payload/shard/output strides, wanted_n, erasure patterns of every
 decode-prefix mode and tile-per-workgroup counts (NP_ENC_TPW / NP_REC_TPW pin
 the multi-tile kernels' split).  Complements the fixed shapes of
 test_gpu_parity.py; like the reference's quickcheck round trips
-(novel_poly_basis/tests.rs), every case is checked bit for bit."""
+(novel_poly_basis/tests.rs), every case is checked bit for bit -- including
+received rows that are not a codeword (a corrupted present row), as the
+reference's reconstruct fuzz target feeds (fuzzit/src/reconstruct.rs:15-43)."""
 import numpy as np
 import pytest
 
@@ -68,6 +70,13 @@ def test_fuzz_device_batch_roundtrip(gpu, oracle, monkeypatch, case):
         return  # reconstruct needs every codeword row
     modes = ["random", "systematic_kept", "heavy"]
     pres = np.stack([_erasures(rng, n, k, modes[(case + b) % 3]) for b in range(batch)])
+    # half the payloads get a corrupted present row (not a codeword any more):
+    # the decode must still equal the reference's linear map of every present row
+    for b in range(batch):
+        if rng.random() < 0.5:
+            v = int(rng.choice(np.flatnonzero(pres[b])))
+            rows[b][v] ^= rng.integers(1, 256, sl, dtype=np.uint8)
+            ds[b, v * sl:(v + 1) * sl] = torch.from_numpy(rows[b][v].copy()).cuda()
     dpres = dev(pres)
     olen = (sl // 2) * 2 * k
     ostride = olen + int(rng.choice([0, 0, 8, 3]))
@@ -81,7 +90,6 @@ def test_fuzz_device_batch_roundtrip(gpu, oracle, monkeypatch, case):
         st, want = oracle.reconstruct(recv, n, k)
         assert st == 0
         assert o[b, :olen].tobytes() == want, ("reconstruct", case, b)
-        assert want[:plen] == pls[b, :plen].tobytes()
 
 
 def dev(a):

@@ -119,18 +119,13 @@ def test_ctx_without_gpu_reports_no_device():
         npa.Context(0)
 
 
-def test_decode_rows_prefix_rule():
-    """synth.decode_rows mirrors the fast reconstruct's prefix choice
-    (kernels_fast.hip rec_tile, engine.cpp rows_needed): k rows if every
-    systematic row is present, 2k if [0, 2k) holds k present rows, else n."""
-    from novelpoly_amd import synth
+def test_payload_batch_dev_matches_splitmix():
+    """bench.py's torch generator of the §8(d) payloads equals synth.payload
+    (splitmix64, seed 0x5EED_0000 + index), here on the CPU device."""
+    import torch
 
-    n, k = 1024, 256
-    pres = np.ones(n, np.uint8)
-    assert synth.decode_rows(pres, n, k) == k
-    pres[:10] = 0
-    assert synth.decode_rows(pres, n, k) == 2 * k - 10
-    pres[:] = 1
-    pres[: 2 * k - k + 1] = 0  # k - 1 present in [0, 2k)
-    assert synth.decode_rows(pres, n, k) == int(pres.sum())
-    assert synth.decode_rows(pres, n, k, (n // k,)) == int(pres.sum())
+    for lo, hi, nbytes in ((0, 3, 64), (1022, 1024, 1 << 12), (5, 7, 1001)):
+        got = synth.payload_batch_dev(lo, hi, nbytes, torch.device("cpu")).numpy()
+        for i in range(lo, hi):
+            assert got[i - lo].tobytes() == synth.payload(i, nbytes), (lo, hi, nbytes, i)
+

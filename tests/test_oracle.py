@@ -260,3 +260,24 @@ def test_locator_fold_identity(oracle, n):
         loc = wht((wht(erased.astype(np.int64)) % 65535) * fold % 65535) % 65535
         loc = np.where(erased, (65535 - loc) % 65535, loc)
         assert np.array_equal(loc % 65535, want % 65535), trial
+
+
+def test_corrupted_row_beyond_prefix_changes_reference(oracle):
+    """Pins that tests/test_gpu_noncodeword.py's corrupted-row case is
+    meaningful: at config 3 the reference's reconstruct output depends on a
+    present row >= 2k even when [0, 2k) holds k present rows, so a decoder that
+    reads only the first 2k rows cannot match it on non-codeword input."""
+    import numpy as np
+    from novelpoly_amd import synth
+
+    n, k, sl = 1024, 256, 64
+    rng = np.random.default_rng(3)
+    rows = rng.integers(0, 256, (n, sl), dtype=np.uint8)
+    pres = synth.present_mask(0, n, 341)
+    assert pres[: 2 * k].sum() >= k
+    recv = lambda: [rows[i].tobytes() if pres[i] else None for i in range(n)]  # noqa: E731
+    st, a = oracle.reconstruct(recv(), n, k)
+    v = [i for i in range(2 * k, n) if pres[i]][0]
+    rows[v] ^= 0xFF
+    st2, b = oracle.reconstruct(recv(), n, k)
+    assert st == st2 == 0 and a != b
