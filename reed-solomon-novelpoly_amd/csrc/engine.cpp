@@ -371,6 +371,9 @@ int np_ctx_create(int device, np_ctx** out) {
   if (e == hipSuccess) e = upload(c, t.log_walsh, &c->T.log_walsh);
   if (e == hipSuccess) e = upload(c, t.lw_fold, &c->T.lw_fold);
   if (e == hipSuccess) e = upload(c, t.perm_pools, &c->T.perm_pools);
+  if (e == hipSuccess) e = upload(c, t.tower_pools, &c->T.tower_pools);
+  if (e == hipSuccess) e = upload(c, t.in_pools, &c->T.in_pools);
+  if (e == hipSuccess) e = upload(c, t.out_pools, &c->T.out_pools);
   if (e == hipSuccess) e = upload(c, std::vector<uint8_t>(np::kZeroPageBytes, 0), &c->T.zeros);
   if (e == hipSuccess) {
     std::lock_guard<std::mutex> g(g_cfg_mu);

@@ -224,14 +224,20 @@ __device__ __forceinline__ Mult make_mult(const uint32_t (&p)[20]) {
 }
 
 // From the SGPR half plus the VGPR half staged in LDS (two broadcast
-// ds_read_b128, no VALU work).
+// ds_read_b128, no VALU work).  SUB: a subfield pool (field_tables.hpp kSubV /
+// kSubS), whose 6 SGPR and 4 VGPR dwords are all the multiply reads.
+template <bool SUB = false>
 __device__ __forceinline__ Mult staged_mult(const uint32_t (&sp)[12], const uint32_t* vp) {
   Mult m;
+  constexpr int ns = SUB ? 6 : 12;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) m.s[i] = sp[i];
-  const uint4 a = *reinterpret_cast<const uint4*>(vp), b = *reinterpret_cast<const uint4*>(vp + 4);
+  for (int i = 0; i < ns; ++i) m.s[i] = sp[i];
+  const uint4 a = *reinterpret_cast<const uint4*>(vp);
   m.v[0] = a.x, m.v[1] = a.y, m.v[2] = a.z, m.v[3] = a.w;
-  m.v[4] = b.x, m.v[5] = b.y, m.v[6] = b.z, m.v[7] = b.w;
+  if constexpr (!SUB) {
+    const uint4 b = *reinterpret_cast<const uint4*>(vp + 4);
+    m.v[4] = b.x, m.v[5] = b.y, m.v[6] = b.z, m.v[7] = b.w;
+  }
   return m;
 }
 
@@ -251,25 +257,93 @@ __device__ __forceinline__ void qmul_set(uint32_t& ol, uint32_t& oh, uint32_t yl
   qplane_set(oh, s, m.v[4], m.v[5], m.v[6], m.v[7], m.s[6], m.s[7], m.s[8], m.s[9], m.s[10], m.s[11]);
 }
 
+// ---- subfield multiply (tower coordinates, field_tables.hpp) ----
+// For c in GF(2^8) both byte planes of a symbol in tower coordinates are
+// GF(2^8) elements that c multiplies separately: per plane 3 lookups
+// (bits 0-2, 3-5, 6-7) instead of the 6 of a full 16 x 16 map.  Pool layout
+// kSubV / kSubS: VGPR dwords v[0..1] (plane a), v[2..3] (plane b); SGPR dwords
+// s[0..2] (a), s[3..5] (b) of Mult.
+__device__ __forceinline__ void qplane_sub(uint32_t& acc, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t va,
+                                           uint32_t vb, uint32_t sa, uint32_t sb, uint32_t sc) {
+  uint32_t t0, t1, t2;
+  asm volatile(
+      "v_perm_b32 %[t0], %[sa], %[va], %[s0]\n\t"
+      "v_perm_b32 %[t1], %[sb], %[vb], %[s1]\n\t"
+      "v_perm_b32 %[t2], %[sc], %[sc], %[s2]\n\t"
+      "v_bitop3_b32 %[acc], %[acc], %[t0], %[t1] bitop3:0x96\n\t"
+      "v_xor_b32 %[acc], %[acc], %[t2]"
+      : [acc] "+v"(acc), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2)
+      : [s0] "v"(s0), [s1] "v"(s1), [s2] "v"(s2), [va] "v"(va), [vb] "v"(vb), [sa] "s"(sa), [sb] "s"(sb),
+        [sc] "s"(sc));
+}
+
+__device__ __forceinline__ void qplane_sub_set(uint32_t& out, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t va,
+                                               uint32_t vb, uint32_t sa, uint32_t sb, uint32_t sc) {
+  uint32_t t0, t1, t2;
+  asm volatile(
+      "v_perm_b32 %[t0], %[sa], %[va], %[s0]\n\t"
+      "v_perm_b32 %[t1], %[sb], %[vb], %[s1]\n\t"
+      "v_perm_b32 %[t2], %[sc], %[sc], %[s2]\n\t"
+      "v_bitop3_b32 %[out], %[t0], %[t1], %[t2] bitop3:0x96"
+      : [out] "=&v"(out), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2)
+      : [s0] "v"(s0), [s1] "v"(s1), [s2] "v"(s2), [va] "v"(va), [vb] "v"(vb), [sa] "s"(sa), [sb] "s"(sb),
+        [sc] "s"(sc));
+}
+
+// x ^= c*y, c in GF(2^8), tower coordinates.
+__device__ __forceinline__ void qmul_sub(uint32_t& xl, uint32_t& xh, uint32_t yl, uint32_t yh, const Mult& m) {
+  uint32_t s[6];
+  selectors(yl, yh, s);
+  qplane_sub(xl, s[0], s[1], s[2], m.v[0], m.v[1], m.s[0], m.s[1], m.s[2]);
+  qplane_sub(xh, s[3], s[4], s[5], m.v[2], m.v[3], m.s[3], m.s[4], m.s[5]);
+}
+
+// (ol, oh) = c*y, c in GF(2^8), tower coordinates.
+__device__ __forceinline__ void qmul_sub_set(uint32_t& ol, uint32_t& oh, uint32_t yl, uint32_t yh, const Mult& m) {
+  uint32_t s[6];
+  selectors(yl, yh, s);
+  qplane_sub_set(ol, s[0], s[1], s[2], m.v[0], m.v[1], m.s[0], m.s[1], m.s[2]);
+  qplane_sub_set(oh, s[3], s[4], s[5], m.v[2], m.v[3], m.s[3], m.s[4], m.s[5]);
+}
+
+// x ^= c*y: the subfield form (SUB) or the full 16 x 16 map.
+template <bool SUB>
+__device__ __forceinline__ void qmul_mode(uint32_t& xl, uint32_t& xh, uint32_t yl, uint32_t yh, const Mult& m) {
+  if constexpr (SUB)
+    qmul_sub(xl, xh, yl, yh, m);
+  else
+    qmul(xl, xh, yl, yh, m);
+}
+
 typedef const __attribute__((address_space(4))) uint32_t* cpool_t;
 
 // Multiplier tables of the additive element c via the scalar cache (c is
-// wave-uniform, so this is s_load).
+// wave-uniform, so this is s_load); TW: tower coordinates (tower_pools).
+template <bool TW = false>
 __device__ __forceinline__ void pool_of(const DevTables& T, uint32_t c, uint32_t (&p)[20]) {
   // opaque index: two fetches of the same table (e.g. beta, or the index-0
   // skews shared by an IFFT and an FFT) must not be merged into one long-lived value
   asm volatile("" : "+s"(c));
-  const cpool_t q = (cpool_t)(T.perm_pools) + c * kPoolWords;
+  const cpool_t q = (cpool_t)(TW ? T.tower_pools : T.perm_pools) + c * kPoolWords;
 #pragma unroll
   for (int i = 0; i < 20; ++i) p[i] = q[i];
 }
 
+// The skew tables of a transform: Cantor coordinates (perm_pools, the k = 1024
+// kernels) or tower coordinates (tower_pools, TW: the fast kernels).
+template <bool TW>
+__device__ __forceinline__ const uint32_t* skew_pools(const DevTables& T) {
+  return TW ? T.tower_pools : T.perm_pools;
+}
+
 // Only the SGPR half (dwords 8..19) of the tables of c.
+// SUB: only the 6 dwords a subfield pool uses.
+template <bool TW = false, bool SUB = false>
 __device__ __forceinline__ void spool_of(const DevTables& T, uint32_t c, uint32_t (&p)[12]) {
   asm volatile("" : "+s"(c));
-  const cpool_t q = (cpool_t)(T.perm_pools) + c * kPoolWords + 8;
+  const cpool_t q = (cpool_t)(skew_pools<TW>(T)) + c * kPoolWords + 8;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) p[i] = q[i];
+  for (int i = 0; i < (SUB ? 6 : 12); ++i) p[i] = q[i];
 }
 
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -311,6 +385,9 @@ __device__ __forceinline__ DevTables fresh_tables(const DevTables& T) {
   t.log_walsh = fresh(t.log_walsh);
   t.lw_fold = fresh(t.lw_fold);
   t.perm_pools = fresh(t.perm_pools);
+  t.tower_pools = fresh(t.tower_pools);
+  t.in_pools = fresh(t.in_pools);
+  t.out_pools = fresh(t.out_pools);
   t.zeros = fresh(t.zeros);
   return t;
 }
@@ -521,23 +598,24 @@ __device__ __forceinline__ void pipelined_rec(RF rec, NF need, GF group) {
 // Same for a transform whose VGPR table halves are staged in LDS (VP, see
 // stage_vpools): group f reads them at vaddr(f); only the SGPR half is
 // prefetched with s_load.
-template <int F, int NG, typename CF, typename VF, typename GF>
-__device__ __forceinline__ void spipe_step(const DevTables& T, CF& cval, VF& vaddr, GF& group, uint32_t (&cur)[12],
-                                           uint32_t (&nxt)[12]) {
+// subf(Int<f>) -> std::integral_constant<bool, group f multiplies in the subfield form>.
+template <int F, int NG, bool TW, typename CF, typename VF, typename SF, typename GF>
+__device__ __forceinline__ void spipe_step(const DevTables& T, CF& cval, VF& vaddr, SF& subf, GF& group,
+                                           uint32_t (&cur)[12], uint32_t (&nxt)[12]) {
   if constexpr (F < NG) {
-    if constexpr (F + 1 < NG) spool_of(T, cval(Int<F + 1>{}), nxt);
+    if constexpr (F + 1 < NG) spool_of<TW, decltype(subf(Int<F + 1>{}))::value>(T, cval(Int<F + 1>{}), nxt);
     __builtin_amdgcn_sched_barrier(0);
-    group(Int<F>{}, staged_mult(cur, vaddr(Int<F>{})));
+    group(Int<F>{}, staged_mult<decltype(subf(Int<F>{}))::value>(cur, vaddr(Int<F>{})));
     __builtin_amdgcn_sched_barrier(0);
-    spipe_step<F + 1, NG>(T, cval, vaddr, group, nxt, cur);
+    spipe_step<F + 1, NG, TW>(T, cval, vaddr, subf, group, nxt, cur);
   }
 }
 
-template <int NG, typename CF, typename VF, typename GF>
-__device__ __forceinline__ void pipelined_staged(const DevTables& T, CF cval, VF vaddr, GF group) {
+template <int NG, bool TW = false, typename CF, typename VF, typename SF, typename GF>
+__device__ __forceinline__ void pipelined_staged(const DevTables& T, CF cval, VF vaddr, SF subf, GF group) {
   uint32_t pa[12], pb[12];
-  spool_of(T, cval(Int<0>{}), pa);
-  spipe_step<0, NG>(T, cval, vaddr, group, pa, pb);
+  spool_of<TW, decltype(subf(Int<0>{}))::value>(T, cval(Int<0>{}), pa);
+  spipe_step<0, NG, TW>(T, cval, vaddr, subf, group, pa, pb);
 }
 
 // LDS slot of the multiplier of group t at level b of a size-K transform:
@@ -549,8 +627,10 @@ __host__ __device__ constexpr uint32_t vslot(int b, uint32_t t) {
 
 // Copies the VGPR halves (8 dwords) of every multiplier of a size-K transform
 // at `index` into VP (K - 1 slots).  Caller synchronises.
+// tw: tower_pools (the transform runs in tower coordinates), else perm_pools.
 template <int K, int NT>
-__device__ __forceinline__ void stage_vpools(const DevTables& T, uint32_t index, uint32_t* VP) {
+__device__ __forceinline__ void stage_vpools(const DevTables& T, uint32_t index, uint32_t* VP, bool tw = false) {
+  const uint32_t* pools = tw ? T.tower_pools : T.perm_pools;
   for (uint32_t i = threadIdx.x; i < 2u * (K - 1); i += NT) {
     const uint32_t slot = i >> 1, half = i & 1u;
     uint32_t b = 0;
@@ -558,7 +638,7 @@ __device__ __forceinline__ void stage_vpools(const DevTables& T, uint32_t index,
     const uint32_t t = slot - static_cast<uint32_t>(K - (K >> b));
     const uint32_t c = 2u * t + (index >> b);
     *reinterpret_cast<uint4*>(VP + 8 * slot + 4 * half) =
-        *reinterpret_cast<const uint4*>(T.perm_pools + static_cast<size_t>(c) * kPoolWords + 4 * half);
+        *reinterpret_cast<const uint4*>(pools + static_cast<size_t>(c) * kPoolWords + 4 * half);
   }
 }
 
@@ -601,7 +681,50 @@ __host__ __device__ constexpr int hi_groups() {
 // 16g + p): inverse transforms skip the groups none of whose input rows is
 // set (all-zero inputs stay zero), forward ones the groups none of whose
 // output rows is set (outputs nobody reads); ~0u runs every group.
-template <int K, bool INVERSE, bool INDEX0>
+// Tower coordinates (field_tables.hpp HostTables::tower_a).  GEN >= 0: the
+// transform runs in tower coordinates and its levels b >= GEN multiply in the
+// subfield form (every skew of such a level lies in GF(2^8)), levels b < GEN
+// with the full map; GEN = -1: Cantor coordinates (perm_pools).  For a size-K
+// transform at index I the skews of level b are Cantor((I >> b) + 2t), all
+// below 256 exactly when (I >> b) < 256 (I is a multiple of K), so the right
+// GEN is gen_of(I).
+template <int GEN>
+constexpr bool kSubLevel(int b) {
+  return GEN >= 0 && b >= GEN;
+}
+
+__host__ __device__ constexpr uint32_t gen_of(uint32_t index) {
+  uint32_t g = 0;
+  while ((index >> g) >= 256u) ++g;
+  return g;
+}
+
+// f(Int<G>) for G = gen_of(index) when MING <= G <= MAXG (a wave-uniform
+// branch over compile-time instances; the caller guarantees G >= MING);
+// beyond MAXG f(Int<-1>) (Cantor coordinates, the caller converts) when
+// FALLBACK, else f(Int<MAXG>) (the caller guarantees G <= MAXG).
+template <int MING, int MAXG, bool FALLBACK, typename F>
+__device__ __forceinline__ void with_gen(uint32_t index, F&& f) {
+  const uint32_t g = __builtin_amdgcn_readfirstlane(gen_of(index));
+  if constexpr (MING <= 0 && MAXG >= 1) {
+    if (g == 0) return f(Int<0>{});
+  }
+  if constexpr (MING <= 1 && MAXG >= 2) {
+    if (g == 1) return f(Int<1>{});
+  }
+  if constexpr (MING <= 2 && MAXG >= 3) {
+    if (g == 2) return f(Int<2>{});
+  }
+  if constexpr (FALLBACK) {
+    if (g == MAXG) return f(Int<MAXG>{});
+    return f(Int<-1>{});
+  } else {
+    return f(Int<MAXG>{});
+  }
+}
+
+// GEN: coordinates and subfield levels (kSubLevel).
+template <int K, bool INVERSE, bool INDEX0, int GEN = -1>
 __device__ __forceinline__ void cq_levels(const DevTables& T, const uint32_t* VP, uint32_t index, uint32_t g,
                                           uint32_t (&L)[16], uint32_t (&H)[16], uint32_t rows = ~0u) {
   if constexpr (kExp & 1) return;
@@ -619,27 +742,34 @@ __device__ __forceinline__ void cq_levels(const DevTables& T, const uint32_t* VP
     const bool live = !INDEX0 || r.t != 0 || g != 0;  // c == 0: the skew sentinel, no product
     constexpr uint32_t span = ((1u << (2 * d)) - 1u) << (r.t * 2 * d);  // the group's rows
     if ((rows & span) == 0) return;
+    auto body = [&](auto sub_c) __attribute__((always_inline)) {
+      constexpr bool SUB = decltype(sub_c)::value;
 #pragma unroll
-    for (int u = 0; u < d; ++u) {
-      const int x = r.t * 2 * d + u, y = x + d;
-      if (INVERSE) {
-        L[y] ^= L[x];
-        H[y] ^= H[x];
-        if (live) qmul(L[x], H[x], L[y], H[y], p);
-      } else {
-        if (live) qmul(L[x], H[x], L[y], H[y], p);
-        L[y] ^= L[x];
-        H[y] ^= H[x];
+      for (int u = 0; u < d; ++u) {
+        const int x = r.t * 2 * d + u, y = x + d;
+        if (INVERSE) {
+          L[y] ^= L[x];
+          H[y] ^= H[x];
+          if (live) qmul_mode<SUB>(L[x], H[x], L[y], H[y], p);
+        } else {
+          if (live) qmul_mode<SUB>(L[x], H[x], L[y], H[y], p);
+          L[y] ^= L[x];
+          H[y] ^= H[x];
+        }
       }
-    }
+    };
+    body(std::integral_constant<bool, kSubLevel<GEN>(r.b)>{});
   };
-  pipelined_staged<15>(T, cval, vaddr, group);
+  auto subf = [&](auto fc) __attribute__((always_inline)) {
+    return std::integral_constant<bool, kSubLevel<GEN>(cq_group<INVERSE>(decltype(fc)::value).b)>{};
+  };
+  pipelined_staged<15, (GEN >= 0)>(T, cval, vaddr, subf, group);
 }
 
 // Levels 4..logK-1 in the high layout: quad j pairs with j + 2^(b-2-logR);
 // group t = j >> (b-1-logR).  FIRST > 0 starts at flat group FIRST (the
 // forward transform's top level, one group, done by the caller: fwd_top).
-template <int K, bool INVERSE, bool INDEX0, int FIRST = 0>
+template <int K, bool INVERSE, bool INDEX0, int FIRST = 0, int GEN = -1>
 __device__ __forceinline__ void hi_levels(const DevTables& T, const uint32_t* VP, uint32_t index, uint32_t (&L)[16],
                                           uint32_t (&H)[16]) {
   if constexpr (kExp & 1) return;
@@ -656,21 +786,28 @@ __device__ __forceinline__ void hi_levels(const DevTables& T, const uint32_t* VP
     constexpr GroupRef r = hi_group<K, INVERSE>(decltype(fc)::value + FIRST);
     constexpr int dj = 1 << (r.b - 2 - logR);
     constexpr bool live = !INDEX0 || r.t != 0;
+    auto body = [&](auto sub_c) __attribute__((always_inline)) {
+      constexpr bool SUB = decltype(sub_c)::value;
 #pragma unroll
-    for (int u = 0; u < dj; ++u) {
-      const int x = r.t * 2 * dj + u, y = x + dj;
-      if (INVERSE) {
-        L[y] ^= L[x];
-        H[y] ^= H[x];
-        if (live) qmul(L[x], H[x], L[y], H[y], p);
-      } else {
-        if (live) qmul(L[x], H[x], L[y], H[y], p);
-        L[y] ^= L[x];
-        H[y] ^= H[x];
+      for (int u = 0; u < dj; ++u) {
+        const int x = r.t * 2 * dj + u, y = x + dj;
+        if (INVERSE) {
+          L[y] ^= L[x];
+          H[y] ^= H[x];
+          if (live) qmul_mode<SUB>(L[x], H[x], L[y], H[y], p);
+        } else {
+          if (live) qmul_mode<SUB>(L[x], H[x], L[y], H[y], p);
+          L[y] ^= L[x];
+          H[y] ^= H[x];
+        }
       }
-    }
+    };
+    body(std::integral_constant<bool, kSubLevel<GEN>(r.b)>{});
   };
-  pipelined_staged<hi_groups<K>() - FIRST>(T, cval, vaddr, group);
+  auto subf = [&](auto fc) __attribute__((always_inline)) {
+    return std::integral_constant<bool, kSubLevel<GEN>(hi_group<K, INVERSE>(decltype(fc)::value + FIRST).b)>{};
+  };
+  pipelined_staged<hi_groups<K>() - FIRST, (GEN >= 0)>(T, cval, vaddr, subf, group);
 }
 
 // Top level (b = logK - 1, one group, quads j and j + 8) of the forward
@@ -680,7 +817,7 @@ __device__ __forceinline__ void hi_levels(const DevTables& T, const uint32_t* VP
 // (the inputs X = M are the same for every shift).  MODE 0: multiply; 1:
 // multiply and keep the products in P; 2: multiply and XOR them into P; 3:
 // take the products from P (no multiply).
-template <int K, int MODE>
+template <int K, int MODE, int GEN = -1>
 __device__ __forceinline__ void fwd_top(const DevTables& T, const uint32_t* VP, uint32_t index, uint32_t (&L)[16],
                                         uint32_t (&H)[16], uint32_t (&PL)[8], uint32_t (&PH)[8]) {
   if constexpr (kExp & 1) return;
@@ -689,16 +826,20 @@ __device__ __forceinline__ void fwd_top(const DevTables& T, const uint32_t* VP, 
   Mult m;
   if constexpr (MODE != 3) {
     uint32_t sp[12];
-    spool_of(T, index >> b, sp);
-    m = staged_mult(sp, VP + 8u * vslot<K>(b, 0));
+    spool_of<(GEN >= 0), kSubLevel<GEN>(b)>(T, index >> b, sp);
+    m = staged_mult<kSubLevel<GEN>(b)>(sp, VP + 8u * vslot<K>(b, 0));
   }
+  constexpr bool sub = kSubLevel<GEN>(b);
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     uint32_t pl, ph;
     if constexpr (MODE == 3) {
       pl = PL[u], ph = PH[u];
     } else {
-      qmul_set(pl, ph, L[u + 8], H[u + 8], m);
+      if constexpr (sub)
+        qmul_sub_set(pl, ph, L[u + 8], H[u + 8], m);
+      else
+        qmul_set(pl, ph, L[u + 8], H[u + 8], m);
       if constexpr (MODE == 1) PL[u] = pl, PH[u] = ph;
       if constexpr (MODE == 2) PL[u] ^= pl, PH[u] ^= ph;
     }
@@ -730,6 +871,33 @@ __device__ __forceinline__ void add_derivative(uint32_t (&A)[16], uint32_t (&X)[
     A[j] ^= v;
     asm volatile("" : "+v"(A[j]));  // finish position j here (bounded temporaries)
     X[j] = 0;                       // dead from here on
+  }
+}
+
+// Cantor <-> tower coordinates of 16 quads (an involution, field_tables.hpp
+// HostTables::tower_a): the low plane takes A(high plane), 3 byte lookups of
+// the high plane through the b slots of tower_pools[kFieldSize].
+__device__ __forceinline__ void tower_convert(const DevTables& T, uint32_t (&L)[16], const uint32_t (&H)[16]) {
+#ifdef NP_NO_CONVERT
+  return;
+#endif
+  const cpool_t q = (cpool_t)(T.tower_pools) + 65536u * kPoolWords;
+  const uint32_t sa = q[8 + 3], sb = q[8 + 4], sc = q[8 + 5];
+  uint64_t vv;
+  asm volatile("v_mov_b64 %0, %1" : "=v"(vv) : "s"((static_cast<uint64_t>(q[3]) << 32) | q[2]));
+  const uint32_t va = static_cast<uint32_t>(vv), vb = static_cast<uint32_t>(vv >> 32);
+#pragma unroll
+  for (int p = 0; p < 16; ++p) {
+    uint32_t s0, s1, s2;  // one asm block: no quad's selectors are computed far ahead of its lookups
+    asm volatile(
+        "v_and_b32 %0, 0x07070707, %3\n\t"
+        "v_lshrrev_b32 %1, 3, %3\n\t"
+        "v_lshrrev_b32 %2, 6, %3\n\t"
+        "v_and_b32 %1, 0x07070707, %1\n\t"
+        "v_and_b32 %2, 0x03030303, %2"
+        : "=&v"(s0), "=&v"(s1), "=&v"(s2)
+        : "v"(H[p]));
+    qplane_sub(L[p], s0, s1, s2, va, vb, sa, sb, sc);
   }
 }
 

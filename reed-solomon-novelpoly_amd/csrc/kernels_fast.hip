@@ -42,6 +42,64 @@ namespace np {
 namespace {
 
 // ----------------------------------------------------------------- encode ----
+// Encode shifts run in tower coordinates while gen_of(index) <= kEncMaxGen
+// (index < 2048: n <= 8K at k = 256, every n the crate derives), their levels
+// below gen_of(index) with the full map; farther shifts of larger explicit
+// codes run in Cantor coordinates.
+constexpr int kEncMaxGen = 3;
+__device__ __forceinline__ bool enc_tower(uint32_t index) {
+  return __builtin_amdgcn_readfirstlane(gen_of(index)) <= static_cast<uint32_t>(kEncMaxGen);
+}
+
+// Shifts 1..3 are compile-time (SH): tower coordinates, the top-level products
+// shared between them (fwd_top), their cq levels below gen_of(SH * K) with the
+// full map.  SH = 23: shift 2 or 3 (runtime sh; both have gen_of = 2 at
+// K = 256).  SH = 0: a shift >= 4 (n > 4K) in Cantor coordinates.  A runtime
+// choice between instances inside a pass makes the register allocator spill,
+// so each call site is one instance.
+template <int K, int SH>
+constexpr int kShiftGen = static_cast<int>(gen_of((SH == 23 ? 2 : SH) * K));
+
+// X = M, then the forward high levels of shift sh (top level included).
+template <int K, int SH>
+__device__ __forceinline__ void shift_hi(const DevTables& T, const uint32_t* vp, uint32_t index,
+                                         const uint32_t (&ML)[16], const uint32_t (&MH)[16], uint32_t (&XL)[16],
+                                         uint32_t (&XH)[16], uint32_t (&PL)[8], uint32_t (&PH)[8]) {
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    XL[q] = ML[q];
+    XH[q] = MH[q];
+  }
+  if constexpr (SH == 0) {
+    tower_convert(T, XL, XH);  // M is in tower coordinates
+    fwd_top<K, 0, -1>(T, vp, index, XL, XH, PL, PH);
+    hi_levels<K, false, false, 1, -1>(T, vp, index, XL, XH);
+  } else {
+    if constexpr (SH == 23) {
+      if (index == 2 * K)
+        fwd_top<K, 2, 0>(T, vp, index, XL, XH, PL, PH);
+      else
+        fwd_top<K, 3, 0>(T, vp, index, XL, XH, PL, PH);
+    } else {
+      fwd_top<K, SH, 0>(T, vp, index, XL, XH, PL, PH);
+    }
+    hi_levels<K, false, false, 1, 0>(T, vp, index, XL, XH);  // hi levels: gen_of(index) <= 4
+  }
+}
+
+// The forward cq levels of shift sh, ending in Cantor coordinates.
+template <int K, int SH>
+__device__ __forceinline__ void shift_cq(const DevTables& T, const uint32_t* vp, uint32_t index, uint32_t g,
+                                         uint32_t (&XL)[16], uint32_t (&XH)[16]) {
+  if constexpr (SH == 0) {
+    cq_levels<K, false, false, -1>(T, vp, index, g, XL, XH);
+  } else {
+    static_assert(SH != 23 || kShiftGen<K, 2> == kShiftGen<K, 3>, "shifts 2 and 3 share one instance");
+    cq_levels<K, false, false, kShiftGen<K, SH>>(T, vp, index, g, XL, XH);
+    tower_convert(T, XL, XH);  // back to Cantor coordinates for the shard rows
+  }
+}
+
 // One workgroup: 256 chunks of one payload.  mod.rs:144-154 / inc_encode.rs:15-48.
 template <int K>
 __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_fast(DevTables T, EncodeArgs a, uint32_t nchunks, uint32_t tiles) {
@@ -93,10 +151,10 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
   const bool resident = nshift <= 4;
   if (resident) {
     for (uint32_t sh = 0; sh < nshift && sh * K < a.wanted_n; ++sh)
-      stage_vpools<K, G::kThreads>(T, sh * K, VP + sh * G::kVPWords);
+      stage_vpools<K, G::kThreads>(T, sh * K, VP + sh * G::kVPWords, true);
   } else {
-    stage_vpools<K, G::kThreads>(T, 0, VP);                              // inverse transform, index 0
-    if (nshift > 1) stage_vpools<K, G::kThreads>(T, K, VP + G::kVPWords);  // first shift
+    stage_vpools<K, G::kThreads>(T, 0, VP, true);                                   // inverse transform, index 0
+    if (nshift > 1) stage_vpools<K, G::kThreads>(T, K, VP + G::kVPWords, true);  // first shift
   }
   __syncthreads();
 
@@ -106,7 +164,8 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     uint32_t CL[16], CH[16];
     cq_read<K>(tile, cqb, CL, CH);
     store_rows(out, a.shard_len, 16 * g, wanted_store, CL, CH, lane, ncols, full);
-    cq_levels<K, true, true>(T, VP, 0, g, CL, CH);
+    tower_convert(T, CL, CH);  // transforms run in tower coordinates
+    cq_levels<K, true, true, 0>(T, VP, 0, g, CL, CH);
     cq_write_p<K>(tile, cqb, CL, CH);
   }
   __syncthreads();
@@ -114,40 +173,31 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
   const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
   uint32_t ML[16], MH[16];
   hi_read_p<K>(tile, hb, ML, MH);
-  hi_levels<K, true, true>(T, VP, 0, ML, MH);
+  hi_levels<K, true, true, 0, 0>(T, VP, 0, ML, MH);
 #pragma unroll
   for (int q = 0; q < 16; ++q) asm volatile("" : "+v"(ML[q]), "+v"(MH[q]));  // materialise M once
 
   uint32_t PL[8], PH[8];  // top-level products of shift 1, then of shifts 1 ^ 2 (fwd_top)
-  for (uint32_t sh = 1; sh < nshift; ++sh) {
+  auto shift = [&](auto shc, uint32_t sh) __attribute__((always_inline)) {
+    constexpr int SH = decltype(shc)::value;
     const uint32_t index = sh * K;
-    if (index >= a.wanted_n) break;
     uint32_t XL[16], XH[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      XL[q] = ML[q];
-      XH[q] = MH[q];
-    }
     const uint32_t* vp = VP + (resident ? sh : (sh & 1u)) * G::kVPWords;
-    if (sh == 1) {
-      fwd_top<K, 1>(T, vp, index, XL, XH, PL, PH);
-    } else if (sh == 2) {
-      fwd_top<K, 2>(T, vp, index, XL, XH, PL, PH);
-    } else if (sh == 3) {
-      fwd_top<K, 3>(T, vp, index, XL, XH, PL, PH);
-    } else {
-      fwd_top<K, 0>(T, vp, index, XL, XH, PL, PH);
-    }
-    hi_levels<K, false, false, 1>(T, vp, index, XL, XH);
+    shift_hi<K, SH>(T, vp, index, ML, MH, XL, XH, PL, PH);
     __syncthreads();  // the previous cq pass is done with the tile and with the other table buffer
     if (!resident && sh + 1 < nshift && (sh + 1) * K < a.wanted_n)
-      stage_vpools<K, G::kThreads>(T, (sh + 1) * K, VP + ((sh + 1) & 1u) * G::kVPWords);
+      stage_vpools<K, G::kThreads>(T, (sh + 1) * K, VP + ((sh + 1) & 1u) * G::kVPWords, sh + 1 < 4);
     hi_write_p<K>(tile, fresh_v(hb), XL, XH);
     __syncthreads();
     cq_read_p<K>(tile, fresh_v(cqb), XL, XH);
-    cq_levels<K, false, false>(T, vp, index, g, XL, XH);
+    shift_cq<K, SH>(T, vp, index, g, XL, XH);
     store_rows(out, a.shard_len, index + 16 * g, wanted_store, XL, XH, lane, ncols, full);
-  }
+  };
+  if (nshift > 1 && K < a.wanted_n) shift(Int<1>{}, 1);
+  if (nshift > 2 && 2 * K < a.wanted_n) shift(Int<2>{}, 2);
+  if (nshift > 3 && 3 * K < a.wanted_n) shift(Int<3>{}, 3);
+#pragma unroll 1
+  for (uint32_t sh = 4; sh < nshift && sh * K < a.wanted_n; ++sh) shift(Int<0>{}, sh);
 }
 
 // ----------------------------------------------------- multi-tile encode ----
@@ -203,33 +253,20 @@ __device__ __forceinline__ void dma_tile(const uint8_t* pay, uint32_t ch0, uint8
   }
 }
 
-// One shift of the encode (rows sK .. sK+K-1).  With `dma_pay`, the last cq
-// pass starts the next tile's payload DMA once every wave has read the tile.
-template <int K>
+// One shift of the encode (rows sK .. sK+K-1), SH = 1..3.  With `dma_pay`,
+// the last cq pass starts the next tile's payload DMA once every wave has read
+// the tile.
+template <int K, int SH>
 __device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArgs& a, uint8_t* tile, uint32_t* VP,
-                                             uint8_t* out, uint32_t sh, uint32_t nshift, uint32_t g, uint32_t lane,
-                                             uint32_t ncols, bool full, uint32_t cqb, uint32_t hb,
-                                             const uint32_t (&ML)[16], const uint32_t (&MH)[16], uint32_t (&PL)[8],
-                                             uint32_t (&PH)[8], const uint8_t* dma_pay, uint32_t dma_ch0) {
+                                             uint8_t* out, uint32_t sh, uint32_t g, uint32_t lane, uint32_t ncols,
+                                             bool full, uint32_t cqb, uint32_t hb, const uint32_t (&ML)[16],
+                                             const uint32_t (&MH)[16], uint32_t (&PL)[8], uint32_t (&PH)[8],
+                                             const uint8_t* dma_pay, uint32_t dma_ch0) {
   using G = Geo<K>;
   const uint32_t index = sh * K;
   uint32_t XL[16], XH[16];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    XL[q] = ML[q];
-    XH[q] = MH[q];
-  }
   const uint32_t* vp = VP + sh * G::kVPWords;  // the tables of every shift stay staged (kEncBuffers)
-  if (sh == 1) {
-    fwd_top<K, 1>(T, vp, index, XL, XH, PL, PH);
-  } else if (sh == 2) {
-    fwd_top<K, 2>(T, vp, index, XL, XH, PL, PH);
-  } else if (sh == 3) {
-    fwd_top<K, 3>(T, vp, index, XL, XH, PL, PH);
-  } else {
-    fwd_top<K, 0>(T, vp, index, XL, XH, PL, PH);
-  }
-  hi_levels<K, false, false, 1>(T, vp, index, XL, XH);
+  shift_hi<K, SH>(T, vp, index, ML, MH, XL, XH, PL, PH);
   __syncthreads();  // the previous cq pass is done with the tile
   hi_write_p<K>(tile, fresh_v(hb), XL, XH);
   __syncthreads();
@@ -238,7 +275,7 @@ __device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArg
     __syncthreads();  // every wave has its cq registers: the tile is free
     if constexpr (!(kExp & 4)) dma_tile<K>(dma_pay, dma_ch0, tile, g, lane);
   }
-  cq_levels<K, false, false>(T, vp, index, g, XL, XH);
+  shift_cq<K, SH>(T, vp, index, g, XL, XH);
   store_rows(out, a.shard_len, index + 16 * g, (kExp & 2) ? 0u : a.wanted_n, XL, XH, lane, ncols, full);
 }
 
@@ -294,7 +331,7 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
   const uint32_t nshift = a.n / K;
   const uint32_t last = min(nshift, (a.wanted_n + K - 1) / K) - 1;  // last shift with wanted rows
   if (first) {  // tables of the inverse transform (index 0) and of every shift, kept for all tiles
-    for (uint32_t sh = 0; sh <= last; ++sh) stage_vpools<K, G::kThreads>(T, sh * K, VP + sh * G::kVPWords);
+    for (uint32_t sh = 0; sh <= last; ++sh) stage_vpools<K, G::kThreads>(T, sh * K, VP + sh * G::kVPWords, true);
   }
   __syncthreads();
 
@@ -303,24 +340,29 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
     uint32_t CL[16], CH[16];
     cq_read<K>(tile, cqb, CL, CH);
     store_rows(out, a.shard_len, 16 * g, (kExp & 2) ? 0u : a.wanted_n, CL, CH, lane, ncols, full);
-    cq_levels<K, true, true>(T, VP, 0, g, CL, CH);
+    tower_convert(T, CL, CH);  // transforms run in tower coordinates
+    cq_levels<K, true, true, 0>(T, VP, 0, g, CL, CH);
     cq_write_p<K>(tile, cqb, CL, CH);
   }
   __syncthreads();
   const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
   uint32_t ML[16], MH[16];
   hi_read_p<K>(tile, hb, ML, MH);
-  hi_levels<K, true, true>(T, VP, 0, ML, MH);
+  hi_levels<K, true, true, 0, 0>(T, VP, 0, ML, MH);
 #pragma unroll
   for (int q = 0; q < 16; ++q) asm volatile("" : "+v"(ML[q]), "+v"(MH[q]));  // materialise M once
   uint32_t PL[8], PH[8];
-#pragma unroll 1
-  for (uint32_t sh = 1; sh < last; ++sh)
-    encode_shift<K>(T, a, tile, VP, out, sh, nshift, g, lane, ncols, full, cqb, hb, ML, MH, PL, PH, nullptr, 0);
   const bool dma = last >= 1 && next_tl != ~0u && tile_fast(next_tl);
+  const uint8_t* dpay = dma ? pay : nullptr;
+  const uint32_t dch0 = next_tl * kTile;
   if (last >= 1)
-    encode_shift<K>(T, a, tile, VP, out, last, nshift, g, lane, ncols, full, cqb, hb, ML, MH, PL, PH,
-                    dma ? pay : nullptr, next_tl * kTile);
+    encode_shift<K, 1>(T, a, tile, VP, out, 1, g, lane, ncols, full, cqb, hb, ML, MH, PL, PH,
+                       last == 1 ? dpay : nullptr, dch0);
+  if (last >= 2)
+    encode_shift<K, 2>(T, a, tile, VP, out, 2, g, lane, ncols, full, cqb, hb, ML, MH, PL, PH,
+                       last == 2 ? dpay : nullptr, dch0);
+  if (last >= 3)
+    encode_shift<K, 3>(T, a, tile, VP, out, 3, g, lane, ncols, full, cqb, hb, ML, MH, PL, PH, dpay, dch0);
   return dma;
 }
 
@@ -433,6 +475,10 @@ __device__ __forceinline__ void copy_out_cq(uint8_t* out_tile, uint32_t lane, ui
 template <int NQ>
 constexpr bool kRowPrefetch = NQ <= 2;
 
+// Largest gen_of over the decode's segment transforms (index qK, q < NQ).
+template <int K, int NQ>
+constexpr int kRecMaxGen = static_cast<int>(gen_of(static_cast<uint32_t>((NQ - 1) * K)));
+
 // The segment sweep: x_q = IFFT(K, qK)(premultiplied segment q), folded into
 // A.  With kRowPrefetch `raw` holds segment seg_of(0)'s rows on entry and the
 // systematic rows (for the merge) on exit.  A runtime loop keeps
@@ -483,13 +529,16 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
         });
     const uint32_t* vp = c.VP + (step & 1) * Geo<K>::kVPWords;
     stamp(c.dbg, 3 + 6 * step);
-    cq_levels<K, true, false>(T, vp, index, g, XL, XH, m);  // absent rows are zero
+    // absent rows are zero; segment q's transform has gen_of(qK) <= kRecMaxGen
+    with_gen<0, kRecMaxGen<K, NQ>, false>(index, [&](auto gc) __attribute__((always_inline)) {
+      cq_levels<K, true, false, decltype(gc)::value>(T, vp, index, g, XL, XH, m);
+    });
     stamp(c.dbg, 4 + 6 * step);
     if (step > 0 || after_tile) {
       __syncthreads();  // the previous high pass (or tile's copy-out) is done with the tile and the other table buffer
       if (step + 1 < NQ) {
         const int qn = seg_of<NQ>(step + 1);
-        stage_vpools<K, Geo<K>::kThreads>(T, static_cast<uint32_t>(qn) * K, c.VP + ((step + 1) & 1) * Geo<K>::kVPWords);
+        stage_vpools<K, Geo<K>::kThreads>(T, static_cast<uint32_t>(qn) * K, c.VP + ((step + 1) & 1) * Geo<K>::kVPWords, true);
       }
     }
     cq_write_p<K>(c.tile, cqb, XL, XH);
@@ -512,7 +561,7 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
     __syncthreads();
     stamp(c.dbg, 5 + 6 * step);
     hi_read_p<K>(c.tile, hb, XL, XH);
-    hi_levels<K, true, false>(T, vp, index, XL, XH);
+    hi_levels<K, true, false, 0, 0>(T, vp, index, XL, XH);  // hi levels: gen_of(index) <= 4
     stamp(c.dbg, 6 + 6 * step);
     __builtin_amdgcn_sched_barrier(0);
     if (step == 0) {
@@ -533,13 +582,13 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
       add_derivative<K>(AH, XH, c.tid % Geo<K>::R);
     } else if (NQ == 4 && q == 3) {
       uint32_t beta[20];
-      pool_of(T, 2u, beta);  // beta = Cantor(2), the t = 1 skew of level logK at index 0
+      pool_of<true>(T, 2u, beta);  // beta = Cantor(2) in GF(2^8), the t = 1 skew of level logK at index 0
       const Mult pool = make_mult(beta);
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         XL[j] ^= AL[j];
         XH[j] ^= AH[j];
-        qmul(AL[j], AH[j], XL[j], XH[j], pool);
+        qmul_sub(AL[j], AH[j], XL[j], XH[j], pool);
       }
     } else {
 #pragma unroll
@@ -577,8 +626,8 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
   uint32_t XL[16], XH[16];
   if constexpr (NQ > 1) {
     // multiplier tables of the first two segment transforms (indices 2K, 3K or K, 0)
-    stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(0)) * K, VP);
-    stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(1)) * K, VP + G::kVPWords);
+    stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(0)) * K, VP, true);
+    stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(1)) * K, VP + G::kVPWords, true);
     __syncthreads();
     stamp(dbg, 1);
 
@@ -589,14 +638,14 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
     // ---- forward transform of size K at index 0
     const uint32_t* vp0 = VP + ((NQ - 1) & 1) * G::kVPWords;  // segment 0's tables = FFT(K, 0)'s
     stamp(dbg, 26);
-    hi_levels<K, false, true>(T, vp0, 0, AL, AH);
+    hi_levels<K, false, true, 0, 0>(T, vp0, 0, AL, AH);
     stamp(dbg, 27);
     __syncthreads();
     hi_write<K>(tile, fresh_v(hb), AL, AH);
     __syncthreads();
     stamp(dbg, 28);
     cq_read<K>(tile, fresh_v(cqb), XL, XH);
-    cq_levels<K, false, true>(T, vp0, 0, g, XL, XH, ~uniform(msk[NQ - 1]));  // erased rows only
+    cq_levels<K, false, true, 0>(T, vp0, 0, g, XL, XH, ~uniform(msk[NQ - 1]));  // erased rows only
     stamp(dbg, 29);
   }
   // ---- merge: received systematic rows, postmultiplied recovered ones
@@ -717,8 +766,8 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
   if constexpr (NQ > 1) {
     // multiplier tables of the first two segment transforms (indices 2K, 3K or
     // K, 0): for NQ = 2 these are all the tables, kept for every tile
-    stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(0)) * K, VP);
-    stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(1)) * K, VP + G::kVPWords);
+    stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(0)) * K, VP, true);
+    stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(1)) * K, VP + G::kVPWords, true);
     __syncthreads();
   }
 
@@ -744,8 +793,8 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
     if constexpr (NQ == 4) {
       if (t > 0) {  // segment 2's tables were replaced during the previous tile
         __syncthreads();
-        stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(0)) * K, VP);
-        stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(1)) * K, VP + G::kVPWords);
+        stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(0)) * K, VP, true);
+        stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(1)) * K, VP + G::kVPWords, true);
         __syncthreads();
       }
     }
@@ -759,14 +808,14 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
       // ---- forward transform of size K at index 0
       const uint32_t* vp0 = VP + ((NQ - 1) & 1) * G::kVPWords;  // segment 0's tables = FFT(K, 0)'s
       stamp(dbg, 26);
-      hi_levels<K, false, true>(T, vp0, 0, AL, AH);
+      hi_levels<K, false, true, 0, 0>(T, vp0, 0, AL, AH);
       stamp(dbg, 27);
       __syncthreads();
       hi_write<K>(tile, fresh_v(hb), AL, AH);
       __syncthreads();
       stamp(dbg, 28);
       cq_read<K>(tile, fresh_v(cqb), XL, XH);
-      cq_levels<K, false, true>(T, vp0, 0, g, XL, XH, ~uniform(msk[NQ - 1]));  // erased rows only
+      cq_levels<K, false, true, 0>(T, vp0, 0, g, XL, XH, ~uniform(msk[NQ - 1]));  // erased rows only
       stamp(dbg, 29);
     }
     // ---- merge: received systematic rows, postmultiplied recovered ones
@@ -895,9 +944,13 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
 // ---------------------------------------------------------- prefix locator ----
 // The v_perm tables of row multipliers E[0..rows) into the record (thread
 // tid copies the rows it wrote E for: no barrier).
-__device__ __forceinline__ void write_row_pools(const DevTables& T, const uint16_t* E, uint32_t rows, uint8_t* dst) {
+// Present rows get the premultiply's tables (Cantor in, tower out: in_pools),
+// erased rows the postmultiply's (tower in, Cantor out: out_pools).
+__device__ __forceinline__ void write_row_pools(const DevTables& T, const uint16_t* E, const uint8_t* PR,
+                                                uint32_t rows, uint8_t* dst) {
   for (uint32_t v = threadIdx.x; v < rows; v += 256) {
-    const uint4* src = reinterpret_cast<const uint4*>(T.perm_pools + static_cast<size_t>(E[v]) * kPoolWords);
+    const uint32_t* pools = PR[v] ? T.in_pools : T.out_pools;
+    const uint4* src = reinterpret_cast<const uint4*>(pools + static_cast<size_t>(E[v]) * kPoolWords);
     uint4* d = reinterpret_cast<uint4*>(dst + static_cast<size_t>(v) * 4 * kPoolWords);
     const uint4 a0 = src[0], a1 = src[1], a2 = src[2], a3 = src[3], a4 = src[4];
     d[0] = a0, d[1] = a1, d[2] = a2, d[3] = a3, d[4] = a4;
@@ -959,7 +1012,7 @@ __global__ __launch_bounds__(256) void k_prefix_locator(DevTables T, Reconstruct
   } else {
     fused_locator<N, 256>(T, pres, W, E, PR);
   }
-  write_row_pools(T, E, static_cast<uint32_t>(nq) * K, rec + prefix_pools_offset(N));
+  write_row_pools(T, E, PR, static_cast<uint32_t>(nq) * K, rec + prefix_pools_offset(N));
 }
 
 // The record for caller locators (log form, all n rows: the full decode,
@@ -979,7 +1032,7 @@ __global__ __launch_bounds__(256) void k_locator_records(DevTables T, Reconstruc
   if (!ok) return;
   // mul(x, log m) == x * EXP[m] (inc_log_mul.rs:42-49)
   for (uint32_t v = tid; v < static_cast<uint32_t>(N); v += 256) E[v] = T.exp[loc[v]];
-  write_row_pools(T, E, N, rec + prefix_pools_offset(N));
+  write_row_pools(T, E, a.present + static_cast<size_t>(pb) * N, N, rec + prefix_pools_offset(N));
 }
 
 // ------------------------------------------------------------- launchers ----
