@@ -135,6 +135,32 @@ def launch_replicas(args) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+def dry_run(args):
+    """NP_BENCH_DRYRUN=1 (CPU tests): the launch and partition logic without a
+    GPU -- each rank joins a gloo group, takes its payload range and rank 0
+    prints the ranges of every rank with n_gpus."""
+    import torch
+    import torch.distributed as dist
+
+    from novelpoly_amd import synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    batch = args.batch or (synth.CONFIGS[args.config]["batch"] if args.config != 5 else
+                           synth.CONFIGS[5]["batch"] // 8)
+    lo, hi = partition(batch, world, rank)
+    ranges = [(lo, hi)]
+    if world > 1:
+        dist.init_process_group("gloo")
+        t = torch.tensor([lo, hi], dtype=torch.int64)
+        out = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(out, t)
+        ranges = [tuple(int(v) for v in o) for o in out]
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranges": ranges, "batch_per_gpu": batch}), flush=True)
+
+
 def main():
     args = parse()
     world_env = os.environ.get("WORLD_SIZE")
@@ -142,6 +168,8 @@ def main():
         sys.exit(launch_replicas(args))
     if world_env is not None and int(world_env) != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}; launch one rank per GPU")
+    if os.environ.get("NP_BENCH_DRYRUN"):
+        return dry_run(args)
     import torch
     import torch.distributed as dist
 

@@ -187,6 +187,35 @@ int np_reconstruct_batch_host(np_ctx* ctx, const np_code_params* params, const u
                               size_t batch_stride, const uint8_t* present, size_t batch, uint8_t* out,
                               size_t out_stride);
 
+/* ---- multi-GPU: one batch over several devices ------------------------------
+ * payloads are independent, so `batch` splits into contiguous
+ * ranges, one per context (np_batch_split: the first batch % nctx ranges hold
+ * one payload more), with no exchange between devices and no collective.  One
+ * host thread per context drives its range on that context's stream; every
+ * call returns when all ranges are done (the first failing status is
+ * returned, its detail in np_last_error_detail).  Replaces the caller-side
+ * loop over payloads (mod.rs:117-239) across GPUs. */
+void np_batch_split(size_t batch, size_t ndev, size_t i, size_t* begin, size_t* count);
+/* Device memory: d_payloads[i] / d_shards[i] / d_present[i] / d_out[i] /
+ * d_status[i] (d_status may be NULL) are device i's buffers holding its range,
+ * laid out as in np_encode_batch_dev / np_reconstruct_batch_dev2 (payload
+ * np_batch_split(...).begin of the batch at index 0). */
+int np_encode_batch_multi(np_ctx* const* ctxs, size_t nctx, const np_code_params* params,
+                          const uint8_t* const* d_payloads, size_t payload_len, size_t payload_stride, size_t batch,
+                          uint8_t* const* d_shards, size_t batch_stride);
+int np_reconstruct_batch_multi(np_ctx* const* ctxs, size_t nctx, const np_code_params* params,
+                               const uint8_t* const* d_shards, size_t shard_len, size_t batch_stride,
+                               const uint8_t* const* d_present, size_t batch, uint8_t* const* d_out,
+                               size_t out_stride, np_payload_status* const* d_status);
+/* Host memory: one whole batch as in np_encode_batch_host / np_reconstruct_batch_host,
+ * each device copying and computing its range. */
+int np_encode_batch_host_multi(np_ctx* const* ctxs, size_t nctx, const np_code_params* params,
+                               const uint8_t* payloads, size_t payload_len, size_t payload_stride, size_t batch,
+                               uint8_t* shards, size_t batch_stride);
+int np_reconstruct_batch_host_multi(np_ctx* const* ctxs, size_t nctx, const np_code_params* params,
+                                    const uint8_t* shards, size_t shard_len, size_t batch_stride,
+                                    const uint8_t* present, size_t batch, uint8_t* out, size_t out_stride);
+
 /* ---- low-level parity hooks (device pointers, `cols` independent columns) ----
  * data layout: column c, position i at d_data[c*size + i] (uint16, plain values). */
 /* inc_afft.rs:267-332 afft */

@@ -6,11 +6,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/novelpoly.h"
@@ -826,6 +828,97 @@ int np_reconstruct_from_systematic_batch_dev(np_ctx* c, const np_code_params* p,
   (void)hipSetDevice(c->device);
   return dev_err(np::launch_systematic(d_shards, shard_len, bstride, static_cast<uint32_t>(p->k), batch, d_out,
                                        out_stride, pick(c, stream)));
+}
+
+// ------------------------------------------------------------ multi-GPU ----
+// payloads are independent, so a batch splits into contiguous
+// ranges, one per device (context), with no exchange between devices; one
+// host thread per context drives its range on that context's stream (the
+// host-memory calls block in their pipeline, so the threads overlap them).
+void np_batch_split(size_t batch, size_t ndev, size_t i, size_t* begin, size_t* count) {
+  if (!begin || !count) return;
+  if (ndev == 0 || i >= ndev) {
+    *begin = batch;
+    *count = 0;
+    return;
+  }
+  const size_t base = batch / ndev, extra = batch % ndev;  // the first `extra` ranges hold one more
+  *begin = i * base + std::min(i, extra);
+  *count = base + (i < extra ? 1 : 0);
+}
+
+}  // extern "C"
+
+namespace {
+
+// Runs fn(i, begin, count) for every context on its own thread; returns the
+// first failing status with its error detail on the calling thread.
+template <class F>
+int run_multi(np_ctx* const* ctxs, size_t nctx, size_t batch, F fn) {
+  if (!ctxs || nctx == 0) return fail(NP_ERR_INVALID_ARGUMENT);
+  for (size_t i = 0; i < nctx; ++i)
+    if (!ctxs[i]) return fail(NP_ERR_INVALID_ARGUMENT);
+  std::vector<int> st(nctx, NP_OK);
+  std::vector<std::array<size_t, 3>> det(nctx);
+  std::vector<std::thread> th;
+  th.reserve(nctx);
+  for (size_t i = 0; i < nctx; ++i) {
+    size_t b0 = 0, cnt = 0;
+    np_batch_split(batch, nctx, i, &b0, &cnt);
+    th.emplace_back([&, i, b0, cnt] {
+      st[i] = cnt ? fn(i, b0, cnt) : NP_OK;
+      np_last_error_detail(det[i].data());
+    });
+  }
+  for (auto& t : th) t.join();
+  for (size_t i = 0; i < nctx; ++i)
+    if (st[i] != NP_OK) return fail(st[i], det[i][0], det[i][1], det[i][2]);
+  return NP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int np_encode_batch_multi(np_ctx* const* ctxs, size_t nctx, const np_code_params* p,
+                          const uint8_t* const* d_payloads, size_t len, size_t pstride, size_t batch,
+                          uint8_t* const* d_shards, size_t bstride) {
+  if (!d_payloads || !d_shards) return fail(NP_ERR_INVALID_ARGUMENT);
+  return run_multi(ctxs, nctx, batch, [&](size_t i, size_t, size_t cnt) {
+    int st = np_encode_batch_dev(ctxs[i], p, d_payloads[i], len, pstride, cnt, d_shards[i], bstride, nullptr);
+    return st ? st : np_ctx_synchronize(ctxs[i]);
+  });
+}
+
+int np_reconstruct_batch_multi(np_ctx* const* ctxs, size_t nctx, const np_code_params* p,
+                               const uint8_t* const* d_shards, size_t shard_len, size_t bstride,
+                               const uint8_t* const* d_present, size_t batch, uint8_t* const* d_out,
+                               size_t out_stride, np_payload_status* const* d_status) {
+  if (!d_shards || !d_present || !d_out) return fail(NP_ERR_INVALID_ARGUMENT);
+  return run_multi(ctxs, nctx, batch, [&](size_t i, size_t, size_t cnt) {
+    int st = np_reconstruct_batch_dev2(ctxs[i], p, d_shards[i], shard_len, bstride, d_present[i], nullptr, cnt,
+                                       d_out[i], out_stride, d_status ? d_status[i] : nullptr, nullptr);
+    return st ? st : np_ctx_synchronize(ctxs[i]);
+  });
+}
+
+int np_encode_batch_host_multi(np_ctx* const* ctxs, size_t nctx, const np_code_params* p, const uint8_t* payloads,
+                               size_t len, size_t pstride, size_t batch, uint8_t* shards, size_t bstride) {
+  if (!payloads || !shards) return fail(NP_ERR_INVALID_ARGUMENT);
+  return run_multi(ctxs, nctx, batch, [&](size_t i, size_t b0, size_t cnt) {
+    return np_encode_batch_host(ctxs[i], p, payloads + b0 * pstride, len, pstride, cnt, shards + b0 * bstride,
+                                bstride);
+  });
+}
+
+int np_reconstruct_batch_host_multi(np_ctx* const* ctxs, size_t nctx, const np_code_params* p,
+                                    const uint8_t* shards, size_t shard_len, size_t bstride, const uint8_t* present,
+                                    size_t batch, uint8_t* out, size_t out_stride) {
+  if (!shards || !present || !out || !p) return fail(NP_ERR_INVALID_ARGUMENT);
+  return run_multi(ctxs, nctx, batch, [&](size_t i, size_t b0, size_t cnt) {
+    return np_reconstruct_batch_host(ctxs[i], p, shards + b0 * bstride, shard_len, bstride, present + b0 * p->n,
+                                     cnt, out + b0 * out_stride, out_stride);
+  });
 }
 
 // --------------------------------------------------------- parity hooks ----

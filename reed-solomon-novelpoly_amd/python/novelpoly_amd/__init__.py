@@ -74,6 +74,12 @@ def lib() -> C.CDLL:
             "np_reconstruct_from_systematic_batch_dev": (C.c_int, [vp, P, vp, _sz, _sz, _sz, vp, _sz, vp]),
             "np_encode_batch_host": (C.c_int, [vp, P, vp, _sz, _sz, _sz, vp, _sz]),
             "np_reconstruct_batch_host": (C.c_int, [vp, P, vp, _sz, _sz, vp, _sz, vp, _sz]),
+            "np_batch_split": (None, [_sz, _sz, _sz, C.POINTER(_sz), C.POINTER(_sz)]),
+            "np_encode_batch_multi": (C.c_int, [C.POINTER(vp), _sz, P, C.POINTER(vp), _sz, _sz, _sz, C.POINTER(vp), _sz]),
+            "np_reconstruct_batch_multi": (C.c_int, [C.POINTER(vp), _sz, P, C.POINTER(vp), _sz, _sz, C.POINTER(vp), _sz,
+                                                     C.POINTER(vp), _sz, C.POINTER(vp)]),
+            "np_encode_batch_host_multi": (C.c_int, [C.POINTER(vp), _sz, P, vp, _sz, _sz, _sz, vp, _sz]),
+            "np_reconstruct_batch_host_multi": (C.c_int, [C.POINTER(vp), _sz, P, vp, _sz, _sz, vp, _sz, vp, _sz]),
             "np_afft_dev": (C.c_int, [vp, vp, _sz, _sz, _sz, vp]),
             "np_inverse_afft_dev": (C.c_int, [vp, vp, _sz, _sz, _sz, vp]),
             "np_walsh_dev": (C.c_int, [vp, vp, _sz, vp]),
@@ -482,6 +488,53 @@ def reconstruct_batch_dev(params: CodeParams, d_shards: int, shard_len: int, bat
     pres = bytes(present)
     _raise(lib().np_reconstruct_batch_dev(ctx.handle, C.byref(params._c()), d_shards, shard_len, batch_stride,
                                           pres, batch, d_out, out_stride, stream or None))
+
+
+# ------------------------------------------------------------ multi-GPU ----
+def batch_split(batch: int, ndev: int, i: int):
+    """np_batch_split: (begin, count) of device i's contiguous payload range."""
+    b, c = _sz(), _sz()
+    lib().np_batch_split(batch, ndev, i, C.byref(b), C.byref(c))
+    return b.value, c.value
+
+
+def _ptr_array(vals):
+    arr = (C.c_void_p * max(1, len(vals)))()
+    for i, v in enumerate(vals):
+        arr[i] = v or None
+    return arr
+
+
+def _ctx_array(ctxs):
+    return _ptr_array([c.handle.value for c in ctxs])
+
+
+def encode_batch_multi(ctxs, params: CodeParams, d_payloads, payload_len: int, payload_stride: int, batch: int,
+                       d_shards, batch_stride: int) -> None:
+    """Device-resident batch over several contexts (one per GPU); d_payloads[i] /
+    d_shards[i]: device i's buffers for its range (:func:`batch_split`)."""
+    _raise(lib().np_encode_batch_multi(_ctx_array(ctxs), len(ctxs), C.byref(params._c()), _ptr_array(d_payloads),
+                                       payload_len, payload_stride, batch, _ptr_array(d_shards), batch_stride))
+
+
+def reconstruct_batch_multi(ctxs, params: CodeParams, d_shards, shard_len: int, batch_stride: int, d_present,
+                            batch: int, d_out, out_stride: int, d_status=None) -> None:
+    st = _ptr_array(d_status) if d_status else None
+    _raise(lib().np_reconstruct_batch_multi(_ctx_array(ctxs), len(ctxs), C.byref(params._c()), _ptr_array(d_shards),
+                                            shard_len, batch_stride, _ptr_array(d_present), batch, _ptr_array(d_out),
+                                            out_stride, st))
+
+
+def encode_batch_host_multi(ctxs, params: CodeParams, payloads: int, payload_len: int, payload_stride: int,
+                            batch: int, shards: int, batch_stride: int) -> None:
+    _raise(lib().np_encode_batch_host_multi(_ctx_array(ctxs), len(ctxs), C.byref(params._c()), payloads, payload_len,
+                                            payload_stride, batch, shards, batch_stride))
+
+
+def reconstruct_batch_host_multi(ctxs, params: CodeParams, shards: int, shard_len: int, batch_stride: int,
+                                 present: int, batch: int, out: int, out_stride: int) -> None:
+    _raise(lib().np_reconstruct_batch_host_multi(_ctx_array(ctxs), len(ctxs), C.byref(params._c()), shards, shard_len,
+                                                 batch_stride, present, batch, out, out_stride))
 
 
 # ---------------------------------------------------- low-level hooks ----

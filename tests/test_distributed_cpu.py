@@ -80,3 +80,29 @@ def test_partition_is_disjoint_and_complete():
         got = [bench.partition(1024, world, r) for r in range(world)]
         assert got[0][0] == 0 and got[-1][1] == 1024 * world
         assert all(a[1] == b[0] for a, b in zip(got, got[1:]))
+
+
+def test_bench_gpus_flag_spawns_ranks():
+    """`python bench.py --gpus 2` outside torchrun starts two ranks under
+    torch.distributed.run (bench.launch_replicas); each takes a disjoint payload
+    range and the job reports n_gpus = 2 (NP_BENCH_DRYRUN: gloo, no GPU)."""
+    import json
+    import subprocess
+
+    env = dict(os.environ, NP_BENCH_DRYRUN="1", OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--batch", "8"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2
+    assert [tuple(x) for x in line["ranges"]] == [(0, 8), (8, 16)]
+
+
+def test_bench_rejects_mismatched_world_size():
+    import subprocess
+
+    env = dict(os.environ, NP_BENCH_DRYRUN="1", WORLD_SIZE="1", RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8"], capture_output=True,
+                       text=True, env=env, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr

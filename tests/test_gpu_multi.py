@@ -1,0 +1,97 @@
+"""Multi-device batch entry points (np_*_batch_multi, np_*_batch_host_multi):
+the batch split into contiguous ranges, one context and host thread per range.
+The test box has one GPU, so the "devices" are several contexts on device 0
+(distinct streams, scratch and threads -- the same code path as distinct
+GPUs); every payload is checked against the oracle."""
+import numpy as np
+import pytest
+
+import novelpoly_amd as npa
+from novelpoly_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(a):
+    import torch
+
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+@pytest.mark.parametrize("nw,kw,plen,batch,nctx", [(1024, 342, 512 * 300 + 5, 7, 2), (256, 86, 128 * 99, 9, 3),
+                                                   (300, 100, 5000, 5, 2)])
+def test_device_batch_multi(gpu, oracle, nw, kw, plen, batch, nctx):
+    import torch
+
+    ctxs = [npa.Context(0) for _ in range(nctx)]
+    p = npa.CodeParams.derive_parameters(nw, kw)
+    n, k = p.n(), p.k()
+    sl = p.make_encoder(gpu).shard_len(plen)
+    olen = (sl // 2) * 2 * k
+    pls = np.stack([np.frombuffer(synth.payload(500 + b, plen), np.uint8) for b in range(batch)])
+    pres = np.stack([synth.present_mask(500 + b, n, (n - k) // 2) for b in range(batch)])
+    rng = np.random.default_rng(batch)
+    ranges = [npa.batch_split(batch, nctx, i) for i in range(nctx)]
+    d_pay = [_dev(pls[b0:b0 + c]) for b0, c in ranges]
+    d_sh = [torch.zeros((c, n, sl), dtype=torch.uint8, device="cuda") for _, c in ranges]
+    torch.cuda.synchronize()
+    npa.encode_batch_multi(ctxs, p, [t.data_ptr() for t in d_pay], plen, plen, batch, [t.data_ptr() for t in d_sh],
+                           n * sl)
+    shards = np.concatenate([t.cpu().numpy() for t in d_sh])
+    for b in range(batch):
+        st, want = oracle.encode(pls[b].tobytes(), n, k, p.wanted_n)
+        assert st == 0 and [shards[b, i].tobytes() for i in range(p.wanted_n)] == want, b
+    # corrupt a present row of some payloads: the decode must still be the reference's map
+    for b in range(0, batch, 2):
+        v = int(rng.choice(np.flatnonzero(pres[b])))
+        shards[b, v] ^= 0x5C
+    d_sh = [_dev(shards[b0:b0 + c]) for b0, c in ranges]
+    d_pr = [_dev(pres[b0:b0 + c]) for b0, c in ranges]
+    d_out = [torch.zeros((c, olen), dtype=torch.uint8, device="cuda") for _, c in ranges]
+    d_st = [torch.full((c, 2), -1, dtype=torch.int32, device="cuda") for _, c in ranges]
+    torch.cuda.synchronize()
+    npa.reconstruct_batch_multi(ctxs, p, [t.data_ptr() for t in d_sh], sl, n * sl, [t.data_ptr() for t in d_pr],
+                                batch, [t.data_ptr() for t in d_out], olen, [t.data_ptr() for t in d_st])
+    out = np.concatenate([t.cpu().numpy() for t in d_out])
+    stat = np.concatenate([t.cpu().numpy() for t in d_st])
+    for b in range(batch):
+        st, want = oracle.reconstruct([shards[b, i].tobytes() if pres[b, i] else None for i in range(n)], n, k)
+        assert st == 0 and out[b].tobytes() == want, b
+        assert tuple(stat[b]) == (0, int(pres[b].sum()))
+
+
+def test_host_batch_multi(gpu, oracle):
+    ctxs = [npa.Context(0), npa.Context(0)]
+    p = npa.CodeParams.derive_parameters(1024, 342)
+    n, k = p.n(), p.k()
+    plen, batch = 512 * 260 + 1, 5
+    sl = p.make_encoder(gpu).shard_len(plen)
+    pay = np.stack([np.frombuffer(synth.payload(900 + b, plen), np.uint8) for b in range(batch)])
+    sh = np.zeros((batch, n * sl), np.uint8)
+    npa.encode_batch_host_multi(ctxs, p, pay.ctypes.data, plen, plen, batch, sh.ctypes.data, n * sl)
+    pres = np.stack([synth.present_mask(900 + b, n, 342) for b in range(batch)])
+    olen = (sl // 2) * 2 * k
+    out = np.zeros((batch, olen), np.uint8)
+    npa.reconstruct_batch_host_multi(ctxs, p, sh.ctypes.data, sl, n * sl, pres.ctypes.data, batch, out.ctypes.data,
+                                     olen)
+    for b in range(batch):
+        st, want = oracle.encode(pay[b].tobytes(), n, k, n)
+        assert st == 0 and sh[b].tobytes() == b"".join(want)
+        assert out[b, :plen].tobytes() == pay[b].tobytes()
+
+
+def test_multi_reports_need_more_shards(gpu):
+    """A host-memory multi call fails like the crate (NeedMoreShards) when one
+    range holds a payload with fewer than k present shards."""
+    ctxs = [npa.Context(0), npa.Context(0)]
+    p = npa.CodeParams.derive_parameters(256, 86)
+    n, k = p.n(), p.k()
+    sl, batch = 256, 4
+    sh = np.zeros((batch, n * sl), np.uint8)
+    pres = np.ones((batch, n), np.uint8)
+    pres[3, : n - k + 1] = 0  # last payload (second range): k - 1 present
+    out = np.zeros((batch, (sl // 2) * 2 * k), np.uint8)
+    with pytest.raises(npa.NeedMoreShards) as e:
+        npa.reconstruct_batch_host_multi(ctxs, p, sh.ctypes.data, sl, n * sl, pres.ctypes.data, batch,
+                                         out.ctypes.data, out.shape[1])
+    assert e.value.fields == (k - 1, k, n)

@@ -129,3 +129,17 @@ def test_payload_batch_dev_matches_splitmix():
         for i in range(lo, hi):
             assert got[i - lo].tobytes() == synth.payload(i, nbytes), (lo, hi, nbytes, i)
 
+
+
+def test_batch_split_contiguous_ranges():
+    """np_batch_split: contiguous, disjoint ranges covering the
+    batch, sizes differing by at most one, the larger ones first."""
+    for batch in (0, 1, 7, 8, 1000, 8192):
+        for ndev in (1, 2, 3, 8):
+            rng = [npa.batch_split(batch, ndev, i) for i in range(ndev)]
+            assert rng[0][0] == 0
+            assert all(a[0] + a[1] == b[0] for a, b in zip(rng, rng[1:]))
+            assert rng[-1][0] + rng[-1][1] == batch
+            sizes = [c for _, c in rng]
+            assert max(sizes) - min(sizes) <= 1 and sizes == sorted(sizes, reverse=True)
+    assert npa.batch_split(10, 2, 5) == (10, 0)  # out-of-range device: empty
