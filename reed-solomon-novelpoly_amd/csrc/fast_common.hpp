@@ -242,7 +242,54 @@ __device__ __forceinline__ Mult staged_mult(const uint32_t (&sp)[12], const uint
 }
 
 // x ^= c*y on four byte-planar symbols (pool layout: field_tables.cpp).
+#ifndef NP_QMUL_MERGED
+#define NP_QMUL_MERGED 0
+#endif
+// One output plane: acc ^= XOR of the 6 lookups of both input planes (asm
+// fragment of a merged quad multiply; operands named as in qmul_merged).
+#define NP_QPLANE_ASM(ACC, VA, VB, VC, VD, SA, SB, SC, SD, SE, SF)                                    \
+  "v_perm_b32 %[t0], %[" SA "], %[" VA "], %[s0]\n\t"                                               \
+  "v_perm_b32 %[t1], %[" SB "], %[" VB "], %[s1]\n\t"                                               \
+  "v_perm_b32 %[t2], %[" SC "], %[" SC "], %[s2]\n\t"                                               \
+  "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t"                                         \
+  "v_perm_b32 %[t1], %[" SD "], %[" VC "], %[s3]\n\t"                                               \
+  "v_perm_b32 %[t2], %[" SE "], %[" VD "], %[s4]\n\t"                                               \
+  "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t"                                         \
+  "v_perm_b32 %[t1], %[" SF "], %[" SF "], %[s5]\n\t"                                               \
+  "v_bitop3_b32 %[" ACC "], %[" ACC "], %[t0], %[t1] bitop3:0x96\n\t"
+
+// The selectors of both planes (32-bit shifts: one asm block per multiply,
+// no hazard s_nop between the pieces of a multiply).
+#define NP_SEL_ASM                                   \
+  "v_and_b32 %[s0], 0x07070707, %[yl]\n\t"          \
+  "v_lshrrev_b32 %[s1], 3, %[yl]\n\t"               \
+  "v_lshrrev_b32 %[s2], 6, %[yl]\n\t"               \
+  "v_and_b32 %[s3], 0x07070707, %[yh]\n\t"          \
+  "v_lshrrev_b32 %[s4], 3, %[yh]\n\t"               \
+  "v_lshrrev_b32 %[s5], 6, %[yh]\n\t"               \
+  "v_and_b32 %[s1], 0x07070707, %[s1]\n\t"          \
+  "v_and_b32 %[s2], 0x03030303, %[s2]\n\t"          \
+  "v_and_b32 %[s4], 0x07070707, %[s4]\n\t"          \
+  "v_and_b32 %[s5], 0x03030303, %[s5]\n\t"
+
+__device__ __forceinline__ void qmul_merged(uint32_t& xl, uint32_t& xh, uint32_t yl, uint32_t yh, const Mult& m) {
+  uint32_t s0, s1, s2, s3, s4, s5, t0, t1, t2;
+  asm volatile(NP_SEL_ASM NP_QPLANE_ASM("xl", "v0", "v1", "v2", "v3", "a0", "a1", "a2", "a3", "a4", "a5")
+                   NP_QPLANE_ASM("xh", "v4", "v5", "v6", "v7", "a6", "a7", "a8", "a9", "a10", "a11")
+               : [xl] "+v"(xl), [xh] "+v"(xh), [s0] "=&v"(s0), [s1] "=&v"(s1), [s2] "=&v"(s2), [s3] "=&v"(s3),
+                 [s4] "=&v"(s4), [s5] "=&v"(s5), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2)
+               : [yl] "v"(yl), [yh] "v"(yh), [v0] "v"(m.v[0]), [v1] "v"(m.v[1]), [v2] "v"(m.v[2]),
+                 [v3] "v"(m.v[3]), [v4] "v"(m.v[4]), [v5] "v"(m.v[5]), [v6] "v"(m.v[6]), [v7] "v"(m.v[7]),
+                 [a0] "s"(m.s[0]), [a1] "s"(m.s[1]), [a2] "s"(m.s[2]), [a3] "s"(m.s[3]), [a4] "s"(m.s[4]),
+                 [a5] "s"(m.s[5]), [a6] "s"(m.s[6]), [a7] "s"(m.s[7]), [a8] "s"(m.s[8]), [a9] "s"(m.s[9]),
+                 [a10] "s"(m.s[10]), [a11] "s"(m.s[11]));
+}
+
 __device__ __forceinline__ void qmul(uint32_t& xl, uint32_t& xh, uint32_t yl, uint32_t yh, const Mult& m) {
+  if constexpr (NP_QMUL_MERGED) {
+    qmul_merged(xl, xh, yl, yh, m);
+    return;
+  }
   uint32_t s[6];
   selectors(yl, yh, s);
   qplane(xl, s, m.v[0], m.v[1], m.v[2], m.v[3], m.s[0], m.s[1], m.s[2], m.s[3], m.s[4], m.s[5]);
@@ -292,6 +339,27 @@ __device__ __forceinline__ void qplane_sub_set(uint32_t& out, uint32_t s0, uint3
 
 // x ^= c*y, c in GF(2^8), tower coordinates.
 __device__ __forceinline__ void qmul_sub(uint32_t& xl, uint32_t& xh, uint32_t yl, uint32_t yh, const Mult& m) {
+  if constexpr (NP_QMUL_MERGED) {
+    // one asm block; both planes read the a-plane tables (equal to the b-plane
+    // ones: field_tables.hpp, e_i = beta_i)
+    uint32_t s0, s1, s2, s3, s4, s5, t0, t1, t2;
+    asm volatile(NP_SEL_ASM
+                 "v_perm_b32 %[t0], %[sa], %[va], %[s0]\n\t"
+                 "v_perm_b32 %[t1], %[sb], %[vb], %[s1]\n\t"
+                 "v_perm_b32 %[t2], %[sc], %[sc], %[s2]\n\t"
+                 "v_bitop3_b32 %[xl], %[xl], %[t0], %[t1] bitop3:0x96\n\t"
+                 "v_xor_b32 %[xl], %[xl], %[t2]\n\t"
+                 "v_perm_b32 %[t0], %[sa], %[va], %[s3]\n\t"
+                 "v_perm_b32 %[t1], %[sb], %[vb], %[s4]\n\t"
+                 "v_perm_b32 %[t2], %[sc], %[sc], %[s5]\n\t"
+                 "v_bitop3_b32 %[xh], %[xh], %[t0], %[t1] bitop3:0x96\n\t"
+                 "v_xor_b32 %[xh], %[xh], %[t2]"
+                 : [xl] "+v"(xl), [xh] "+v"(xh), [s0] "=&v"(s0), [s1] "=&v"(s1), [s2] "=&v"(s2), [s3] "=&v"(s3),
+                   [s4] "=&v"(s4), [s5] "=&v"(s5), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2)
+                 : [yl] "v"(yl), [yh] "v"(yh), [va] "v"(m.v[0]), [vb] "v"(m.v[1]), [sa] "s"(m.s[0]),
+                   [sb] "s"(m.s[1]), [sc] "s"(m.s[2]));
+    return;
+  }
   uint32_t s[6];
   selectors(yl, yh, s);
   qplane_sub(xl, s[0], s[1], s[2], m.v[0], m.v[1], m.s[0], m.s[1], m.s[2]);

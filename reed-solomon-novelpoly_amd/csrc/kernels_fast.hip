@@ -475,6 +475,9 @@ __device__ __forceinline__ void copy_out_cq(uint8_t* out_tile, uint32_t lane, ui
 template <int NQ>
 constexpr bool kRowPrefetch = NQ <= 2;
 
+#ifndef NP_REC_IDX0
+#define NP_REC_IDX0 1  // measured: reconstruct -1.1 % (config 3)
+#endif
 // Largest gen_of over the decode's segment transforms (index qK, q < NQ).
 template <int K, int NQ>
 constexpr int kRecMaxGen = static_cast<int>(gen_of(static_cast<uint32_t>((NQ - 1) * K)));
@@ -561,7 +564,13 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
     __syncthreads();
     stamp(c.dbg, 5 + 6 * step);
     hi_read_p<K>(c.tile, hb, XL, XH);
-    hi_levels<K, true, false, 0, 0>(T, vp, index, XL, XH);  // hi levels: gen_of(index) <= 4
+    // hi levels: gen_of(index) <= 4; segment 0 (index 0) skips the t = 0
+    // groups, whose skew is the zero element (15 of the 32 quad multiplies)
+    // (the 2-segment decode keeps its rows prefetch live here: no room for two instances)
+    if (NP_REC_IDX0 && NQ == 4 && q == 0)
+      hi_levels<K, true, true, 0, 0>(T, vp, 0, XL, XH);
+    else
+      hi_levels<K, true, false, 0, 0>(T, vp, index, XL, XH);
     stamp(c.dbg, 6 + 6 * step);
     __builtin_amdgcn_sched_barrier(0);
     if (step == 0) {
