@@ -63,11 +63,16 @@ def aggregate_gib_s(world: int, per_rank: int, payload_len: int, elapsed: float,
     return world * per_rank * payload_len / (elapsed / steps) / 2**30
 
 
-def load_traffic(round_tag="r01"):
+ROUND_TAG = "r02"
+
+
+def load_traffic(config: int):
     """Per-launch HBM bytes (FETCH_SIZE + WRITE_SIZE, calibrated) of each kernel
-    from the committed PMC summary of this round (tools/profile_round.sh +
-    tools/pmc_summary.py, measured on this same bench command)."""
-    p = os.path.join(ROOT, "profiles", f"{round_tag}_pmc_summary.json")
+    from the committed PMC summary of this round for this config
+    (tools/profile_round.sh + tools/pmc_summary.py, measured on this same bench
+    command: profiles/r02_pmc_summary.json for config 3, r02_cfg<c>_... else)."""
+    tag = ROUND_TAG if config == 3 else f"{ROUND_TAG}_cfg{config}"
+    p = os.path.join(ROOT, "profiles", f"{tag}_pmc_summary.json")
     if not os.path.exists(p):
         return {}
     with open(p) as f:
@@ -261,9 +266,9 @@ def main():
         "encode": batch * (plen + nshard * sl),
         "reconstruct": present_rows * sl + batch * out_len,
     }
-    # the committed PMC summary was measured on the default workload (config 3
-    # at its BASELINE batch): other configs and batches report traffic null
-    traffic = load_traffic() if args.config == 3 and batch == cfg["batch"] else {}
+    # the committed PMC summaries were measured at each config's BASELINE batch:
+    # other batches report traffic null
+    traffic = load_traffic(args.config) if batch == cfg["batch"] else {}
     roof = {}
     for name in kt:
         achieved = algo[name] / (kt[name] / 1e3) / 1e9

@@ -1,5 +1,5 @@
 """Summarise a round's rocprofv3 outputs (tools/profile_round.sh) into
-profiles/<tag>_pmc_summary.json: per-launch HBM traffic of the codec kernels
+profiles/<tag>_pmc_summary.json: per-bench-step HBM traffic of the codec kernels
 (FETCH_SIZE and WRITE_SIZE from separate passes, corrected by the calibration
 microbenchmark for 8-byte lanes), SQ utilisation counters, and the kernel-trace
 averages.  Usage: python tools/pmc_summary.py r01"""
@@ -20,9 +20,13 @@ os.makedirs(dst, exist_ok=True)
 # The bench's "reconstruct" span is the prefix-locator launch plus both fast
 # reconstruct instances (prefixes of <= 2 and of 4 segments); their per-launch
 # traffic and durations add up.  Each instance is also reported on its own.
-KINDS = {"encode": ("k_encode_fast", "k_encode_multi"), "reconstruct": ("k_reconstruct_fast", "k_prefix_locator"),
-         "locator": ("k_error_locator",), "encode_big": ("k_encode_big",), "reconstruct_big": ("k_reconstruct_big",),
-         "calib_read8": ("read8",), "calib_copy8": ("copy8",)}
+KINDS = {"encode": ("k_encode_fast", "k_encode_multi", "k_encode_big"),
+         "reconstruct": ("k_reconstruct_fast", "k_prefix_locator", "k_reconstruct_big", "k_payload_status"),
+         "locator": ("k_error_locator",), "calib_read8": ("read8",), "calib_copy8": ("copy8",)}
+# bench steps per profiled command (tools/profile_round.sh): PMC passes run
+# 1 warmup + 3 timed steps, the kernel-trace pass 3 + 10; per-step values are
+# the sums over every dispatch of a kind divided by these
+PMC_STEPS, STATS_STEPS = 4, 13
 
 
 def instance(name):
@@ -63,10 +67,11 @@ def counters(pass_name):
     return agg
 
 
-def by_kind(c, k, name):
-    """Per-launch value of counter `name` for kind k: the sum over its instances."""
-    vals = [mean(v[name]) for i, v in c.items() if kind(i) == k and v.get(name)]
-    return sum(vals) if vals else None
+def by_kind(c, k, name, steps=PMC_STEPS):
+    """Per-step value of counter `name` for kind k: the sum over every dispatch
+    of its instances, divided by the steps of the profiled run."""
+    vals = [sum(v[name]) for i, v in c.items() if kind(i) == k and v.get(name)]
+    return sum(vals) / steps if vals else None
 
 
 def mean(v):
@@ -78,8 +83,12 @@ fetch, write = counters("fetch"), counters("write")
 cf, cw = counters("calib_fetch"), counters("calib_write")
 GIB = 1 << 30
 # calibration: read8 reads exactly 1 GiB per dispatch; copy8 reads 1 GiB and writes 1 GiB
-f_read8 = by_kind(cf, "calib_read8", "FETCH_SIZE")
-w_copy8 = by_kind(cw, "calib_copy8", "WRITE_SIZE")
+f_read8 = by_kind(cf, "calib_read8", "FETCH_SIZE", 1)
+w_copy8 = by_kind(cw, "calib_copy8", "WRITE_SIZE", 1)
+if f_read8:  # per dispatch of the calibration kernels
+    f_read8 /= len(next(v["FETCH_SIZE"] for i, v in cf.items() if kind(i) == "calib_read8"))
+if w_copy8:
+    w_copy8 /= len(next(v["WRITE_SIZE"] for i, v in cw.items() if kind(i) == "calib_copy8"))
 # FETCH_SIZE / WRITE_SIZE are reported in KB (1024 B) by rocprofv3
 fetch_factor = GIB / (f_read8 * 1024) if f_read8 else None
 write_factor = GIB / (w_copy8 * 1024) if w_copy8 else None
@@ -87,7 +96,7 @@ out["calibration"] = {"read8_FETCH_SIZE_KB": f_read8, "copy8_WRITE_SIZE_KB": w_c
                       "fetch_factor": fetch_factor, "write_factor": write_factor,
                       "note": "factor = known bytes / (counter * 1024) for 8-byte-per-lane coalesced access, "
                               "1 GiB buffers (beyond the 256 MiB Infinity Cache)"}
-for k in ("encode", "reconstruct", "locator", "encode_big", "reconstruct_big"):
+for k in ("encode", "reconstruct", "locator"):
     fs, ws = by_kind(fetch, k, "FETCH_SIZE"), by_kind(write, k, "WRITE_SIZE")
     if fs is None or ws is None:
         continue
@@ -111,7 +120,8 @@ if st:
             out["instances"].setdefault(i, {})["avg_ns"] = float(r["AverageNs"])
             out["instances"][i]["calls"] = int(r["Calls"])
             k = out["kernels"].setdefault(kind(i), {})
-            k["avg_ns"] = k.get("avg_ns", 0.0) + float(r["AverageNs"])
+            # per bench step: every dispatch of the kind in one step
+            k["ns_per_step"] = k.get("ns_per_step", 0.0) + float(r["TotalDurationNs"]) / STATS_STEPS
     shutil.copy(st[0], os.path.join(dst, f"{tag}_kernel_stats.csv"))
 for i, v in out["instances"].items():
     if "SQ_INSTS_VALU" in v and v.get("SQ_WAVES"):
