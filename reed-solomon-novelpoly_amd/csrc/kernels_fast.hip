@@ -409,10 +409,23 @@ struct RecCtx {
 };
 
 // Segment q of the sweep at step `step` (segments 2, 3, 1, 0 for NQ = 4; 1, 0
-// for NQ = 2).
+// for NQ = 2; 7, 6, ..., 0 for NQ = 8).
 template <int NQ>
 __host__ __device__ constexpr int seg_of(int step) {
-  return NQ == 4 ? (step == 0 ? 2 : step == 1 ? 3 : 3 - step) : 1 - step;
+  return NQ == 8 ? 7 - step : NQ == 4 ? (step == 0 ? 2 : step == 1 ? 3 : 3 - step) : 1 - step;
+}
+
+// NQ = 8: the first K outputs of the size-8K decode need
+//   d = D_K(x0) ^ sum_q kappa_q x_q,  x_q = IFFT(K, qK)(premultiplied segment q),
+// the three top inverse levels of index 0 (skews 0, Cantor(2), Cantor(4),
+// Cantor(6)) and the derivative's single-bit terms K, 2K, 4K folded into one
+// coefficient per segment: kappa = (1, 1, 1+b1, b1, (1+b1)(1+b2), (1+b1) b2,
+// b1 (1+b3), b1 b3) with b_i = Cantor(2i), in Cantor coordinates below (all in
+// GF(16); tests/test_host_cpu.py::test_rec8_kappa re-derives them with the
+// oracle).  One accumulator, one subfield multiply per segment and position.
+__host__ __device__ constexpr uint32_t rec8_kappa(int q) {
+  constexpr uint32_t k[8] = {1, 1, 3, 2, 12, 15, 10, 8};
+  return k[q];
 }
 
 // Presence of rows row0..row0+15 as bits (wave-uniform): one byte load per
@@ -573,14 +586,34 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
       hi_levels<K, true, false, 0, 0>(T, vp, index, XL, XH);
     stamp(c.dbg, 6 + 6 * step);
     __builtin_amdgcn_sched_barrier(0);
-    if (step == 0) {
+    if (NQ == 8 && q != 0) {  // A ^= kappa_q x_q (kRec8Kappa, all in GF(2^8))
+      const uint32_t kq = uniform(rec8_kappa(q));
+      if (kq == 1u) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          AL[j] ^= XL[j];
+          AH[j] ^= XH[j];
+        }
+      } else {
+        uint32_t kp[20];
+        pool_of<true>(T, kq, kp);
+        const Mult pool = make_mult(kp);
+        if (step == 0) {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) qmul_sub_set(AL[j], AH[j], XL[j], XH[j], pool);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) qmul_sub(AL[j], AH[j], XL[j], XH[j], pool);
+        }
+      }
+    } else if (step == 0) {
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         AL[j] = XL[j];
         AH[j] = XH[j];
       }
     } else if (q == 0) {
-      if (NQ == 2) {
+      if (NQ == 2 || NQ == 8) {  // kappa_0 = 1
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
           AL[j] ^= XL[j];
@@ -799,8 +832,8 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
                                                                static_cast<size_t>(nsyms) * 2 * K + 256u * tl)
                                  : nullptr;
     stamp(dbg, 0);
-    if constexpr (NQ == 4) {
-      if (t > 0) {  // segment 2's tables were replaced during the previous tile
+    if constexpr (NQ >= 4) {
+      if (t > 0) {  // the first two segments' tables were replaced during the previous tile
         __syncthreads();
         stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(0)) * K, VP, true);
         stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(1)) * K, VP + G::kVPWords, true);
@@ -924,11 +957,11 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
   const int nq = uniform(rec[0]);
   const uint32_t* rows = reinterpret_cast<const uint32_t*>(rec + prefix_pools_offset(N));
   if constexpr (kMultiTile<K>) {
-    if constexpr (SERVE == 4) {
-      if (nq == 4) rec_tiles<K, 4>(T, a, pres, rows, smem, pb, tl0, ntl, nsyms);
+    if constexpr (SERVE >= 4) {
+      if (nq == SERVE) rec_tiles<K, SERVE>(T, a, pres, rows, smem, pb, tl0, ntl, nsyms);
     } else if (nq == 1) {
       rec_tiles<K, 1>(T, a, pres, rows, smem, pb, tl0, ntl, nsyms);
-    } else if (nq == 2) {
+    } else if (NQ <= 4 && nq == 2) {
       rec_tiles<K, 2>(T, a, pres, rows, smem, pb, tl0, ntl, nsyms);
     }
   } else {  // tpw == 1
@@ -940,11 +973,11 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     uint64_t* dbg = (kExp & 64) ? reinterpret_cast<uint64_t*>(a.out + static_cast<size_t>(pb) * a.out_stride +
                                                                static_cast<size_t>(nsyms) * 2 * K + 256u * tl0)
                                  : nullptr;
-    if constexpr (SERVE == 4) {
-      if (nq == 4) rec_tile<K, 4>(T, a, sh, pres, rows, smem, pb, col0, ncols, full, dbg);
+    if constexpr (SERVE >= 4) {
+      if (nq == SERVE) rec_tile<K, SERVE>(T, a, sh, pres, rows, smem, pb, col0, ncols, full, dbg);
     } else if (nq == 1) {
       rec_tile<K, 1>(T, a, sh, pres, rows, smem, pb, col0, ncols, full, dbg);
-    } else if (nq == 2) {
+    } else if (NQ <= 4 && nq == 2) {
       rec_tile<K, 2>(T, a, sh, pres, rows, smem, pb, col0, ncols, full, dbg);
     }
   }
@@ -1117,10 +1150,19 @@ hipError_t launch_reconstruct_k(const DevTables& T, const ReconstructArgs& a, hi
   if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
   k_reconstruct_fast<K, NQ, 2><<<static_cast<uint32_t>(blocks), Geo<K>::kThreads, reconstruct_lds_bytes<K, NQ>(), s>>>(
       T, a, static_cast<uint32_t>(nsyms), tiles, tpw);
-  if constexpr (NQ == 4)
-    k_reconstruct_fast<K, NQ, 4><<<static_cast<uint32_t>(blocks), Geo<K>::kThreads, reconstruct_lds_bytes<K, NQ>(), s>>>(
+  if constexpr (NQ >= 4)
+    k_reconstruct_fast<K, NQ, NQ><<<static_cast<uint32_t>(blocks), Geo<K>::kThreads, reconstruct_lds_bytes<K, NQ>(), s>>>(
         T, a, static_cast<uint32_t>(nsyms), tiles, tpw);
   return hipGetLastError();
+}
+
+// f(K, NQ) with NQ = n / k in {2, 4, 8} as compile-time constants.
+template <int K, typename F>
+hipError_t by_nq(const ReconstructArgs& a, F f) {
+  using KC = std::integral_constant<int, K>;
+  if (a.n == 8u * K) return f(KC{}, std::integral_constant<int, 8>{});
+  if (a.n == 4u * K) return f(KC{}, std::integral_constant<int, 4>{});
+  return f(KC{}, std::integral_constant<int, 2>{});
 }
 
 }  // namespace
@@ -1130,7 +1172,7 @@ bool fast_encode_supported(uint32_t n, uint32_t k) {
 }
 
 bool fast_reconstruct_supported(uint32_t n, uint32_t k) {
-  return (k == 64 || k == 128 || k == 256) && (n == 2 * k || n == 4 * k);
+  return (k == 64 || k == 128 || k == 256) && (n == 2 * k || n == 4 * k || n == 8 * k);
 }
 
 hipError_t launch_encode_fast(const DevTables& T, const EncodeArgs& a, hipStream_t s) {
@@ -1145,21 +1187,19 @@ hipError_t launch_encode_fast(const DevTables& T, const EncodeArgs& a, hipStream
 size_t prefix_stride(uint32_t n, uint32_t k) { return prefix_stride_c(n, k); }
 
 hipError_t launch_prefix_locator(const DevTables& T, const ReconstructArgs& a, uint8_t* out, hipStream_t s) {
-  const bool q4 = a.n == 4 * a.k;
   switch (a.k) {
-    case 64: return q4 ? launch_prefix_k<64, 4>(T, a, out, s) : launch_prefix_k<64, 2>(T, a, out, s);
-    case 128: return q4 ? launch_prefix_k<128, 4>(T, a, out, s) : launch_prefix_k<128, 2>(T, a, out, s);
-    case 256: return q4 ? launch_prefix_k<256, 4>(T, a, out, s) : launch_prefix_k<256, 2>(T, a, out, s);
+    case 64: return by_nq<64>(a, [&](auto K, auto NQ) { return launch_prefix_k<K.value, NQ.value>(T, a, out, s); });
+    case 128: return by_nq<128>(a, [&](auto K, auto NQ) { return launch_prefix_k<K.value, NQ.value>(T, a, out, s); });
+    case 256: return by_nq<256>(a, [&](auto K, auto NQ) { return launch_prefix_k<K.value, NQ.value>(T, a, out, s); });
     default: return hipErrorNotSupported;
   }
 }
 
 hipError_t launch_reconstruct_fast(const DevTables& T, const ReconstructArgs& a, hipStream_t s) {
-  const bool q4 = a.n == 4 * a.k;
   switch (a.k) {
-    case 64: return q4 ? launch_reconstruct_k<64, 4>(T, a, s) : launch_reconstruct_k<64, 2>(T, a, s);
-    case 128: return q4 ? launch_reconstruct_k<128, 4>(T, a, s) : launch_reconstruct_k<128, 2>(T, a, s);
-    case 256: return q4 ? launch_reconstruct_k<256, 4>(T, a, s) : launch_reconstruct_k<256, 2>(T, a, s);
+    case 64: return by_nq<64>(a, [&](auto K, auto NQ) { return launch_reconstruct_k<K.value, NQ.value>(T, a, s); });
+    case 128: return by_nq<128>(a, [&](auto K, auto NQ) { return launch_reconstruct_k<K.value, NQ.value>(T, a, s); });
+    case 256: return by_nq<256>(a, [&](auto K, auto NQ) { return launch_reconstruct_k<K.value, NQ.value>(T, a, s); });
     default: return hipErrorNotSupported;
   }
 }
@@ -1183,6 +1223,12 @@ hipError_t configure_fast_kernels() {
   set(reinterpret_cast<const void*>(&k_reconstruct_fast<256, 2, 2>), reconstruct_lds_bytes<256, 2>());
   set(reinterpret_cast<const void*>(&k_reconstruct_fast<256, 4, 2>), reconstruct_lds_bytes<256, 4>());
   set(reinterpret_cast<const void*>(&k_reconstruct_fast<256, 4, 4>), reconstruct_lds_bytes<256, 4>());
+  set(reinterpret_cast<const void*>(&k_reconstruct_fast<64, 8, 2>), reconstruct_lds_bytes<64, 8>());
+  set(reinterpret_cast<const void*>(&k_reconstruct_fast<64, 8, 8>), reconstruct_lds_bytes<64, 8>());
+  set(reinterpret_cast<const void*>(&k_reconstruct_fast<128, 8, 2>), reconstruct_lds_bytes<128, 8>());
+  set(reinterpret_cast<const void*>(&k_reconstruct_fast<128, 8, 8>), reconstruct_lds_bytes<128, 8>());
+  set(reinterpret_cast<const void*>(&k_reconstruct_fast<256, 8, 2>), reconstruct_lds_bytes<256, 8>());
+  set(reinterpret_cast<const void*>(&k_reconstruct_fast<256, 8, 8>), reconstruct_lds_bytes<256, 8>());
   return e;
 }
 

@@ -16,7 +16,8 @@ from novelpoly_amd import synth
 pytestmark = pytest.mark.gpu
 
 # (n_wanted, k_wanted) -> effective k in {64, 128, 256}, n in {2k, 4k, 8k}
-SHAPES = [(1024, 342), (512, 256), (2048, 300), (256, 86), (512, 128), (256, 128), (768, 256)]
+SHAPES = [(1024, 342), (512, 256), (2048, 300), (256, 86), (512, 128), (256, 128), (768, 256), (300, 100),
+          (700, 234)]
 
 
 def _erasures(rng, n, k, mode):
@@ -53,8 +54,7 @@ def test_fuzz_device_batch_roundtrip(gpu, oracle, monkeypatch, case):
     dp = dev(pls)
     ds = torch.zeros((batch, sstride), dtype=torch.uint8, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
-    p_enc = p if wanted == n else npa.CodeParams.derive_parameters(wanted, kw)
-    assert p_enc.n() == n and p_enc.k() == k
+    p_enc = npa.CodeParams(n, k, wanted)
     npa.encode_batch_dev(p_enc, dp.data_ptr(), plen, pstride, batch, ds.data_ptr(), sstride, ctx=gpu, stream=s)
     torch.cuda.synchronize()
     hs = ds.cpu().numpy()

@@ -320,14 +320,17 @@ def test_fast_encode_shapes(gpu, oracle, nw, kw, plen):
                                               (512, 256, 512 * 257, 256), (1000, 256, 4097, 0),
                                               (1024, 342, 512 * 256, -1), (4096, 1366, 2048 * 256, 2730),
                                               (4096, 1366, 2048 * 260 + 1, 3072), (2048, 1024, 2048 * 100, 1024),
-                                              (4096, 1366, 2048 * 256, -1), (3000, 1024, 7777, 1000)])
+                                              (4096, 1366, 2048 * 256, -1), (3000, 1024, 7777, 1000),
+                                              (300, 100, 128 * 256, 200), (300, 100, 128 * 300 + 7, -1),
+                                              (700, 234, 256 * 256 + 1, 500), (1200, 400, 512 * 256, 900),
+                                              (1200, 400, 512 * 257, -1), (512, 64, 128 * 64, 448)])
 def test_fast_reconstruct_shapes(gpu, oracle, nw, kw, plen, erase):
-    """Specialised reconstruct kernel (k in {64,128,256}, n in {2k,4k}): full and
-    partial column tiles, random and worst-case erasure sets (erase = -1: every
-    systematic shard lost), bit-exact against the oracle."""
+    """Specialised reconstruct kernel (k in {64,128,256}, n in {2k,4k,8k}): full
+    and partial column tiles, random and worst-case erasure sets (erase = -1:
+    every systematic shard lost), bit-exact against the oracle."""
     p = npa.CodeParams.derive_parameters(nw, kw)
     n, k = p.n(), p.k()
-    assert n in (2 * k, 4 * k) and k in (64, 128, 256, 1024)
+    assert n in (2 * k, 4 * k, 8 * k) and k in (64, 128, 256, 1024)
     pl = synth.payload(7 * nw + plen, plen)
     shards = p.make_encoder(gpu).encode(pl)
     if erase == -1:
@@ -343,7 +346,8 @@ def test_fast_reconstruct_shapes(gpu, oracle, nw, kw, plen, erase):
 
 
 @pytest.mark.parametrize("nw,kw,plen,batch", [(1024, 342, 512 * 300, 5), (256, 86, 128 * 256 + 7, 9),
-                                              (512, 256, 512 * 256, 3), (2048, 512, 1024 * 40, 2)])
+                                              (512, 256, 512 * 256, 3), (2048, 512, 1024 * 40, 2),
+                                              (300, 100, 128 * 300, 4), (1200, 400, 512 * 260, 3)])
 def test_device_reconstruct_locator_modes(gpu, oracle, nw, kw, plen, batch):
     """np_reconstruct_batch_dev2 with locators from np_error_locator_dev and with
     d_locators = NULL (computed on the device: fused folded locator on the fast
@@ -357,7 +361,10 @@ def test_device_reconstruct_locator_modes(gpu, oracle, nw, kw, plen, batch):
     dp = dev(pls)
     ds = torch.empty((batch, n, sl), dtype=torch.uint8, device="cuda")
     npa.encode_batch_dev(p, dp.data_ptr(), plen, plen, batch, ds.data_ptr(), n * sl, ctx=gpu, stream=stream())
-    pres = np.stack([synth.present_mask(900 + b, n, (n - k) if b % 2 else (n - k) // 3) for b in range(batch)])
+    wn = p.wanted_n  # rows >= wanted_n were never encoded: absent
+    pres = np.zeros((batch, n), np.uint8)
+    for b in range(batch):
+        pres[b, :wn] = synth.present_mask(900 + b, wn, (wn - k) if b % 2 else (wn - k) // 3)
     dpres = dev(pres)
     loc = torch.empty((batch, n), dtype=torch.int16, device="cuda")
     npa.error_locator_dev(n, dpres.data_ptr(), batch, loc.data_ptr(), ctx=gpu, stream=stream())
