@@ -36,6 +36,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--out", default="", help="also write the JSON line to this file")
+    # ad-hoc shapes for DESIGN measurements (never the headline): override the config's
+    ap.add_argument("--n-wanted", type=int, default=0)
+    ap.add_argument("--k-wanted", type=int, default=0)
+    ap.add_argument("--payload", type=int, default=0, help="payload bytes")
+    ap.add_argument("--erase", type=int, default=-1, help="erasures per payload")
     return ap.parse_args()
 
 
@@ -193,6 +198,13 @@ def main():
 
     cfg = dict(synth.CONFIGS[args.config])
     cfg["id"] = args.config
+    if args.n_wanted or args.k_wanted or args.payload or args.erase >= 0:  # ad-hoc shape
+        cfg["id"] = f"{args.config}+override"
+        cfg["n_wanted"] = args.n_wanted or cfg["n_wanted"]
+        cfg["k_wanted"] = args.k_wanted or npa.recoverablity_subset_size(cfg["n_wanted"])
+        cfg["payload"] = args.payload or cfg["payload"]
+        if args.erase >= 0:
+            cfg["erase"] = args.erase
     params = npa.CodeParams.derive_parameters(cfg["n_wanted"], cfg["k_wanted"])
     n, k = params.n(), params.k()
     batch = args.batch or (cfg["batch"] if args.config != 5 else cfg["batch"] // 8)
@@ -209,8 +221,12 @@ def main():
     # with seed 0xE7A5_0000 + i
     payloads = synth.payload_batch_dev(lo, hi, plen, dev)
     shards = torch.empty((batch, n, sl), dtype=torch.uint8, device=dev)
-    present_h = torch.from_numpy(
-        __import__("numpy").stack([synth.present_mask(i, n, erase) for i in range(lo, hi)]))
+    np_ = __import__("numpy")
+    wn = params.wanted_n  # rows >= wanted_n are never produced: absent (BASELINE configs: wanted_n == n)
+    pres_np = np_.zeros((hi - lo, n), np_.uint8)
+    for i in range(lo, hi):
+        pres_np[i - lo, :wn] = synth.present_mask(i, wn, erase)
+    present_h = torch.from_numpy(pres_np)
     present = present_h.to(dev)
     out = torch.empty((batch, out_len), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -257,7 +273,7 @@ def main():
     value = aggregate_gib_s(world, batch, plen, elapsed, args.steps)
 
     kt = {name: sum(a.elapsed_time(b) for a, b in pairs) / len(pairs) for name, pairs in ev.items()}
-    nshard = n  # wanted_n == n for the BASELINE configs
+    nshard = params.wanted_n  # == n for the BASELINE configs
     # SURVEY.md §8(d) algorithmic bytes per payload: encode = P + n * shard_len;
     # reconstruct = present * shard_len + (shard_len / 2) * 2k (every present
     # row is read: the reference decodes from all of them)
@@ -268,7 +284,7 @@ def main():
     }
     # the committed PMC summaries were measured at each config's BASELINE batch:
     # other batches report traffic null
-    traffic = load_traffic(args.config) if batch == cfg["batch"] else {}
+    traffic = load_traffic(args.config) if batch == cfg["batch"] and cfg["id"] == args.config else {}
     roof = {}
     for name in kt:
         achieved = algo[name] / (kt[name] / 1e3) / 1e9
@@ -290,7 +306,7 @@ def main():
         "vs_baseline": None,
         "dtype": "u16",
         "data": "synthetic",
-        "config": {"workload": f"BASELINE config {args.config}: n_wanted={cfg['n_wanted']} "
+        "config": {"workload": f"BASELINE config {cfg['id']}: n_wanted={cfg['n_wanted']} "
                                f"k_wanted={cfg['k_wanted']} (effective n={n}, k={k}), {plen} B payloads, "
                                f"batch {batch}/GPU, encode + error locator + reconstruct with {erase} "
                                f"random erasures per payload",

@@ -421,7 +421,7 @@ __host__ __device__ constexpr int seg_of(int step) {
 // Cantor(6)) and the derivative's single-bit terms K, 2K, 4K folded into one
 // coefficient per segment: kappa = (1, 1, 1+b1, b1, (1+b1)(1+b2), (1+b1) b2,
 // b1 (1+b3), b1 b3) with b_i = Cantor(2i), in Cantor coordinates below (all in
-// GF(16); tests/test_host_cpu.py::test_rec8_kappa re-derives them with the
+// GF(16); tests/test_oracle.py::test_rec8_kappa re-derives them with the
 // oracle).  One accumulator, one subfield multiply per segment and position.
 __host__ __device__ constexpr uint32_t rec8_kappa(int q) {
   constexpr uint32_t k[8] = {1, 1, 3, 2, 12, 15, 10, 8};

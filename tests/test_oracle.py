@@ -281,3 +281,31 @@ def test_corrupted_row_beyond_prefix_changes_reference(oracle):
     rows[v] ^= 0xFF
     st2, b = oracle.reconstruct(recv(), n, k)
     assert st == st2 == 0 and a != b
+
+
+def test_rec8_kappa(oracle):
+    """The n = 8k decode folds the top inverse levels and the derivative's
+    single-bit terms into one coefficient per segment (kernels_fast.hip
+    rec8_kappa): d = D_K(x0) ^ sum_q kappa_q x_q equals the first K entries of
+    formal_derivative(inverse_afft(a, n, 0)) (inc_reconstruct.rs:76-78) for
+    random inputs; and the constants in the kernel source are these."""
+    import os
+    import re
+
+    import numpy as np
+
+    src = open(os.path.join(os.path.dirname(__file__), "..", "reed-solomon-novelpoly_amd", "csrc",
+                            "kernels_fast.hip")).read()
+    kappa = [int(v) for v in re.search(r"constexpr uint32_t k\[8\] = \{([^}]*)\}", src).group(1).split(",")]
+    rng = np.random.default_rng(8)
+    for K in (8, 16):
+        n = 8 * K
+        for _ in range(5):
+            a = rng.integers(0, 65536, n, dtype=np.uint16)
+            want = oracle.formal_derivative(oracle.inverse_afft(a.copy(), n, 0))[:K]
+            xs = [oracle.inverse_afft(a[q * K:(q + 1) * K].copy(), K, q * K) for q in range(8)]
+            d = oracle.formal_derivative(xs[0].copy()).astype(np.uint16)
+            for q in range(8):
+                m = oracle.log_table()[kappa[q]]  # mul by the element kappa_q: log form
+                d ^= np.array([oracle.mul(int(x), int(m)) for x in xs[q]], dtype=np.uint16)
+            assert np.array_equal(d, want)
