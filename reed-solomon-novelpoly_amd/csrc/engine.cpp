@@ -159,7 +159,7 @@ np::EncodeArgs enc_args(const np_code_params* p, const uint8_t* payloads, size_t
   return a;
 }
 
-constexpr size_t kBigScratchCap = size_t(1) << 30;  // bytes of k = 1024 scratch per context
+constexpr size_t kBigScratchCap = size_t(1) << 30;  // bytes of big-kernel scratch per context
 
 // Big-kernel scratch of `want` bytes (capped), ordered after every earlier
 // big launch of this context on any stream.  Caller holds the context lock.
@@ -183,7 +183,7 @@ hipError_t big_done(np_ctx* c, hipStream_t s, hipError_t e) {
   return hipEventRecord(c->big_done, s);
 }
 
-// Scratch slots of a k = 1024 launch over `tiles` tiles: one per resident workgroup.
+// Scratch slots of a k = 512 / 1024 launch over `tiles` tiles: one per resident workgroup.
 size_t big_slots(const np_ctx* c, size_t tiles) {
   return std::min((tiles + 7) / 8 * 8, np::big_resident_slots(c->device));
 }
@@ -195,7 +195,7 @@ hipError_t launch_encode(np_ctx* c, const np::EncodeArgs& a, hipStream_t s) {
     const size_t tiles = ((a.payload_len + 2 * a.k - 1) / (2 * a.k) + 255) / 256;
     uint8_t* scr = nullptr;
     size_t bytes = 0;
-    hipError_t e = big_scratch(c, big_slots(c, a.batch * tiles) * np::big_encode_scratch_per_tile(), s, &scr, &bytes);
+    hipError_t e = big_scratch(c, big_slots(c, a.batch * tiles) * np::big_encode_scratch_per_tile(a.k), s, &scr, &bytes);
     if (e == hipSuccess) e = np::launch_encode_big(c->T, a, scr, bytes, s);
     return big_done(c, s, e);
   }
@@ -245,7 +245,7 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
   }
   if (np::big_reconstruct_supported(a.n, a.k)) {
     const size_t tiles = (a.shard_len / 2 + 255) / 256;
-    const size_t per_tile = np::big_reconstruct_scratch_per_tile(a.n);
+    const size_t per_tile = np::big_reconstruct_scratch_per_tile(a.n, a.k);
     const size_t status_bytes = (a.batch * own_status + 255) / 256 * 256;
     if (status_bytes + 8 * per_tile > kBigScratchCap) return hipErrorInvalidValue;  // > 13M payloads
     uint8_t* scr = nullptr;

@@ -1,13 +1,14 @@
-// Specialised gfx950 kernels for k = 1024 (BASELINE config 4: n = 4096).
+// Specialised gfx950 kernels for k = 512 and k = 1024 (BASELINE config 4:
+// n = 4096, k = 1024; 1,366-2,730 validators: k = 512).
 //
-// A 256-column tile of a size-1024 transform needs 512 KiB, more than the LDS
+// A 256-column tile of a size-KB transform needs KB/2 KiB, more than the LDS
 // holds, so a workgroup (1024 threads, the K = 256 register layouts of
-// fast_common.hpp) runs the transform as four size-256 sub-segments plus the
-// two top levels (8, 9) that mix them:
+// fast_common.hpp) runs the transform as SUBS = KB / 256 size-256 sub-segments
+// plus the top levels (8, and 9 for KB = 1024) that mix them:
 //
 //   phase 1  per sub-segment: LDS tile -> column-quad levels 0..3 -> high-layout
 //            levels 4..7 -> registers -> per-workgroup scratch in HBM / L2;
-//   phase 2  per position quad, across the sub-segments: levels 8, 9 (and for
+//   phase 2  per position quad, across the sub-segments: the top levels (and for
 //            reconstruct the segment combination, formal derivative and the
 //            forward transform's top levels) -> scratch;
 //   phase 3  per sub-segment: scratch -> high-layout levels 7..4 -> LDS ->
@@ -15,7 +16,7 @@
 //
 // Scratch traffic stays in the workgroup (each thread reads back what it
 // wrote), so no inter-workgroup synchronisation is needed.  The top-level
-// skews of a size-1024 transform at index I are Cantor((I >> 9) + 2t) for
+// skews of a size-KB transform at index I are Cantor((I >> 9) + 2t) for
 // level 9 and Cantor((I >> 8) + 2t) for level 8 (fast_common.hpp, skew_c).
 //
 // Reference: inc_afft.rs:139-214 / :267-332, inc_encode.rs:15-48,
@@ -29,7 +30,6 @@ namespace np {
 namespace {
 
 constexpr int kS = 256;                   // sub-segment (register-layout) size
-constexpr int kKB = 1024;                 // k served here
 constexpr int kTB = Geo<kS>::kThreads;    // 1024 threads
 constexpr size_t kSegScr = 16u * kTB * 8; // one sub-segment of a tile in thread order: 128 KiB
 
@@ -47,8 +47,8 @@ __device__ __forceinline__ const uint64_t* scr_at(const uint8_t* seg, uint32_t j
 }
 
 template <bool NT>
-__device__ __forceinline__ void scr_q_store(uint8_t* seg, uint32_t j, uint32_t tid, uint32_t l, uint32_t h) {
-  const uint64_t v = static_cast<uint64_t>(l) | (static_cast<uint64_t>(h) << 32);
+__device__ __forceinline__ void scr_q_store(uint8_t* seg, uint32_t j, uint32_t tid, const uint2& x) {
+  const uint64_t v = static_cast<uint64_t>(x.x) | (static_cast<uint64_t>(x.y) << 32);
   if constexpr (NT)
     __builtin_nontemporal_store(v, scr_at(seg, j, tid));
   else
@@ -68,7 +68,7 @@ template <bool NT>
 __device__ __forceinline__ void scr_store(uint8_t* seg, uint32_t tid, const uint32_t (&L)[16],
                                           const uint32_t (&H)[16]) {
 #pragma unroll
-  for (int j = 0; j < 16; ++j) scr_q_store<NT>(seg, j, tid, L[j], H[j]);
+  for (int j = 0; j < 16; ++j) scr_q_store<NT>(seg, j, tid, make_uint2(L[j], H[j]));
 }
 
 template <bool NT>
@@ -94,17 +94,65 @@ __device__ __forceinline__ void qx(uint2& x, const uint2& y) {
   x.y ^= y.y;
 }
 
+// Top inverse levels of a size-(256 SUBS) transform at index 256 SUBS q, on one
+// position quad of each sub-segment: level 8 (groups t, skew Cantor(q SUBS + 2t)),
+// then level 9 (SUBS = 4, skew Cantor(2q)); inverse butterfly hi ^= lo; lo ^= c hi.
+// q is a compile-time constant at every call, so the zero skews of q = 0 fold.
+template <int SUBS>
+__device__ __forceinline__ void top_inverse(const DevTables& T, uint2 (&y)[SUBS], uint32_t q) {
+#pragma unroll
+  for (int t = 0; t < SUBS / 2; ++t) {
+    qx(y[2 * t + 1], y[2 * t]);
+    const uint32_t c = q * SUBS + 2u * t;
+    if (c) qm(y[2 * t], y[2 * t + 1], mult_of(T, c));
+  }
+  if constexpr (SUBS == 4) {
+    qx(y[2], y[0]);
+    qx(y[3], y[1]);
+    if (q) {
+      const Mult m9 = mult_of(T, 2u * q);
+      qm(y[0], y[2], m9);
+      qm(y[1], y[3], m9);
+    }
+  }
+}
+
+// Top forward levels at index 256 SUBS c (level 9, then 8): lo ^= c hi; hi ^= lo.
+template <int SUBS>
+__device__ __forceinline__ void top_forward(const DevTables& T, uint2 (&w)[SUBS], uint32_t c) {
+  if constexpr (SUBS == 4) {
+    if (c) {
+      const Mult m9 = mult_of(T, 2u * c);
+      qm(w[0], w[2], m9);
+      qm(w[1], w[3], m9);
+    }
+    qx(w[2], w[0]);
+    qx(w[3], w[1]);
+  }
+#pragma unroll
+  for (int t = 0; t < SUBS / 2; ++t) {
+    const uint32_t c8 = c * SUBS + 2u * t;
+    if (c8) qm(w[2 * t], w[2 * t + 1], mult_of(T, c8));
+    qx(w[2 * t + 1], w[2 * t]);
+  }
+}
+
 // ------------------------------------------------------------------ encode ----
 // The shift's top-level outputs W are written once and read once: streaming
 // (-6 % on the encode); the coefficients M keep the default policy.
 #ifndef NP_W_NT
 #define NP_W_NT true
 #endif
-constexpr size_t kEncScratch = 8 * kSegScr;  // M (4 sub-segments) + W (4 sub-segments)
+template <int KB>
+constexpr size_t enc_scratch() {
+  return 2u * (KB / kS) * kSegScr;  // M (SUBS sub-segments) + W (SUBS sub-segments)
+}
 
+template <int KB>
 __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_big(
     DevTables T, EncodeArgs a, uint32_t nchunks, uint32_t tiles, uint32_t tile0, uint8_t* scratch) {
   using G = Geo<kS>;
+  constexpr int SUBS = KB / kS;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
   uint32_t* VP = reinterpret_cast<uint32_t*>(smem + G::kTileBytes);
@@ -115,37 +163,37 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   const uint32_t ncols = min(static_cast<uint32_t>(kTile), nchunks - ch0);
   const uint8_t* pay = a.payloads + static_cast<size_t>(pb) * a.payload_stride;
   uint8_t* out = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(ch0);
-  uint8_t* scrM = scratch + static_cast<size_t>(blockIdx.x) * kEncScratch;
-  uint8_t* scrW = scrM + 4 * kSegScr;
+  uint8_t* scrM = scratch + static_cast<size_t>(blockIdx.x) * enc_scratch<KB>();
+  uint8_t* scrW = scrM + SUBS * kSegScr;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, g = uniform(tid >> 6);
   const bool full =
       ncols == kTile && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
   const uint32_t cqb = col_base<kS>(4 * lane) ^ (32u * g);
   const uint32_t hb = col_base<kS>(tid / G::R) ^ (8u * (tid % G::R));
   const bool fast_in = ((reinterpret_cast<uintptr_t>(pay) & 7u) == 0) &&
-                       static_cast<size_t>(ch0 + kTile) * 2 * kKB <= a.payload_len;
+                       static_cast<size_t>(ch0 + kTile) * 2 * KB <= a.payload_len;
 
-  // ---- phase 1: x_s = IFFT(256, 256 s)(sub-segment s of every chunk), s = 0..3
+  // ---- phase 1: x_s = IFFT(256, 256 s)(sub-segment s of every chunk)
 #pragma unroll 1
-  for (uint32_t s = 0; s < 4; ++s) {
+  for (uint32_t s = 0; s < SUBS; ++s) {
     const uint32_t index = 256u * s;
     __syncthreads();  // previous sub-segment is done with the tile and the tables
     stage_vpools<kS, kTB>(T, index, VP);
     {
       const uint32_t c0 = tid / G::Q, m0 = tid % G::Q;
       const uint32_t base = col_base<kS>(c0) ^ (8u * m0);
-      const size_t gbase = static_cast<size_t>(ch0 + c0) * 2 * kKB + 2u * index + 8u * m0;
+      const size_t gbase = static_cast<size_t>(ch0 + c0) * 2 * KB + 2u * index + 8u * m0;
       if (fast_in) {
         uint2 v[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i)
-          v[i] = load_once(pay + gbase + static_cast<size_t>(i) * 16 * 2 * kKB);
+          v[i] = load_once(pay + gbase + static_cast<size_t>(i) * 16 * 2 * KB);
 #pragma unroll
         for (int i = 0; i < 16; ++i) *reinterpret_cast<uint2*>(tile + (base ^ col_base_c<kS>(16u * i))) = v[i];
       } else {
 #pragma unroll 1
         for (uint32_t i = 0; i < 16; ++i) {
-          const size_t g0 = gbase + static_cast<size_t>(i) * 16 * 2 * kKB;
+          const size_t g0 = gbase + static_cast<size_t>(i) * 16 * 2 * KB;
           uint32_t w[2] = {0, 0};
 #pragma unroll
           for (int e = 0; e < 8; ++e)
@@ -170,52 +218,35 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
     scr_store<false>(scrM + s * kSegScr, tid, XL, XH);
   }
 
-  // ---- phase 2: top inverse levels at index 0 -> coefficients M (in place)
-  {
-    const Mult beta = mult_of(T, 2u);  // level 8, t = 1; the t = 0 skews at index 0 are zero
+  // ---- phase 2: top inverse levels at index 0 -> coefficients M (in place;
+  // sub-segment 0 is unchanged: every level-8/9 butterfly at index 0 keeps lo)
 #pragma unroll 1
-    for (uint32_t j = 0; j < 16; ++j) {
-      uint2 x0 = scr_q<false>(scrM, j, tid), x1 = scr_q<false>(scrM + kSegScr, j, tid);
-      uint2 x2 = scr_q<false>(scrM + 2 * kSegScr, j, tid), x3 = scr_q<false>(scrM + 3 * kSegScr, j, tid);
-      qx(x1, x0);     // level 8, t = 0: hi ^= lo
-      qx(x3, x2);     // level 8, t = 1
-      qm(x2, x3, beta);
-      qx(x2, x0);     // level 9, t = 0
-      qx(x3, x1);
-      scr_q_store<false>(scrM + kSegScr, j, tid, x1.x, x1.y);
-      scr_q_store<false>(scrM + 2 * kSegScr, j, tid, x2.x, x2.y);
-      scr_q_store<false>(scrM + 3 * kSegScr, j, tid, x3.x, x3.y);
-    }
+  for (uint32_t j = 0; j < 16; ++j) {
+    uint2 x[SUBS];
+#pragma unroll
+    for (int s = 0; s < SUBS; ++s) x[s] = scr_q<false>(scrM + s * kSegScr, j, tid);
+    top_inverse<SUBS>(T, x, 0u);
+#pragma unroll
+    for (int s = 1; s < SUBS; ++s) scr_q_store<false>(scrM + s * kSegScr, j, tid, x[s]);
   }
 
-  // ---- phase 3: every shift c = 1.. : top forward levels, then 4 x FFT(256)
-  const uint32_t nshift = a.n / kKB;
+  // ---- phase 3: every shift c = 1.. : top forward levels, then SUBS x FFT(256)
+  const uint32_t nshift = a.n / KB;
 #pragma unroll 1
   for (uint32_t c = 1; c < nshift; ++c) {
-    if (c * kKB >= a.wanted_n) break;
-    {
-      const Mult m9 = mult_of(T, 2u * c), m80 = mult_of(T, 4u * c), m81 = mult_of(T, 4u * c + 2u);
+    if (c * KB >= a.wanted_n) break;
 #pragma unroll 1
-      for (uint32_t j = 0; j < 16; ++j) {
-        uint2 w0 = scr_q<false>(scrM, j, tid), w1 = scr_q<false>(scrM + kSegScr, j, tid);
-        uint2 w2 = scr_q<false>(scrM + 2 * kSegScr, j, tid), w3 = scr_q<false>(scrM + 3 * kSegScr, j, tid);
-        qm(w0, w2, m9);  // level 9: lo ^= c9 * hi; hi ^= lo
-        qx(w2, w0);
-        qm(w1, w3, m9);
-        qx(w3, w1);
-        qm(w0, w1, m80);  // level 8, t = 0
-        qx(w1, w0);
-        qm(w2, w3, m81);  // level 8, t = 1
-        qx(w3, w2);
-        scr_q_store<NP_W_NT>(scrW, j, tid, w0.x, w0.y);
-        scr_q_store<NP_W_NT>(scrW + kSegScr, j, tid, w1.x, w1.y);
-        scr_q_store<NP_W_NT>(scrW + 2 * kSegScr, j, tid, w2.x, w2.y);
-        scr_q_store<NP_W_NT>(scrW + 3 * kSegScr, j, tid, w3.x, w3.y);
-      }
+    for (uint32_t j = 0; j < 16; ++j) {
+      uint2 w[SUBS];
+#pragma unroll
+      for (int s = 0; s < SUBS; ++s) w[s] = scr_q<false>(scrM + s * kSegScr, j, tid);
+      top_forward<SUBS>(T, w, c);
+#pragma unroll
+      for (int s = 0; s < SUBS; ++s) scr_q_store<NP_W_NT>(scrW + s * kSegScr, j, tid, w[s]);
     }
 #pragma unroll 1
-    for (uint32_t s = 0; s < 4; ++s) {
-      const uint32_t index = c * kKB + 256u * s;
+    for (uint32_t s = 0; s < SUBS; ++s) {
+      const uint32_t index = c * KB + 256u * s;
       if (index >= a.wanted_n) break;
       __syncthreads();  // the tile and the tables are free
       stage_vpools<kS, kTB>(T, index, VP);
@@ -233,18 +264,45 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
 }
 
 // ------------------------------------------------------------- reconstruct ----
-// n = NQ * 1024.  As in k_reconstruct_fast (kernels_fast.hip), for the first
-// k = 1024 outputs d = D_1024(x0) ^ x1 ^ x2 ^ beta (x2 ^ x3) (NQ = 4) or
-// D_1024(x0) ^ x0 ^ x1 (NQ = 2) with x_q = IFFT(1024, 1024 q)(premultiplied
-// segment q), then out = FFT(1024, 0)(d).  Here each x_q is 4 sub-segment
-// transforms y_qs = IFFT(256, 1024 q + 256 s) plus levels 8, 9, and
-// D_1024 = (I (x) D_256) + (high single-bit terms l = 256, 512); the D_256 part
-// commutes with levels 8, 9, so it is applied to y_0s in phase 1.
+// n = NQ * KB.  As in k_reconstruct_fast (kernels_fast.hip), the first KB
+// outputs are out = FFT(KB, 0)(d) with
+//   d = D_KB(x0) ^ sum_q kappa_q x_q,  x_q = IFFT(KB, KB q)(premultiplied segment q)
+// (kappa: NQ = 2 (1, 1); NQ = 4 (0, 1, 3, 2); NQ = 8 rec8_kappa; Cantor
+// coordinates, all in GF(16)).  The sum is formed per Cantor bit b of kappa,
+// S_b = XOR of the x_q with bit b set, d ^= S_0 ^ sum_b Cantor(2^b) S_b: one
+// multiply per bit rather than per segment.  Each x_q is SUBS sub-segment
+// transforms y_qs = IFFT(256, KB q + 256 s) plus the top levels, and
+// D_KB = (I (x) D_256) + (high single-bit terms l = 256, 512 < KB); the D_256
+// part commutes with the top levels, so it is applied to y_0s in phase 1.
 template <int NQ>
+__host__ __device__ constexpr uint32_t big_kappa(int q) {
+  if constexpr (NQ == 2) {
+    return 1u;
+  } else if constexpr (NQ == 4) {
+    constexpr uint32_t k[4] = {0, 1, 3, 2};
+    return k[q];
+  } else {
+    constexpr uint32_t k[8] = {1, 1, 3, 2, 12, 15, 10, 8};  // kernels_fast.hip rec8_kappa
+    return k[q];
+  }
+}
+template <int... Q, typename F>
+__device__ __forceinline__ void for_each_q(std::integer_sequence<int, Q...>, F&& f) {
+  (f(Int<Q>{}), ...);
+}
+template <int NQ>
+__host__ __device__ constexpr bool kappa_bit_used(int b) {
+  for (int q = 0; q < NQ; ++q)
+    if ((big_kappa<NQ>(q) >> b) & 1u) return true;
+  return false;
+}
+
+template <int KB, int NQ>
 __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k_reconstruct_big(
     DevTables T, ReconstructArgs a, uint32_t nsyms, uint32_t tiles, uint32_t tile0, uint8_t* scratch) {
   using G = Geo<kS>;
-  constexpr int N = NQ * kKB;
+  constexpr int SUBS = KB / kS;
+  constexpr int N = NQ * KB;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
   uint32_t* VP = reinterpret_cast<uint32_t*>(smem + G::kTileBytes);
@@ -259,8 +317,9 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);
   const uint8_t* pres = a.present + static_cast<size_t>(pb) * N;
   const uint16_t* loc = a.locators ? a.locators + static_cast<size_t>(pb) * N : nullptr;
-  uint8_t* scrY = scratch + static_cast<size_t>(blockIdx.x) * (4 * NQ + 4) * kSegScr;  // y_qs, then D_256(y_0s)
-  uint8_t* scrD = scrY + 4 * NQ * kSegScr;                                               // reused for e_s
+  // y_qs (SUBS NQ slots), then D_256(y_0s) (SUBS slots, reused for e_s)
+  uint8_t* scrY = scratch + static_cast<size_t>(blockIdx.x) * (SUBS * NQ + SUBS) * kSegScr;
+  uint8_t* scrD = scrY + SUBS * NQ * kSegScr;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, g = uniform(tid >> 6);
   const bool full =
       ncols == kTile && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
@@ -279,8 +338,8 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   // ---- phase 1: y_qs for every segment q and sub-segment s
   __syncthreads();  // E, PR ready
 #pragma unroll 1
-  for (uint32_t qs = 0; qs < 4u * NQ; ++qs) {
-    const uint32_t index = 256u * qs;  // = 1024 q + 256 s
+  for (uint32_t qs = 0; qs < static_cast<uint32_t>(SUBS * NQ); ++qs) {
+    const uint32_t index = 256u * qs;  // = KB q + 256 s
     const uint32_t gg = fresh(g);
     // the sub-segment's present rows load while the tables are staged
     uint2 rows[2][8];
@@ -316,7 +375,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
     hi_read<kS>(tile, fresh_v(hb), XL, XH);
     hi_levels<kS, true, false>(T, VP, index, XL, XH);
     scr_store<true>(scrY + qs * kSegScr, tid, XL, XH);
-    if (qs < 4) {  // segment 0: also D_256(y_0s)
+    if (qs < static_cast<uint32_t>(SUBS)) {  // segment 0: also D_256(y_0s)
       uint32_t DL[16] = {0}, DH[16] = {0};
       add_derivative<kS>(DL, XL, tid % G::R);
       add_derivative<kS>(DH, XH, tid % G::R);
@@ -324,98 +383,76 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
     }
   }
 
-  // ---- phase 2: levels 8, 9 of every x_q, the combination, the derivative's
-  // high terms and the forward transform's levels 9, 8 -> e_s (over D's slots)
-  {
-    const Mult beta = mult_of(T, 2u);
+  // ---- phase 2: top levels of every x_q, the combination, the derivative's
+  // high terms and the forward transform's top levels at index 0 -> e_s (over
+  // D's slots)
 #pragma unroll 1
-    for (uint32_t j = 0; j < 16; ++j) {
-      uint2 d[4], x0[4];
-      // x_0 and D_256 lifted: level 8 (t = 0 skew 0, t = 1 beta), level 9 (skew 0)
-      {
-        uint2 y[4], z[4];
+  for (uint32_t j = 0; j < 16; ++j) {
+    uint2 d[SUBS], x0[SUBS];
+    {
+      uint2 z[SUBS];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          y[s] = scr_q<true>(scrY + s * kSegScr, j, tid);
-          z[s] = scr_q<true>(scrD + s * kSegScr, j, tid);
-        }
-        qx(y[1], y[0]);
-        qx(y[3], y[2]);
-        qm(y[2], y[3], beta);
-        qx(y[2], y[0]);
-        qx(y[3], y[1]);
-        qx(z[1], z[0]);
-        qx(z[3], z[2]);
-        qm(z[2], z[3], beta);
-        qx(z[2], z[0]);
-        qx(z[3], z[1]);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) x0[s] = y[s];
-        // D_1024(x0)_s = (lifted D_256)_s ^ x0_{s|1} (s even) ^ x0_{s|2} (s < 2)
-        d[0] = z[0];
-        qx(d[0], x0[1]);
-        qx(d[0], x0[2]);
-        d[1] = z[1];
-        qx(d[1], x0[3]);
-        d[2] = z[2];
-        qx(d[2], x0[3]);
-        d[3] = z[3];
-        if (NQ == 2) {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) qx(d[s], x0[s]);
-        }
+      for (int s = 0; s < SUBS; ++s) {
+        x0[s] = scr_q<true>(scrY + s * kSegScr, j, tid);
+        z[s] = scr_q<true>(scrD + s * kSegScr, j, tid);
       }
-      uint2 yq[NQ - 1][4];  // every segment's quads in flight at once (one latency per j)
+      top_inverse<SUBS>(T, x0, 0u);
+      top_inverse<SUBS>(T, z, 0u);  // D_256 lifted
+      // D_KB(x0)_s = (lifted D_256)_s ^ x0_{s | 2^m} for each high bit 256 2^m < KB clear in s
 #pragma unroll
-      for (int q = 1; q < NQ; ++q)
+      for (int s = 0; s < SUBS; ++s) {
+        d[s] = z[s];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) yq[q - 1][s] = scr_q<true>(scrY + (4 * q + s) * kSegScr, j, tid);
-#pragma unroll
-      for (uint32_t q = 1; q < static_cast<uint32_t>(NQ); ++q) {
-        uint2 (&y)[4] = yq[q - 1];
-        // levels 8 (t = 0: Cantor(4q), t = 1: Cantor(4q + 2)) and 9 (Cantor(2q)): hi ^= lo; lo ^= c hi
-        {
-          const Mult m80 = mult_of(T, 4u * q), m81 = mult_of(T, 4u * q + 2u);
-          qx(y[1], y[0]);
-          qm(y[0], y[1], m80);
-          qx(y[3], y[2]);
-          qm(y[2], y[3], m81);
-        }
-        {
-          const Mult m9 = mult_of(T, 2u * q);
-          qx(y[2], y[0]);
-          qm(y[0], y[2], m9);
-          qx(y[3], y[1]);
-          qm(y[1], y[3], m9);
-        }
-        if (NQ == 2 || q == 1) {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) qx(d[s], y[s]);  // ^ x1 (and for NQ = 4: x1)
-        } else if (q == 2) {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) qx(d[s], y[s]);  // ^ x2 (kept in yq[1] for q = 3)
-        } else {  // q == 3: ^ beta (x2 ^ x3)
-#pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            qx(y[s], yq[1][s]);
-            qm(d[s], y[s], beta);
-          }
-        }
+        for (int m = 1; m < SUBS; m <<= 1)
+          if (!(s & m)) qx(d[s], x0[s | m]);
       }
-      // forward levels 9 (t = 0: skew 0) and 8 (t = 0: 0, t = 1: beta) at index 0
-      qx(d[2], d[0]);
-      qx(d[3], d[1]);
-      qx(d[1], d[0]);
-      qm(d[2], d[3], beta);
-      qx(d[3], d[2]);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) scr_q_store<true>(scrD + s * kSegScr, j, tid, d[s].x, d[s].y);
     }
+    uint2 acc[4][SUBS];  // S_b, per Cantor bit b of kappa
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int s = 0; s < SUBS; ++s) acc[b][s] = make_uint2(0u, 0u);
+    uint2 yq[NQ - 1][SUBS];  // every segment's quads in flight at once (one latency per j)
+#pragma unroll
+    for (int q = 1; q < NQ; ++q)
+#pragma unroll
+      for (int s = 0; s < SUBS; ++s) yq[q - 1][s] = scr_q<true>(scrY + (SUBS * q + s) * kSegScr, j, tid);
+    auto accumulate = [&](const uint2 (&y)[SUBS], uint32_t kq) __attribute__((always_inline)) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        if ((kq >> b) & 1u)
+#pragma unroll
+          for (int s = 0; s < SUBS; ++s) qx(acc[b][s], y[s]);
+    };
+    for_each_q(std::make_integer_sequence<int, NQ>{}, [&](auto qc) __attribute__((always_inline)) {
+      constexpr int q = decltype(qc)::value;
+      constexpr uint32_t kq = big_kappa<NQ>(q);
+      if constexpr (kq != 0) {
+        if constexpr (q == 0) {
+          accumulate(x0, kq);
+        } else {
+          top_inverse<SUBS>(T, yq[q - 1], static_cast<uint32_t>(q));
+          accumulate(yq[q - 1], kq);
+        }
+      }
+    });
+#pragma unroll
+    for (int s = 0; s < SUBS; ++s) qx(d[s], acc[0][s]);
+#pragma unroll
+    for (int b = 1; b < 4; ++b) {
+      if (!kappa_bit_used<NQ>(b)) continue;
+      const Mult m = mult_of(T, 1u << b);
+#pragma unroll
+      for (int s = 0; s < SUBS; ++s) qm(d[s], acc[b][s], m);
+    }
+    top_forward<SUBS>(T, d, 0u);
+#pragma unroll
+    for (int s = 0; s < SUBS; ++s) scr_q_store<true>(scrD + s * kSegScr, j, tid, d[s]);
   }
 
   // ---- phase 3: FFT(256, 256 s) of e_s, postmultiply erased rows, copy out
 #pragma unroll 1
-  for (uint32_t s = 0; s < 4; ++s) {
+  for (uint32_t s = 0; s < SUBS; ++s) {
     const uint32_t index = 256u * s;
     __syncthreads();
     stage_vpools<kS, kTB>(T, index, VP);
@@ -450,8 +487,8 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       cq_write<kS>(tile, cq, XL, XH);
     }
     __syncthreads();
-    {  // output column c, symbols 256 s .. 256 s + 255: bytes [2048 c + 512 s, +512)
-      uint8_t* outp = a.out + static_cast<size_t>(pb) * a.out_stride + static_cast<size_t>(col0) * 2 * kKB + 512u * s;
+    {  // output column c, symbols 256 s .. 256 s + 255: bytes [2 KB c + 512 s, +512)
+      uint8_t* outp = a.out + static_cast<size_t>(pb) * a.out_stride + static_cast<size_t>(col0) * 2 * KB + 512u * s;
       const bool al_o = ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 7u) == 0;
       const uint32_t c0 = tid / G::Q, m0 = tid % G::Q;
       const uint32_t base = col_base<kS>(c0) ^ (8u * m0);
@@ -460,7 +497,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
         const uint32_t c = c0 + 16u * i;
         if (c >= ncols) break;
         const uint2 v = *reinterpret_cast<const uint2*>(tile + (base ^ col_base_c<kS>(16u * i)));
-        uint8_t* o = outp + static_cast<size_t>(c) * 2 * kKB + 8u * m0;
+        uint8_t* o = outp + static_cast<size_t>(c) * 2 * KB + 8u * m0;
         if (al_o) {
           store_once(o, v);
         } else {
@@ -473,22 +510,39 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
 }
 
 size_t enc_big_lds() { return static_cast<size_t>(Geo<kS>::kTileBytes) + 4u * Geo<kS>::kVPWords; }
-template <int NQ>
-size_t rec_big_lds() {
-  return static_cast<size_t>(Geo<kS>::kTileBytes) + 4u * Geo<kS>::kVPWords + 3u * NQ * kKB;
+size_t rec_big_lds(uint32_t n) {  // tile, tables, E (2 n bytes), PR (n bytes)
+  return static_cast<size_t>(Geo<kS>::kTileBytes) + 4u * Geo<kS>::kVPWords + 3u * n;
+}
+
+// Calls f(kernel pointer) for the reconstruct instance of (n, k); false if none.
+template <typename F>
+bool with_rec_big(uint32_t n, uint32_t k, F&& f) {
+  if (k == 512) {
+    if (n == 1024) return f(&k_reconstruct_big<512, 2>), true;
+    if (n == 2048) return f(&k_reconstruct_big<512, 4>), true;
+    if (n == 4096) return f(&k_reconstruct_big<512, 8>), true;
+  } else if (k == 1024) {
+    if (n == 2048) return f(&k_reconstruct_big<1024, 2>), true;
+    if (n == 4096) return f(&k_reconstruct_big<1024, 4>), true;
+    if (n == 8192) return f(&k_reconstruct_big<1024, 8>), true;
+  }
+  return false;
 }
 
 }  // namespace
 
-bool big_encode_supported(uint32_t n, uint32_t k) { return k == kKB && n >= 2 * k && n <= 65536; }
+bool big_encode_supported(uint32_t n, uint32_t k) { return (k == 512 || k == 1024) && n >= 2 * k && n <= 65536; }
 bool big_reconstruct_supported(uint32_t n, uint32_t k) {
-  return k == kKB && (n == 2 * k || n == 4 * k);
+  return with_rec_big(n, k, [](auto) {});
 }
-size_t big_encode_scratch_per_tile() { return kEncScratch; }
-size_t big_reconstruct_scratch_per_tile(uint32_t n) { return (4u * (n / kKB) + 4u) * kSegScr; }
+size_t big_encode_scratch_per_tile(uint32_t k) { return k == 512 ? enc_scratch<512>() : enc_scratch<1024>(); }
+size_t big_reconstruct_scratch_per_tile(uint32_t n, uint32_t k) {
+  const uint32_t subs = k / kS;
+  return static_cast<size_t>(subs) * (n / k + 1) * kSegScr;
+}
 
-// Workgroups of the k = 1024 kernels resident on the device at once (one per
-// CU: 1024 threads and ~150 KiB of LDS each), rounded down to a multiple of 8.
+// Workgroups of the big kernels resident on the device at once (one per CU:
+// 1024 threads and 130-160 KiB of LDS each), rounded down to a multiple of 8.
 // Each launch covers at most that many tiles, so a launch is one full round of
 // workgroups on the CUs (no partial last round) and its scratch stays that of
 // the resident workgroups.
@@ -508,8 +562,8 @@ size_t big_resident_slots(int device) {
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
   // the occupancy query runs on the current device: switch to `device` for it
   const bool sw = hipGetDevice(&prev) == hipSuccess && prev != device && hipSetDevice(device) == hipSuccess;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&k_reconstruct_big<4>), kTB,
-                                                   rec_big_lds<4>()) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&k_reconstruct_big<1024, 4>),
+                                                   kTB, rec_big_lds(4096)) != hipSuccess ||
       per <= 0)
     per = 1;
   if (sw) (void)hipSetDevice(prev);
@@ -520,17 +574,23 @@ size_t big_resident_slots(int device) {
 
 hipError_t launch_encode_big(const DevTables& T, const EncodeArgs& a, uint8_t* scratch, size_t scratch_bytes,
                              hipStream_t s) {
+  if (!big_encode_supported(a.n, a.k)) return hipErrorInvalidValue;
   const size_t nchunks = (a.payload_len + 2 * a.k - 1) / (2 * a.k);
   if (nchunks == 0 || a.batch == 0) return hipSuccess;
   const uint32_t tiles = static_cast<uint32_t>((nchunks + kTile - 1) / kTile);
   const size_t total = a.batch * tiles;
   // multiple of 8 keeps tile0 % 8 == 0 (tile_of)
-  const size_t per_launch = std::min(big_resident_slots(current_device()), scratch_bytes / kEncScratch / 8 * 8);
+  const size_t per_tile = big_encode_scratch_per_tile(a.k);
+  const size_t per_launch = std::min(big_resident_slots(current_device()), scratch_bytes / per_tile / 8 * 8);
   if (per_launch == 0 || total > 0xffffffffu) return hipErrorInvalidValue;
   for (size_t t0 = 0; t0 < total; t0 += per_launch) {
     const uint32_t blocks = static_cast<uint32_t>(std::min(per_launch, total - t0));
-    k_encode_big<<<blocks, kTB, enc_big_lds(), s>>>(T, a, static_cast<uint32_t>(nchunks), tiles,
-                                                     static_cast<uint32_t>(t0), scratch);
+    if (a.k == 512)
+      k_encode_big<512><<<blocks, kTB, enc_big_lds(), s>>>(T, a, static_cast<uint32_t>(nchunks), tiles,
+                                                            static_cast<uint32_t>(t0), scratch);
+    else
+      k_encode_big<1024><<<blocks, kTB, enc_big_lds(), s>>>(T, a, static_cast<uint32_t>(nchunks), tiles,
+                                                             static_cast<uint32_t>(t0), scratch);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -539,21 +599,20 @@ hipError_t launch_encode_big(const DevTables& T, const EncodeArgs& a, uint8_t* s
 
 hipError_t launch_reconstruct_big(const DevTables& T, const ReconstructArgs& a, uint8_t* scratch,
                                   size_t scratch_bytes, hipStream_t s) {
+  if (!big_reconstruct_supported(a.n, a.k)) return hipErrorInvalidValue;
   const size_t nsyms = a.shard_len / 2;
   if (nsyms == 0 || a.batch == 0) return hipSuccess;
   const uint32_t tiles = static_cast<uint32_t>((nsyms + kTile - 1) / kTile);
   const size_t total = a.batch * tiles;
-  const size_t per_tile = big_reconstruct_scratch_per_tile(a.n);
+  const size_t per_tile = big_reconstruct_scratch_per_tile(a.n, a.k);
   const size_t per_launch = std::min(big_resident_slots(current_device()), scratch_bytes / per_tile / 8 * 8);
   if (per_launch == 0 || total > 0xffffffffu) return hipErrorInvalidValue;
   for (size_t t0 = 0; t0 < total; t0 += per_launch) {
     const uint32_t blocks = static_cast<uint32_t>(std::min(per_launch, total - t0));
-    if (a.n == 4 * kKB)
-      k_reconstruct_big<4><<<blocks, kTB, rec_big_lds<4>(), s>>>(T, a, static_cast<uint32_t>(nsyms), tiles,
-                                                                 static_cast<uint32_t>(t0), scratch);
-    else
-      k_reconstruct_big<2><<<blocks, kTB, rec_big_lds<2>(), s>>>(T, a, static_cast<uint32_t>(nsyms), tiles,
-                                                                 static_cast<uint32_t>(t0), scratch);
+    with_rec_big(a.n, a.k, [&](auto kern) {
+      kern<<<blocks, kTB, rec_big_lds(a.n), s>>>(T, a, static_cast<uint32_t>(nsyms), tiles, static_cast<uint32_t>(t0),
+                                                 scratch);
+    });
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -566,9 +625,11 @@ hipError_t configure_big_kernels() {
     hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
     if (r != hipSuccess && e == hipSuccess) e = r;
   };
-  set(reinterpret_cast<const void*>(&k_encode_big), enc_big_lds());
-  set(reinterpret_cast<const void*>(&k_reconstruct_big<2>), rec_big_lds<2>());
-  set(reinterpret_cast<const void*>(&k_reconstruct_big<4>), rec_big_lds<4>());
+  set(reinterpret_cast<const void*>(&k_encode_big<512>), enc_big_lds());
+  set(reinterpret_cast<const void*>(&k_encode_big<1024>), enc_big_lds());
+  for (uint32_t k : {512u, 1024u})
+    for (uint32_t nq : {2u, 4u, 8u})
+      with_rec_big(nq * k, k, [&](auto kern) { set(reinterpret_cast<const void*>(kern), rec_big_lds(nq * k)); });
   return e;
 }
 

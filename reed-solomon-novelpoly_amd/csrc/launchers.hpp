@@ -85,12 +85,12 @@ hipError_t launch_reconstruct_fast(const DevTables& T, const ReconstructArgs& a,
 size_t prefix_stride(uint32_t n, uint32_t k);
 hipError_t launch_prefix_locator(const DevTables& T, const ReconstructArgs& a, uint8_t* out, hipStream_t s);
 
-// ---- k = 1024 (kernels_big.hip): per-workgroup scratch, launches split to fit it ----
+// ---- k = 512, 1024 (kernels_big.hip): per-workgroup scratch, launches split to fit it ----
 bool big_encode_supported(uint32_t n, uint32_t k);
-bool big_reconstruct_supported(uint32_t n, uint32_t k);
-size_t big_encode_scratch_per_tile();
+bool big_reconstruct_supported(uint32_t n, uint32_t k);  // n / k in {2, 4, 8}
+size_t big_encode_scratch_per_tile(uint32_t k);
 size_t big_resident_slots(int device);  // scratch slots a launch uses at most (multiple of 8)
-size_t big_reconstruct_scratch_per_tile(uint32_t n);
+size_t big_reconstruct_scratch_per_tile(uint32_t n, uint32_t k);
 hipError_t launch_encode_big(const DevTables& T, const EncodeArgs& a, uint8_t* scratch, size_t scratch_bytes,
                              hipStream_t s);
 hipError_t launch_reconstruct_big(const DevTables& T, const ReconstructArgs& a, uint8_t* scratch,

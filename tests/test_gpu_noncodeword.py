@@ -22,10 +22,12 @@ pytestmark = pytest.mark.gpu
 
 # (n_wanted, k_wanted, shard_len): config 2 (n256 k64), config 3 (n1024 k256),
 # config 4 (n4096 k1024), n/k = 8 (n512 k64, n1024 k128, n2048 k256), n/k = 2
-# (n1024 k256 with wanted_n 600; n2048 k1024); shard lengths of one full
-# 256-column tile plus a partial one
+# (n1024 k256 with wanted_n 600; n2048 k1024), k = 512 (n1024, n2048, n4096)
+# and n/k = 8 at k = 1024 (n8192); shard lengths of one full 256-column tile
+# plus a partial one
 SHAPES = [(256, 86, 2 * 300), (1024, 342, 2 * 300), (4096, 1366, 2 * 260), (300, 100, 2 * 270),
-          (700, 234, 2 * 300), (1200, 400, 2 * 290), (600, 256, 2 * 280), (2048, 1024, 2 * 270)]
+          (700, 234, 2 * 300), (1200, 400, 2 * 290), (600, 256, 2 * 280), (2048, 1024, 2 * 270),
+          (1024, 512, 2 * 270), (2000, 667, 2 * 260), (2500, 834, 2 * 270), (5000, 1667, 2 * 260)]
 
 
 def _dev(a):

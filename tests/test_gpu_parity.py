@@ -299,10 +299,14 @@ def test_big_path_launch_rounds(gpu, oracle, batch, plen):
                                         (1024, 342, 512 * 512 + 77), (300, 100, 77777), (512, 128, 256 * 600),
                                         (600, 256, 512 * 300), (2048, 300, 512 * 260),
                                         (4096, 1366, 2048 * 256), (4096, 1366, 2048 * 300 + 3),
-                                        (2048, 1024, 2048 * 100), (3000, 1024, 5000)])
+                                        (2048, 1024, 2048 * 100), (3000, 1024, 5000),
+                                        (1024, 512, 1024 * 100 + 3), (2000, 667, 1024 * 256),
+                                        (2000, 667, 1024 * 300 + 5), (2500, 834, 1024 * 256 + 1),
+                                        (5000, 1667, 2048 * 64 + 1), (1500, 512, 999)])
 def test_fast_encode_shapes(gpu, oracle, nw, kw, plen):
-    """Specialised encode kernel (k in {64,128,256}): single/multi/partial tiles,
-    odd payload tails, wanted_n < n and n/k in {2,4,8}."""
+    """Specialised encode kernels (k in {64,128,256}; k in {512,1024} in
+    kernels_big.hip): single/multi/partial tiles, odd payload tails, wanted_n < n
+    and n/k in {2,4,8}."""
     p = npa.CodeParams.derive_parameters(nw, kw)
     assert p.is_faster8()
     pl = synth.payload(nw + plen, plen)
@@ -323,14 +327,19 @@ def test_fast_encode_shapes(gpu, oracle, nw, kw, plen):
                                               (4096, 1366, 2048 * 256, -1), (3000, 1024, 7777, 1000),
                                               (300, 100, 128 * 256, 200), (300, 100, 128 * 300 + 7, -1),
                                               (700, 234, 256 * 256 + 1, 500), (1200, 400, 512 * 256, 900),
-                                              (1200, 400, 512 * 257, -1), (512, 64, 128 * 64, 448)])
+                                              (1200, 400, 512 * 257, -1), (512, 64, 128 * 64, 448),
+                                              (1024, 512, 1024 * 100, 512), (2000, 667, 1024 * 256, 1333),
+                                              (2000, 667, 1024 * 257 + 9, -1), (2500, 834, 1024 * 260 + 1, 1666),
+                                              (2500, 834, 1024 * 256, -1), (5000, 1667, 2048 * 40 + 3, 3333),
+                                              (5000, 1667, 2048 * 33, -1)])
 def test_fast_reconstruct_shapes(gpu, oracle, nw, kw, plen, erase):
-    """Specialised reconstruct kernel (k in {64,128,256}, n in {2k,4k,8k}): full
+    """Specialised reconstruct kernels (k in {64,128,256} fast, {512,1024} big;
+    n in {2k,4k,8k}): full
     and partial column tiles, random and worst-case erasure sets (erase = -1:
     every systematic shard lost), bit-exact against the oracle."""
     p = npa.CodeParams.derive_parameters(nw, kw)
     n, k = p.n(), p.k()
-    assert n in (2 * k, 4 * k, 8 * k) and k in (64, 128, 256, 1024)
+    assert n in (2 * k, 4 * k, 8 * k) and k in (64, 128, 256, 512, 1024)
     pl = synth.payload(7 * nw + plen, plen)
     shards = p.make_encoder(gpu).encode(pl)
     if erase == -1:
