@@ -244,18 +244,27 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
     return hipSuccess;
   }
   if (np::big_reconstruct_supported(a.n, a.k)) {
+    // per-payload records (status, locator as row multipliers) for a slice of
+    // the batch, then the decode over the resident workgroups' tile scratch
     const size_t tiles = (a.shard_len / 2 + 255) / 256;
     const size_t per_tile = np::big_reconstruct_scratch_per_tile(a.n, a.k);
-    const size_t status_bytes = (a.batch * own_status + 255) / 256 * 256;
-    if (status_bytes + 8 * per_tile > kBigScratchCap) return hipErrorInvalidValue;  // > 13M payloads
-    uint8_t* scr = nullptr;
-    size_t bytes = 0;
-    hipError_t e = big_scratch(c, status_bytes + big_slots(c, a.batch * tiles) * per_tile, s, &scr, &bytes);
-    np::ReconstructArgs b = a;
-    if (!a.status) b.status = reinterpret_cast<uint32_t*>(scr);
-    if (e == hipSuccess) e = np::launch_payload_status(b, s);
-    if (e == hipSuccess) e = np::launch_reconstruct_big(c->T, b, scr + status_bytes, bytes - status_bytes, s);
-    return big_done(c, s, e);
+    const size_t rstride = np::big_record_stride(a.n) + own_status;
+    const size_t per = std::max<size_t>(1, kBigScratchCap / 4 / rstride);
+    for (size_t b0 = 0; b0 < a.batch; b0 += per) {
+      np::ReconstructArgs sub = slice(a, b0, std::min(per, a.batch - b0));
+      const size_t rec_bytes = (sub.batch * rstride + 255) / 256 * 256;
+      uint8_t* scr = nullptr;
+      size_t bytes = 0;
+      hipError_t e = big_scratch(c, rec_bytes + big_slots(c, sub.batch * tiles) * per_tile, s, &scr, &bytes);
+      if (e == hipSuccess && bytes < rec_bytes + 8 * per_tile) e = hipErrorInvalidValue;
+      if (!a.status) sub.status = reinterpret_cast<uint32_t*>(scr + sub.batch * np::big_record_stride(a.n));
+      sub.prefix = scr;
+      if (e == hipSuccess) e = np::launch_big_records(c->T, sub, scr, s);
+      if (e == hipSuccess) e = np::launch_reconstruct_big(c->T, sub, scr + rec_bytes, bytes - rec_bytes, s);
+      e = big_done(c, s, e);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
   }
   // generic path: the status, and the locators unless the caller gave them,
   // into the ordered context scratch

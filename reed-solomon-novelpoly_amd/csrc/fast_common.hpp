@@ -771,24 +771,26 @@ __host__ __device__ constexpr uint32_t gen_of(uint32_t index) {
 // branch over compile-time instances; the caller guarantees G >= MING);
 // beyond MAXG f(Int<-1>) (Cantor coordinates, the caller converts) when
 // FALLBACK, else f(Int<MAXG>) (the caller guarantees G <= MAXG).
+template <int G, int MAXG, bool FALLBACK, typename F>
+__device__ __forceinline__ void with_gen_from(uint32_t g, F& f) {
+  if constexpr (G == MAXG) {
+    if constexpr (FALLBACK) {
+      if (g == MAXG) return f(Int<MAXG>{});
+      return f(Int<-1>{});
+    } else {
+      return f(Int<MAXG>{});
+    }
+  } else {
+    if (g == G) return f(Int<G>{});
+    return with_gen_from<G + 1, MAXG, FALLBACK>(g, f);
+  }
+}
+
 template <int MING, int MAXG, bool FALLBACK, typename F>
 __device__ __forceinline__ void with_gen(uint32_t index, F&& f) {
+  static_assert(MING <= MAXG, "gen range");
   const uint32_t g = __builtin_amdgcn_readfirstlane(gen_of(index));
-  if constexpr (MING <= 0 && MAXG >= 1) {
-    if (g == 0) return f(Int<0>{});
-  }
-  if constexpr (MING <= 1 && MAXG >= 2) {
-    if (g == 1) return f(Int<1>{});
-  }
-  if constexpr (MING <= 2 && MAXG >= 3) {
-    if (g == 2) return f(Int<2>{});
-  }
-  if constexpr (FALLBACK) {
-    if (g == MAXG) return f(Int<MAXG>{});
-    return f(Int<-1>{});
-  } else {
-    return f(Int<MAXG>{});
-  }
+  with_gen_from<(MING > 0 ? MING : 0), MAXG, FALLBACK>(g, f);
 }
 
 // GEN: coordinates and subfield levels (kSubLevel).

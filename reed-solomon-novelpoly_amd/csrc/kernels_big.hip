@@ -81,14 +81,17 @@ __device__ __forceinline__ void scr_load(const uint8_t* seg, uint32_t tid, uint3
   }
 }
 
-__device__ __forceinline__ Mult mult_of(const DevTables& T, uint32_t c) {
+// Multiplier of a skew or segment coefficient c < 256 (Cantor index): every
+// one the big kernels use outside the sub-segment transforms lies in GF(2^8),
+// so it is a subfield multiply in tower coordinates (tower_pools, qmul_sub).
+__device__ __forceinline__ Mult tmult(const DevTables& T, uint32_t c) {
   uint32_t p[20];
-  pool_of(T, c, p);
+  pool_of<true>(T, c, p);
   return make_mult(p);
 }
 
-// x ^= c * y for one (L, H) quad pair.
-__device__ __forceinline__ void qm(uint2& x, const uint2& y, const Mult& m) { qmul(x.x, x.y, y.x, y.y, m); }
+// x ^= c * y for one (L, H) quad pair, c from tmult.
+__device__ __forceinline__ void qm(uint2& x, const uint2& y, const Mult& m) { qmul_sub(x.x, x.y, y.x, y.y, m); }
 __device__ __forceinline__ void qx(uint2& x, const uint2& y) {
   x.x ^= y.x;
   x.y ^= y.y;
@@ -104,13 +107,13 @@ __device__ __forceinline__ void top_inverse(const DevTables& T, uint2 (&y)[SUBS]
   for (int t = 0; t < SUBS / 2; ++t) {
     qx(y[2 * t + 1], y[2 * t]);
     const uint32_t c = q * SUBS + 2u * t;
-    if (c) qm(y[2 * t], y[2 * t + 1], mult_of(T, c));
+    if (c) qm(y[2 * t], y[2 * t + 1], tmult(T, c));
   }
   if constexpr (SUBS == 4) {
     qx(y[2], y[0]);
     qx(y[3], y[1]);
     if (q) {
-      const Mult m9 = mult_of(T, 2u * q);
+      const Mult m9 = tmult(T, 2u * q);
       qm(y[0], y[2], m9);
       qm(y[1], y[3], m9);
     }
@@ -122,7 +125,7 @@ template <int SUBS>
 __device__ __forceinline__ void top_forward(const DevTables& T, uint2 (&w)[SUBS], uint32_t c) {
   if constexpr (SUBS == 4) {
     if (c) {
-      const Mult m9 = mult_of(T, 2u * c);
+      const Mult m9 = tmult(T, 2u * c);
       qm(w[0], w[2], m9);
       qm(w[1], w[3], m9);
     }
@@ -132,7 +135,7 @@ __device__ __forceinline__ void top_forward(const DevTables& T, uint2 (&w)[SUBS]
 #pragma unroll
   for (int t = 0; t < SUBS / 2; ++t) {
     const uint32_t c8 = c * SUBS + 2u * t;
-    if (c8) qm(w[2 * t], w[2 * t + 1], mult_of(T, c8));
+    if (c8) qm(w[2 * t], w[2 * t + 1], tmult(T, c8));
     qx(w[2 * t + 1], w[2 * t]);
   }
 }
@@ -143,6 +146,20 @@ __device__ __forceinline__ void top_forward(const DevTables& T, uint2 (&w)[SUBS]
 #ifndef NP_W_NT
 #define NP_W_NT true
 #endif
+// Sub-segment transforms of the shifts run in tower coordinates while
+// gen_of(index) <= kEncBigMaxGen (index < 4096: n <= 4096, config 4); their
+// levels below gen_of(index) with the full map.  Farther shifts of larger codes
+// run in Cantor coordinates.
+constexpr int kEncBigMaxGen = 4;
+
+// Quads per thread whose scratch loads the top-level passes issue together.
+// Measured at config 4: 4 is +4 % on the encode (the passes are bound by
+// scratch traffic, not load latency), so 1.
+#ifndef NP_ENC_JB
+#define NP_ENC_JB 1
+#endif
+constexpr int kEncJB = NP_ENC_JB;
+
 template <int KB>
 constexpr size_t enc_scratch() {
   return 2u * (KB / kS) * kSegScr;  // M (SUBS sub-segments) + W (SUBS sub-segments)
@@ -178,7 +195,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   for (uint32_t s = 0; s < SUBS; ++s) {
     const uint32_t index = 256u * s;
     __syncthreads();  // previous sub-segment is done with the tile and the tables
-    stage_vpools<kS, kTB>(T, index, VP);
+    stage_vpools<kS, kTB>(T, index, VP, true);
     {
       const uint32_t c0 = tid / G::Q, m0 = tid % G::Q;
       const uint32_t base = col_base<kS>(c0) ^ (8u * m0);
@@ -208,26 +225,38 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       const uint32_t cq = fresh_v(cqb);
       cq_read<kS>(tile, cq, CL, CH);
       store_rows(out, a.shard_len, index + 16 * g, a.wanted_n, CL, CH, lane, ncols, full);  // systematic rows
-      cq_levels<kS, true, false>(T, VP, index, g, CL, CH);
+      tower_convert(T, CL, CH);  // the transforms run in tower coordinates
+      with_gen<0, 2, false>(index, [&](auto gc) __attribute__((always_inline)) {
+        constexpr int GEN = decltype(gc)::value;  // 0 only at index 0
+        cq_levels<kS, true, GEN == 0, GEN>(T, VP, index, g, CL, CH);
+      });
       cq_write<kS>(tile, cq, CL, CH);
     }
     __syncthreads();
     uint32_t XL[16], XH[16];
     hi_read<kS>(tile, fresh_v(hb), XL, XH);
-    hi_levels<kS, true, false>(T, VP, index, XL, XH);
+    with_gen<0, 2, false>(index, [&](auto gc) __attribute__((always_inline)) {
+      constexpr int GEN = decltype(gc)::value;
+      hi_levels<kS, true, GEN == 0, 0, GEN>(T, VP, index, XL, XH);
+    });
     scr_store<false>(scrM + s * kSegScr, tid, XL, XH);
   }
 
   // ---- phase 2: top inverse levels at index 0 -> coefficients M (in place;
   // sub-segment 0 is unchanged: every level-8/9 butterfly at index 0 keeps lo)
 #pragma unroll 1
-  for (uint32_t j = 0; j < 16; ++j) {
-    uint2 x[SUBS];
+  for (uint32_t j0 = 0; j0 < 16; j0 += kEncJB) {
+    uint2 x[kEncJB][SUBS];  // kEncJB quads' loads in flight at once
 #pragma unroll
-    for (int s = 0; s < SUBS; ++s) x[s] = scr_q<false>(scrM + s * kSegScr, j, tid);
-    top_inverse<SUBS>(T, x, 0u);
+    for (int u = 0; u < kEncJB; ++u)
 #pragma unroll
-    for (int s = 1; s < SUBS; ++s) scr_q_store<false>(scrM + s * kSegScr, j, tid, x[s]);
+      for (int s = 0; s < SUBS; ++s) x[u][s] = scr_q<false>(scrM + s * kSegScr, j0 + u, tid);
+#pragma unroll
+    for (int u = 0; u < kEncJB; ++u) {
+      top_inverse<SUBS>(T, x[u], 0u);
+#pragma unroll
+      for (int s = 1; s < SUBS; ++s) scr_q_store<false>(scrM + s * kSegScr, j0 + u, tid, x[u][s]);
+    }
   }
 
   // ---- phase 3: every shift c = 1.. : top forward levels, then SUBS x FFT(256)
@@ -236,28 +265,41 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   for (uint32_t c = 1; c < nshift; ++c) {
     if (c * KB >= a.wanted_n) break;
 #pragma unroll 1
-    for (uint32_t j = 0; j < 16; ++j) {
-      uint2 w[SUBS];
+    for (uint32_t j0 = 0; j0 < 16; j0 += kEncJB) {
+      uint2 w[kEncJB][SUBS];
 #pragma unroll
-      for (int s = 0; s < SUBS; ++s) w[s] = scr_q<false>(scrM + s * kSegScr, j, tid);
-      top_forward<SUBS>(T, w, c);
+      for (int u = 0; u < kEncJB; ++u)
 #pragma unroll
-      for (int s = 0; s < SUBS; ++s) scr_q_store<NP_W_NT>(scrW + s * kSegScr, j, tid, w[s]);
+        for (int s = 0; s < SUBS; ++s) w[u][s] = scr_q<false>(scrM + s * kSegScr, j0 + u, tid);
+#pragma unroll
+      for (int u = 0; u < kEncJB; ++u) {
+        top_forward<SUBS>(T, w[u], c);
+#pragma unroll
+        for (int s = 0; s < SUBS; ++s) scr_q_store<NP_W_NT>(scrW + s * kSegScr, j0 + u, tid, w[u][s]);
+      }
     }
 #pragma unroll 1
     for (uint32_t s = 0; s < SUBS; ++s) {
       const uint32_t index = c * KB + 256u * s;
       if (index >= a.wanted_n) break;
       __syncthreads();  // the tile and the tables are free
-      stage_vpools<kS, kTB>(T, index, VP);
+      stage_vpools<kS, kTB>(T, index, VP, gen_of(index) <= kEncBigMaxGen);
       __syncthreads();
       uint32_t XL[16], XH[16];
       scr_load<NP_W_NT>(scrW + s * kSegScr, tid, XL, XH);
-      hi_levels<kS, false, false>(T, VP, index, XL, XH);
+      with_gen<1, kEncBigMaxGen, true>(index, [&](auto gc) __attribute__((always_inline)) {
+        constexpr int GEN = decltype(gc)::value;
+        if constexpr (GEN < 0) tower_convert(T, XL, XH);  // a far shift: Cantor coordinates
+        hi_levels<kS, false, false, 0, GEN>(T, VP, index, XL, XH);
+      });
       hi_write<kS>(tile, fresh_v(hb), XL, XH);
       __syncthreads();
       cq_read<kS>(tile, fresh_v(cqb), XL, XH);
-      cq_levels<kS, false, false>(T, VP, index, g, XL, XH);
+      with_gen<1, kEncBigMaxGen, true>(index, [&](auto gc) __attribute__((always_inline)) {
+        constexpr int GEN = decltype(gc)::value;
+        cq_levels<kS, false, false, GEN>(T, VP, index, g, XL, XH);
+        if constexpr (GEN >= 0) tower_convert(T, XL, XH);  // back to Cantor coordinates for the rows
+      });
       store_rows(out, a.shard_len, index + 16 * g, a.wanted_n, XL, XH, lane, ncols, full);
     }
   }
@@ -297,6 +339,75 @@ __host__ __device__ constexpr bool kappa_bit_used(int b) {
   return false;
 }
 
+// Highest gen_of of a phase-1 sub-segment transform (index 256 (SUBS NQ - 1)).
+template <int KB, int NQ>
+constexpr int kRecBigMaxGen = static_cast<int>(gen_of(256u * (KB / kS * NQ - 1)));
+
+// Per-payload record of the big reconstruct (k_big_records): a mode word, then
+// the row multipliers E[0..n) (u16: EXP[loc] of present rows, EXP[-loc] of
+// erased ones) and the present flags PR[0..n) (bytes), as the kernel's LDS
+// holds them.
+constexpr uint32_t kBigSkip = 0;  // fewer than k present rows (NeedMoreShards)
+constexpr uint32_t kBigCopy = 1;  // all k systematic rows present: a copy
+constexpr uint32_t kBigDecode = 2;
+constexpr size_t kBigRecHeader = 16;
+__host__ __device__ constexpr size_t big_rec_stride(uint32_t n) { return kBigRecHeader + 3u * n; }
+
+// Output column c, symbols 256 s .. 256 s + 255 (bytes [2 KB c + 512 s, +512))
+// from the tile's natural blocks.
+template <int KB>
+__device__ __forceinline__ void tile_copy_out(const ReconstructArgs& a, const uint8_t* tile, uint32_t pb,
+                                              uint32_t col0, uint32_t ncols, uint32_t s) {
+  using G = Geo<kS>;
+  uint8_t* outp = a.out + static_cast<size_t>(pb) * a.out_stride + static_cast<size_t>(col0) * 2 * KB + 512u * s;
+  const bool al_o = ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 7u) == 0;
+  const uint32_t tid = threadIdx.x, c0 = tid / G::Q, m0 = tid % G::Q;
+  const uint32_t base = col_base<kS>(c0) ^ (8u * m0);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const uint32_t c = c0 + 16u * i;
+    if (c >= ncols) break;
+    const uint2 v = *reinterpret_cast<const uint2*>(tile + (base ^ col_base_c<kS>(16u * i)));
+    uint8_t* o = outp + static_cast<size_t>(c) * 2 * KB + 8u * m0;
+    if (al_o) {
+      store_once(o, v);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = static_cast<uint8_t>((e < 4 ? v.x : v.y) >> (8 * (e & 3)));
+    }
+  }
+}
+
+// Every systematic row present: the reference returns them unchanged
+// (inc_reconstruct.rs:46-50), so the output is their column gather.
+template <int KB>
+__device__ __forceinline__ void big_copy_systematic(const ReconstructArgs& a, const uint8_t* sh, uint8_t* tile,
+                                                    uint32_t pb, uint32_t col0, uint32_t ncols, bool full) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, g = uniform(tid >> 6);
+  const uint32_t cqb = col_base<kS>(4 * lane) ^ (32u * g);
+#pragma unroll 1
+  for (uint32_t s = 0; s < static_cast<uint32_t>(KB / kS); ++s) {
+    uint32_t XL[16], XH[16];
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+      const uint32_t row = 256u * s + 16u * g + p;
+      blk_to_quad(load4(sh + static_cast<size_t>(row) * a.shard_len, lane, ncols, full), XL[p], XH[p]);
+    }
+    __syncthreads();  // the previous sub-segment's copy-out is done with the tile
+    cq_write<kS>(tile, cqb, XL, XH);
+    __syncthreads();
+    tile_copy_out<KB>(a, tile, pb, col0, ncols, s);
+  }
+}
+
+// Quad positions whose scratch loads phase 2 issues together (NQ <= 4);
+// 2 measured +3 % at config 4.
+#ifndef NP_REC_JB
+#define NP_REC_JB 1
+#endif
+template <int NQ>
+constexpr int kRecJB = NQ <= 4 ? NP_REC_JB : 1;
+
 template <int KB, int NQ>
 __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k_reconstruct_big(
     DevTables T, ReconstructArgs a, uint32_t nsyms, uint32_t tiles, uint32_t tile0, uint8_t* scratch) {
@@ -311,12 +422,13 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   const uint32_t blk = tile0 + blockIdx.x;
   const TileRef tr = tile_of(blk, tiles, (a.batch & 7u) == 0);
   const uint32_t pb = tr.pb, tl = tr.tl;
-  if (a.status && uniform(a.status[2 * pb]) != 0) return;  // fewer than k present rows (k_payload_status)
+  // the payload's record (k_big_records): mode, row multipliers E, present flags
+  const uint8_t* rec = a.prefix + static_cast<size_t>(pb) * big_rec_stride(N);
+  const uint32_t mode = uniform(*reinterpret_cast<const uint32_t*>(rec));
+  if (mode == kBigSkip) return;  // fewer than k present rows: status NeedMoreShards
   const uint32_t col0 = tl * kTile;
   const uint32_t ncols = min(static_cast<uint32_t>(kTile), nsyms - col0);
   const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);
-  const uint8_t* pres = a.present + static_cast<size_t>(pb) * N;
-  const uint16_t* loc = a.locators ? a.locators + static_cast<size_t>(pb) * N : nullptr;
   // y_qs (SUBS NQ slots), then D_256(y_0s) (SUBS slots, reused for e_s)
   uint8_t* scrY = scratch + static_cast<size_t>(blockIdx.x) * (SUBS * NQ + SUBS) * kSegScr;
   uint8_t* scrD = scrY + SUBS * NQ * kSegScr;
@@ -326,13 +438,14 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   const uint32_t cqb = col_base<kS>(4 * lane) ^ (32u * g);
   const uint32_t hb = col_base<kS>(tid / G::R) ^ (8u * (tid % G::R));
 
-  if (loc) {
-    for (uint32_t v = tid; v < static_cast<uint32_t>(N); v += kTB) {
-      E[v] = T.exp[loc[v]];
-      PR[v] = pres[v];
-    }
-  } else {
-    fused_locator<N, kTB>(T, pres, reinterpret_cast<uint32_t*>(tile), E, PR);
+  if (mode == kBigCopy) {  // all k systematic rows present: the output is those rows
+    big_copy_systematic<KB>(a, sh, tile, pb, col0, ncols, full);
+    return;
+  }
+  {  // E (2N bytes) and PR (N bytes) are contiguous in the record and in LDS
+    const uint4* src = reinterpret_cast<const uint4*>(rec + kBigRecHeader);
+    uint4* dst = reinterpret_cast<uint4*>(E);
+    for (uint32_t v = tid; v < 3u * N / 16u; v += kTB) dst[v] = src[v];
   }
 
   // ---- phase 1: y_qs for every segment q and sub-segment s
@@ -347,15 +460,20 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
     for (int half = 0; half < 2; ++half)
       load_rows<8>(rows[half], sh, a.shard_len, PR, index + 16 * gg + 8 * half, T.zeros, lane, ncols, full);
     __syncthreads();  // tile / tables free
-    stage_vpools<kS, kTB>(T, index, VP);
+    stage_vpools<kS, kTB>(T, index, VP, true);
     __syncthreads();
     uint32_t XL[16], XH[16];
     {
 #pragma unroll
       for (int half = 0; half < 2; ++half) {
         const uint2 (&raw)[8] = rows[half];
-        pipelined<8>(
-            T, [&](auto pc) __attribute__((always_inline)) { return uniform(E[index + 16 * gg + 8 * half + decltype(pc)::value]); },
+        const uint32_t r0 = index + 16 * gg + 8 * half;
+        // premultiply (Cantor in, tower out: in_pools) of the present rows
+        pipelined_rec<8>(
+            [&](auto pc) __attribute__((always_inline)) {
+              return (cpool_t)(T.in_pools) + uniform(E[r0 + decltype(pc)::value]) * kPoolWords;
+            },
+            [&](auto pc) __attribute__((always_inline)) { return uniform(PR[r0 + decltype(pc)::value]) != 0; },
             [&](auto pc, const Mult& pool) __attribute__((always_inline)) {
               constexpr int p = decltype(pc)::value;
               const int x = 8 * half + p;
@@ -368,12 +486,18 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
               }
             });
       }
-      cq_levels<kS, true, false>(T, VP, index, gg, XL, XH);
+      with_gen<0, kRecBigMaxGen<KB, NQ>, false>(index, [&](auto gc) __attribute__((always_inline)) {
+        constexpr int GEN = decltype(gc)::value;  // 0 only at index 0
+        cq_levels<kS, true, GEN == 0, GEN>(T, VP, index, gg, XL, XH);
+      });
       cq_write<kS>(tile, fresh_v(cqb), XL, XH);
     }
     __syncthreads();
     hi_read<kS>(tile, fresh_v(hb), XL, XH);
-    hi_levels<kS, true, false>(T, VP, index, XL, XH);
+    with_gen<0, kRecBigMaxGen<KB, NQ>, false>(index, [&](auto gc) __attribute__((always_inline)) {
+      constexpr int GEN = decltype(gc)::value;
+      hi_levels<kS, true, GEN == 0, 0, GEN>(T, VP, index, XL, XH);
+    });
     scr_store<true>(scrY + qs * kSegScr, tid, XL, XH);
     if (qs < static_cast<uint32_t>(SUBS)) {  // segment 0: also D_256(y_0s)
       uint32_t DL[16] = {0}, DH[16] = {0};
@@ -386,37 +510,26 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   // ---- phase 2: top levels of every x_q, the combination, the derivative's
   // high terms and the forward transform's top levels at index 0 -> e_s (over
   // D's slots)
-#pragma unroll 1
-  for (uint32_t j = 0; j < 16; ++j) {
-    uint2 d[SUBS], x0[SUBS];
-    {
-      uint2 z[SUBS];
+  // One quad position j: x0, z = D_256(y_0.) and the other segments' quads in,
+  // e_s out.
+  auto fold = [&](uint32_t j, uint2 (&x0)[SUBS], uint2 (&z)[SUBS], uint2 (&yq)[NQ - 1][SUBS])
+      __attribute__((always_inline)) {
+    uint2 d[SUBS];
+    top_inverse<SUBS>(T, x0, 0u);
+    top_inverse<SUBS>(T, z, 0u);  // D_256 lifted
+    // D_KB(x0)_s = (lifted D_256)_s ^ x0_{s | 2^m} for each high bit 256 2^m < KB clear in s
 #pragma unroll
-      for (int s = 0; s < SUBS; ++s) {
-        x0[s] = scr_q<true>(scrY + s * kSegScr, j, tid);
-        z[s] = scr_q<true>(scrD + s * kSegScr, j, tid);
-      }
-      top_inverse<SUBS>(T, x0, 0u);
-      top_inverse<SUBS>(T, z, 0u);  // D_256 lifted
-      // D_KB(x0)_s = (lifted D_256)_s ^ x0_{s | 2^m} for each high bit 256 2^m < KB clear in s
+    for (int s = 0; s < SUBS; ++s) {
+      d[s] = z[s];
 #pragma unroll
-      for (int s = 0; s < SUBS; ++s) {
-        d[s] = z[s];
-#pragma unroll
-        for (int m = 1; m < SUBS; m <<= 1)
-          if (!(s & m)) qx(d[s], x0[s | m]);
-      }
+      for (int m = 1; m < SUBS; m <<= 1)
+        if (!(s & m)) qx(d[s], x0[s | m]);
     }
     uint2 acc[4][SUBS];  // S_b, per Cantor bit b of kappa
 #pragma unroll
     for (int b = 0; b < 4; ++b)
 #pragma unroll
       for (int s = 0; s < SUBS; ++s) acc[b][s] = make_uint2(0u, 0u);
-    uint2 yq[NQ - 1][SUBS];  // every segment's quads in flight at once (one latency per j)
-#pragma unroll
-    for (int q = 1; q < NQ; ++q)
-#pragma unroll
-      for (int s = 0; s < SUBS; ++s) yq[q - 1][s] = scr_q<true>(scrY + (SUBS * q + s) * kSegScr, j, tid);
     auto accumulate = [&](const uint2 (&y)[SUBS], uint32_t kq) __attribute__((always_inline)) {
 #pragma unroll
       for (int b = 0; b < 4; ++b)
@@ -441,13 +554,33 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
     for (int b = 1; b < 4; ++b) {
       if (!kappa_bit_used<NQ>(b)) continue;
-      const Mult m = mult_of(T, 1u << b);
+      const Mult m = tmult(T, 1u << b);
 #pragma unroll
       for (int s = 0; s < SUBS; ++s) qm(d[s], acc[b][s], m);
     }
     top_forward<SUBS>(T, d, 0u);
 #pragma unroll
     for (int s = 0; s < SUBS; ++s) scr_q_store<true>(scrD + s * kSegScr, j, tid, d[s]);
+  };
+  constexpr int JB = kRecJB<NQ>;
+#pragma unroll 1
+  for (uint32_t j0 = 0; j0 < 16; j0 += JB) {
+    // every quad of JB positions in flight at once (one latency per JB positions)
+    uint2 x0[JB][SUBS], z[JB][SUBS], yq[JB][NQ - 1][SUBS];
+#pragma unroll
+    for (int u = 0; u < JB; ++u) {
+#pragma unroll
+      for (int s = 0; s < SUBS; ++s) {
+        x0[u][s] = scr_q<true>(scrY + s * kSegScr, j0 + u, tid);
+        z[u][s] = scr_q<true>(scrD + s * kSegScr, j0 + u, tid);
+      }
+#pragma unroll
+      for (int q = 1; q < NQ; ++q)
+#pragma unroll
+        for (int s = 0; s < SUBS; ++s) yq[u][q - 1][s] = scr_q<true>(scrY + (SUBS * q + s) * kSegScr, j0 + u, tid);
+    }
+#pragma unroll
+    for (int u = 0; u < JB; ++u) fold(j0 + u, x0[u], z[u], yq[u]);
   }
 
   // ---- phase 3: FFT(256, 256 s) of e_s, postmultiply erased rows, copy out
@@ -455,23 +588,34 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   for (uint32_t s = 0; s < SUBS; ++s) {
     const uint32_t index = 256u * s;
     __syncthreads();
-    stage_vpools<kS, kTB>(T, index, VP);
+    stage_vpools<kS, kTB>(T, index, VP, true);
     __syncthreads();
     uint32_t XL[16], XH[16];
     scr_load<true>(scrD + s * kSegScr, tid, XL, XH);
-    hi_levels<kS, false, false>(T, VP, index, XL, XH);
+    with_gen<0, 2, false>(index, [&](auto gc) __attribute__((always_inline)) {
+      constexpr int GEN = decltype(gc)::value;
+      hi_levels<kS, false, GEN == 0, 0, GEN>(T, VP, index, XL, XH);
+    });
     hi_write<kS>(tile, fresh_v(hb), XL, XH);
     __syncthreads();
     {
       const uint32_t gg = fresh(g), cq = fresh_v(cqb);
       cq_read<kS>(tile, cq, XL, XH);
-      cq_levels<kS, false, false>(T, VP, index, gg, XL, XH);
+      with_gen<0, 2, false>(index, [&](auto gc) __attribute__((always_inline)) {
+        constexpr int GEN = decltype(gc)::value;
+        cq_levels<kS, false, GEN == 0, GEN>(T, VP, index, gg, XL, XH);
+      });
 #pragma unroll
       for (int half = 0; half < 2; ++half) {
         uint2 raw[8];
-        load_rows<8>(raw, sh, a.shard_len, PR, index + 16 * gg + 8 * half, T.zeros, lane, ncols, full);
-        pipelined<8>(
-            T, [&](auto pc) __attribute__((always_inline)) { return uniform(E[index + 16 * gg + 8 * half + decltype(pc)::value]); },
+        const uint32_t r0 = index + 16 * gg + 8 * half;
+        load_rows<8>(raw, sh, a.shard_len, PR, r0, T.zeros, lane, ncols, full);
+        // received symbol (present) or postmultiplied (erased; tower in, Cantor out: out_pools)
+        pipelined_rec<8>(
+            [&](auto pc) __attribute__((always_inline)) {
+              return (cpool_t)(T.out_pools) + uniform(E[r0 + decltype(pc)::value]) * kPoolWords;
+            },
+            [&](auto pc) __attribute__((always_inline)) { return uniform(PR[r0 + decltype(pc)::value]) == 0; },
             [&](auto pc, const Mult& pool) __attribute__((always_inline)) {
               constexpr int p = decltype(pc)::value;
               const int x = 8 * half + p;
@@ -487,26 +631,51 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       cq_write<kS>(tile, cq, XL, XH);
     }
     __syncthreads();
-    {  // output column c, symbols 256 s .. 256 s + 255: bytes [2 KB c + 512 s, +512)
-      uint8_t* outp = a.out + static_cast<size_t>(pb) * a.out_stride + static_cast<size_t>(col0) * 2 * KB + 512u * s;
-      const bool al_o = ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 7u) == 0;
-      const uint32_t c0 = tid / G::Q, m0 = tid % G::Q;
-      const uint32_t base = col_base<kS>(c0) ^ (8u * m0);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const uint32_t c = c0 + 16u * i;
-        if (c >= ncols) break;
-        const uint2 v = *reinterpret_cast<const uint2*>(tile + (base ^ col_base_c<kS>(16u * i)));
-        uint8_t* o = outp + static_cast<size_t>(c) * 2 * KB + 8u * m0;
-        if (al_o) {
-          store_once(o, v);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] = static_cast<uint8_t>((e < 4 ? v.x : v.y) >> (8 * (e & 3)));
-        }
-      }
-    }
+    tile_copy_out<KB>(a, tile, pb, col0, ncols, s);
   }
+}
+
+// One workgroup per payload: the status (mod.rs:178-180), the mode, and for a
+// decode the erasure locator (fused_locator: eval_error_polynomial,
+// inc_reconstruct.rs:90-113, folded to the n rows; or the caller's
+// locators) as row multipliers E and present flags PR.  Once per payload
+// instead of once per column tile.
+template <int K, int N>
+__global__ __launch_bounds__(256) void k_big_records(DevTables T, ReconstructArgs a, uint8_t* out) {
+  __shared__ uint32_t W[N];
+  __shared__ __attribute__((aligned(16))) uint16_t E[N];
+  __shared__ __attribute__((aligned(16))) uint8_t PR[N];
+  const uint32_t pb = blockIdx.x, tid = threadIdx.x;
+  const uint8_t* pres = a.present + static_cast<size_t>(pb) * N;
+  uint8_t* rec = out + static_cast<size_t>(pb) * big_rec_stride(N);
+  int have1 = 0, have = 0;  // present rows in [0, K) and [0, N)
+  for (int r = 0; r < N; r += 256) {
+    const bool p = pres[r + static_cast<int>(tid)] != 0;
+    if (r < K) have1 += __syncthreads_count(p);
+    have += __syncthreads_count(p);
+  }
+  const bool ok = have >= K;
+  if (tid == 0 && a.status) {
+    a.status[2 * pb] = ok ? 0u : kStatusNeedMoreShards;
+    a.status[2 * pb + 1] = static_cast<uint32_t>(have);
+  }
+  const uint32_t mode = !ok ? kBigSkip : have1 == K ? kBigCopy : kBigDecode;
+  if (tid == 0) *reinterpret_cast<uint32_t*>(rec) = mode;
+  if (mode != kBigDecode) return;
+  if (a.locators) {  // mul(x, log m) == x * EXP[m] (inc_log_mul.rs:42-49)
+    const uint16_t* loc = a.locators + static_cast<size_t>(pb) * N;
+    for (uint32_t v = tid; v < static_cast<uint32_t>(N); v += 256) {
+      E[v] = T.exp[loc[v]];
+      PR[v] = pres[v];
+    }
+  } else {
+    fused_locator<N, 256>(T, pres, W, E, PR);
+  }
+  __syncthreads();
+  uint4* dst = reinterpret_cast<uint4*>(rec + kBigRecHeader);
+  for (uint32_t v = tid; v < 2u * N / 16u; v += 256) dst[v] = reinterpret_cast<const uint4*>(E)[v];
+  dst += 2u * N / 16u;
+  for (uint32_t v = tid; v < static_cast<uint32_t>(N) / 16u; v += 256) dst[v] = reinterpret_cast<const uint4*>(PR)[v];
 }
 
 size_t enc_big_lds() { return static_cast<size_t>(Geo<kS>::kTileBytes) + 4u * Geo<kS>::kVPWords; }
@@ -514,17 +683,18 @@ size_t rec_big_lds(uint32_t n) {  // tile, tables, E (2 n bytes), PR (n bytes)
   return static_cast<size_t>(Geo<kS>::kTileBytes) + 4u * Geo<kS>::kVPWords + 3u * n;
 }
 
-// Calls f(kernel pointer) for the reconstruct instance of (n, k); false if none.
+// Calls f(reconstruct kernel, record kernel) for the instances of (n, k);
+// false if none.
 template <typename F>
 bool with_rec_big(uint32_t n, uint32_t k, F&& f) {
   if (k == 512) {
-    if (n == 1024) return f(&k_reconstruct_big<512, 2>), true;
-    if (n == 2048) return f(&k_reconstruct_big<512, 4>), true;
-    if (n == 4096) return f(&k_reconstruct_big<512, 8>), true;
+    if (n == 1024) return f(&k_reconstruct_big<512, 2>, &k_big_records<512, 1024>), true;
+    if (n == 2048) return f(&k_reconstruct_big<512, 4>, &k_big_records<512, 2048>), true;
+    if (n == 4096) return f(&k_reconstruct_big<512, 8>, &k_big_records<512, 4096>), true;
   } else if (k == 1024) {
-    if (n == 2048) return f(&k_reconstruct_big<1024, 2>), true;
-    if (n == 4096) return f(&k_reconstruct_big<1024, 4>), true;
-    if (n == 8192) return f(&k_reconstruct_big<1024, 8>), true;
+    if (n == 2048) return f(&k_reconstruct_big<1024, 2>, &k_big_records<1024, 2048>), true;
+    if (n == 4096) return f(&k_reconstruct_big<1024, 4>, &k_big_records<1024, 4096>), true;
+    if (n == 8192) return f(&k_reconstruct_big<1024, 8>, &k_big_records<1024, 8192>), true;
   }
   return false;
 }
@@ -533,7 +703,7 @@ bool with_rec_big(uint32_t n, uint32_t k, F&& f) {
 
 bool big_encode_supported(uint32_t n, uint32_t k) { return (k == 512 || k == 1024) && n >= 2 * k && n <= 65536; }
 bool big_reconstruct_supported(uint32_t n, uint32_t k) {
-  return with_rec_big(n, k, [](auto) {});
+  return with_rec_big(n, k, [](auto, auto) {});
 }
 size_t big_encode_scratch_per_tile(uint32_t k) { return k == 512 ? enc_scratch<512>() : enc_scratch<1024>(); }
 size_t big_reconstruct_scratch_per_tile(uint32_t n, uint32_t k) {
@@ -597,6 +767,17 @@ hipError_t launch_encode_big(const DevTables& T, const EncodeArgs& a, uint8_t* s
   return hipSuccess;
 }
 
+size_t big_record_stride(uint32_t n) { return big_rec_stride(n); }
+
+hipError_t launch_big_records(const DevTables& T, const ReconstructArgs& a, uint8_t* records, hipStream_t s) {
+  if (!big_reconstruct_supported(a.n, a.k) || a.batch > 0x7fffffffu) return hipErrorInvalidValue;
+  if (a.batch == 0) return hipSuccess;
+  with_rec_big(a.n, a.k, [&](auto, auto recs) {
+    recs<<<static_cast<uint32_t>(a.batch), 256, 0, s>>>(T, a, records);
+  });
+  return hipGetLastError();
+}
+
 hipError_t launch_reconstruct_big(const DevTables& T, const ReconstructArgs& a, uint8_t* scratch,
                                   size_t scratch_bytes, hipStream_t s) {
   if (!big_reconstruct_supported(a.n, a.k)) return hipErrorInvalidValue;
@@ -609,7 +790,7 @@ hipError_t launch_reconstruct_big(const DevTables& T, const ReconstructArgs& a, 
   if (per_launch == 0 || total > 0xffffffffu) return hipErrorInvalidValue;
   for (size_t t0 = 0; t0 < total; t0 += per_launch) {
     const uint32_t blocks = static_cast<uint32_t>(std::min(per_launch, total - t0));
-    with_rec_big(a.n, a.k, [&](auto kern) {
+    with_rec_big(a.n, a.k, [&](auto kern, auto) {
       kern<<<blocks, kTB, rec_big_lds(a.n), s>>>(T, a, static_cast<uint32_t>(nsyms), tiles, static_cast<uint32_t>(t0),
                                                  scratch);
     });
@@ -629,7 +810,7 @@ hipError_t configure_big_kernels() {
   set(reinterpret_cast<const void*>(&k_encode_big<1024>), enc_big_lds());
   for (uint32_t k : {512u, 1024u})
     for (uint32_t nq : {2u, 4u, 8u})
-      with_rec_big(nq * k, k, [&](auto kern) { set(reinterpret_cast<const void*>(kern), rec_big_lds(nq * k)); });
+      with_rec_big(nq * k, k, [&](auto kern, auto) { set(reinterpret_cast<const void*>(kern), rec_big_lds(nq * k)); });
   return e;
 }
 

@@ -25,7 +25,8 @@ struct ReconstructArgs {
   const uint8_t* present;    // device, batch x n
   const uint16_t* locators;  // device, batch x n (log form)
   // fast path: per-payload decode prefix, row multipliers and their tables
-  // from launch_prefix_locator (stride prefix_stride(n) bytes)
+  // from launch_prefix_locator (stride prefix_stride(n) bytes); big path: the
+  // records of launch_big_records (stride big_record_stride(n))
   const uint8_t* prefix;
   size_t batch;
   uint32_t n, k;
@@ -91,6 +92,11 @@ bool big_reconstruct_supported(uint32_t n, uint32_t k);  // n / k in {2, 4, 8}
 size_t big_encode_scratch_per_tile(uint32_t k);
 size_t big_resident_slots(int device);  // scratch slots a launch uses at most (multiple of 8)
 size_t big_reconstruct_scratch_per_tile(uint32_t n, uint32_t k);
+// Per-payload records (status, mode, row multipliers, present flags) of the
+// big reconstruct, big_record_stride(n) bytes each, into `records`; the
+// reconstruct launch reads them through a.prefix.
+size_t big_record_stride(uint32_t n);
+hipError_t launch_big_records(const DevTables& T, const ReconstructArgs& a, uint8_t* records, hipStream_t s);
 hipError_t launch_encode_big(const DevTables& T, const EncodeArgs& a, uint8_t* scratch, size_t scratch_bytes,
                              hipStream_t s);
 hipError_t launch_reconstruct_big(const DevTables& T, const ReconstructArgs& a, uint8_t* scratch,
