@@ -635,6 +635,45 @@ __device__ __forceinline__ void pipelined(const DevTables& T, CF cval, GF group)
   pipe_step<0, NG>(T, cval, group, pa, pb);
 }
 
+// NP_PIPE_WAIT: group f starts with an explicit wait for every outstanding
+// scalar / LDS load (the tables of group f, issued during group f-1), and only
+// then issues the prefetch of group f+1 (SGPR half by s_load, VGPR half by
+// ds_read).  Without it the compiler's wait for group f's tables also waits
+// for the prefetch issued just before (scalar loads return out of order, so
+// the only wait it can use is lgkmcnt(0)): the prefetch never overlaps.
+// Measured neutral (config 3 +0.3 %, config 4 within its run-to-run noise):
+// the table fetches do not bound the kernels, so off.  Loading the row
+// tables' VGPR half by vector loads instead of s_load + v_mov measured +7 %
+// on the decode.
+#ifndef NP_PIPE_WAIT
+#define NP_PIPE_WAIT 0
+#endif
+constexpr uint16_t kWaitLgkm0 = 0xC07F;  // s_waitcnt lgkmcnt(0), vmcnt / expcnt untouched (gfx9 encoding)
+
+struct VHalf {
+  uint32_t v[8];
+};
+
+template <bool SUB>
+__device__ __forceinline__ void vhalf_load(const uint32_t* vp, VHalf& h) {
+  const uint4 a = *reinterpret_cast<const uint4*>(vp);
+  h.v[0] = a.x, h.v[1] = a.y, h.v[2] = a.z, h.v[3] = a.w;
+  if constexpr (!SUB) {
+    const uint4 b = *reinterpret_cast<const uint4*>(vp + 4);
+    h.v[4] = b.x, h.v[5] = b.y, h.v[6] = b.z, h.v[7] = b.w;
+  }
+}
+
+template <bool SUB>
+__device__ __forceinline__ Mult mult_from(const uint32_t (&sp)[12], const VHalf& h) {
+  Mult m;
+#pragma unroll
+  for (int i = 0; i < (SUB ? 6 : 12); ++i) m.s[i] = sp[i];
+#pragma unroll
+  for (int i = 0; i < (SUB ? 4 : 8); ++i) m.v[i] = h.v[i];
+  return m;
+}
+
 // Same with group f's tables at rec(Int<f>) (a wave-uniform global address).
 __device__ __forceinline__ void pool_at(cpool_t q, uint32_t (&p)[20]) {
 #pragma unroll
@@ -646,6 +685,7 @@ __device__ __forceinline__ void pool_at(cpool_t q, uint32_t (&p)[20]) {
 template <int F, int NG, typename RF, typename NF, typename GF>
 __device__ __forceinline__ void rpipe_step(RF& rec, NF& need, GF& group, uint32_t (&cur)[20], uint32_t (&nxt)[20]) {
   if constexpr (F < NG) {
+    if constexpr (NP_PIPE_WAIT) __builtin_amdgcn_s_waitcnt(kWaitLgkm0);  // see spipe_step
     if constexpr (F + 1 < NG) {
       if (need(Int<F + 1>{})) pool_at(rec(Int<F + 1>{}), nxt);
     }
@@ -669,21 +709,33 @@ __device__ __forceinline__ void pipelined_rec(RF rec, NF need, GF group) {
 // subf(Int<f>) -> std::integral_constant<bool, group f multiplies in the subfield form>.
 template <int F, int NG, bool TW, typename CF, typename VF, typename SF, typename GF>
 __device__ __forceinline__ void spipe_step(const DevTables& T, CF& cval, VF& vaddr, SF& subf, GF& group,
-                                           uint32_t (&cur)[12], uint32_t (&nxt)[12]) {
+                                           uint32_t (&cur)[12], uint32_t (&nxt)[12], VHalf& curv, VHalf& nxtv) {
   if constexpr (F < NG) {
-    if constexpr (F + 1 < NG) spool_of<TW, decltype(subf(Int<F + 1>{}))::value>(T, cval(Int<F + 1>{}), nxt);
+    if constexpr (NP_PIPE_WAIT) {
+      __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+      if constexpr (F + 1 < NG) {
+        spool_of<TW, decltype(subf(Int<F + 1>{}))::value>(T, cval(Int<F + 1>{}), nxt);
+        vhalf_load<decltype(subf(Int<F + 1>{}))::value>(vaddr(Int<F + 1>{}), nxtv);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      group(Int<F>{}, mult_from<decltype(subf(Int<F>{}))::value>(cur, curv));
+    } else {
+      if constexpr (F + 1 < NG) spool_of<TW, decltype(subf(Int<F + 1>{}))::value>(T, cval(Int<F + 1>{}), nxt);
+      __builtin_amdgcn_sched_barrier(0);
+      group(Int<F>{}, staged_mult<decltype(subf(Int<F>{}))::value>(cur, vaddr(Int<F>{})));
+    }
     __builtin_amdgcn_sched_barrier(0);
-    group(Int<F>{}, staged_mult<decltype(subf(Int<F>{}))::value>(cur, vaddr(Int<F>{})));
-    __builtin_amdgcn_sched_barrier(0);
-    spipe_step<F + 1, NG, TW>(T, cval, vaddr, subf, group, nxt, cur);
+    spipe_step<F + 1, NG, TW>(T, cval, vaddr, subf, group, nxt, cur, nxtv, curv);
   }
 }
 
 template <int NG, bool TW = false, typename CF, typename VF, typename SF, typename GF>
 __device__ __forceinline__ void pipelined_staged(const DevTables& T, CF cval, VF vaddr, SF subf, GF group) {
   uint32_t pa[12], pb[12];
+  VHalf va, vb;
   spool_of<TW, decltype(subf(Int<0>{}))::value>(T, cval(Int<0>{}), pa);
-  spipe_step<0, NG, TW>(T, cval, vaddr, subf, group, pa, pb);
+  if constexpr (NP_PIPE_WAIT) vhalf_load<decltype(subf(Int<0>{}))::value>(vaddr(Int<0>{}), va);
+  spipe_step<0, NG, TW>(T, cval, vaddr, subf, group, pa, pb, va, vb);
 }
 
 // LDS slot of the multiplier of group t at level b of a size-K transform:

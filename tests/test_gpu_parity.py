@@ -331,7 +331,8 @@ def test_fast_encode_shapes(gpu, oracle, nw, kw, plen):
                                               (1024, 512, 1024 * 100, 512), (2000, 667, 1024 * 256, 1333),
                                               (2000, 667, 1024 * 257 + 9, -1), (2500, 834, 1024 * 260 + 1, 1666),
                                               (2500, 834, 1024 * 256, -1), (5000, 1667, 2048 * 40 + 3, 3333),
-                                              (5000, 1667, 2048 * 33, -1)])
+                                              (5000, 1667, 2048 * 33, -1), (2000, 667, 1024 * 256 + 5, 0),
+                                              (4096, 1366, 2048 * 256, 0)])
 def test_fast_reconstruct_shapes(gpu, oracle, nw, kw, plen, erase):
     """Specialised reconstruct kernels (k in {64,128,256} fast, {512,1024} big;
     n in {2k,4k,8k}): full
