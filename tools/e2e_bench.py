@@ -61,8 +61,10 @@ t_enc = timed(lambda: npa.encode_batch_host(p, h_pay.data_ptr(), plen, plen, B, 
 t_rec = timed(lambda: npa.reconstruct_batch_host(p, h_sh.data_ptr(), sl, n * sl, pres.ctypes.data, B,
                                                  h_out.data_ptr(), olen, ctx=ctx))
 ok = torch.equal(h_out[:, :plen], h_pay)
-# bytes crossing PCIe: encode P in + n*sl out; reconstruct the prefix rows in (+ flags) and 2k*sl/2 out
-rows = max(k if pres[b, :k].all() else (2 * k if (n == 4 * k and pres[b, :2 * k].sum() >= k) else n) for b in range(B))
+# bytes crossing PCIe: encode P in + n*sl out; reconstruct the rows the engine
+# ships (engine.cpp rows_needed: the k systematic rows when every payload of the
+# batch has them all, else all n rows: exactness) in (+ flags) and 2k*sl/2 out
+rows = k if all(pres[b, :k].all() for b in range(B)) else n
 res = {
     "config": args.config, "batch": B, "payload_bytes": plen, "n": n, "k": k,
     "pcie_GB_s": {"h2d": round(bw_h2d, 1), "d2h": round(bw_d2h, 1)},
