@@ -491,9 +491,42 @@ constexpr bool kRowPrefetch = NQ <= 2;
 #ifndef NP_REC_IDX0
 #define NP_REC_IDX0 1  // measured: reconstruct -1.1 % (config 3)
 #endif
+// The tables of all NQ segment transforms fit in LDS next to the tile (K = 256:
+// 128 KiB + 4 x 8 KiB of the 160 KiB): staged once per workgroup and kept for
+// all its tiles, instead of two buffers restaged per step.  Measured -1 % to
+// +0.6 % at config 3 (noise), -1.2 % at config 2.  (An L2 prefetch of the next
+// step's rows by LDS-DMA into a dummy LDS area measured +8 %: vector loads
+// complete in order, so the wait for a step's last row also waited for the
+// prefetch behind it.)
+#ifndef NP_REC_RESIDENT
+#define NP_REC_RESIDENT 1
+#endif
+template <int K, int NQ>
+constexpr bool kRecResident =
+    NP_REC_RESIDENT && NQ > 1 && Geo<K>::kTileBytes + NQ * 4u * Geo<K>::kVPWords <= 160u * 1024u;
+// LDS buffer of segment q's tables at decode step `step`.
+template <int K, int NQ>
+__device__ __forceinline__ uint32_t vp_slot(int q, int step) {
+  return kRecResident<K, NQ> ? static_cast<uint32_t>(q) : static_cast<uint32_t>(step & 1);
+}
+
 // Largest gen_of over the decode's segment transforms (index qK, q < NQ).
 template <int K, int NQ>
 constexpr int kRecMaxGen = static_cast<int>(gen_of(static_cast<uint32_t>((NQ - 1) * K)));
+
+// Tables staged before the first step: every segment's (kRecResident, slot q)
+// or those of steps 0 and 1 (slots 0 and 1).  Caller synchronises.
+template <int K, int NQ>
+__device__ __forceinline__ void stage_rec_tables(const DevTables& T, uint32_t* VP) {
+  if constexpr (kRecResident<K, NQ>) {
+#pragma unroll 1
+    for (int q = 0; q < NQ; ++q)
+      stage_vpools<K, Geo<K>::kThreads>(T, static_cast<uint32_t>(q) * K, VP + q * Geo<K>::kVPWords, true);
+  } else {
+    stage_vpools<K, Geo<K>::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(0)) * K, VP, true);
+    stage_vpools<K, Geo<K>::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(1)) * K, VP + Geo<K>::kVPWords, true);
+  }
+}
 
 // The segment sweep: x_q = IFFT(K, qK)(premultiplied segment q), folded into
 // A.  With kRowPrefetch `raw` holds segment seg_of(0)'s rows on entry and the
@@ -518,9 +551,10 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
 #pragma unroll
     for (int i = 1; i < NQ; ++i) m = step == i ? msk[i] : m;
     m = uniform(m);
-    if constexpr (!kRowPrefetch<NQ>)
+    if constexpr (!kRowPrefetch<NQ>) {
       issue_rows(raw, (kExp & 32) ? T.zeros : sh, (kExp & 32) ? 0 : shard_len, m, index + 16 * g, T.zeros, c.lane,
                  c.ncols, c.full);
+    }
     uint32_t XL[16], XH[16];
     stamp(c.dbg, 2 + 6 * step);
     pipelined_rec<16>(
@@ -543,7 +577,7 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
             }
           }
         });
-    const uint32_t* vp = c.VP + (step & 1) * Geo<K>::kVPWords;
+    const uint32_t* vp = c.VP + vp_slot<K, NQ>(q, step) * Geo<K>::kVPWords;
     stamp(c.dbg, 3 + 6 * step);
     // absent rows are zero; segment q's transform has gen_of(qK) <= kRecMaxGen
     with_gen<0, kRecMaxGen<K, NQ>, false>(index, [&](auto gc) __attribute__((always_inline)) {
@@ -552,7 +586,7 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
     stamp(c.dbg, 4 + 6 * step);
     if (step > 0 || after_tile) {
       __syncthreads();  // the previous high pass (or tile's copy-out) is done with the tile and the other table buffer
-      if (step + 1 < NQ) {
+      if (!kRecResident<K, NQ> && step + 1 < NQ) {
         const int qn = seg_of<NQ>(step + 1);
         stage_vpools<K, Geo<K>::kThreads>(T, static_cast<uint32_t>(qn) * K, c.VP + ((step + 1) & 1) * Geo<K>::kVPWords, true);
       }
@@ -667,9 +701,9 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
 
   uint32_t XL[16], XH[16];
   if constexpr (NQ > 1) {
-    // multiplier tables of the first two segment transforms (indices 2K, 3K or K, 0)
-    stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(0)) * K, VP, true);
-    stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(1)) * K, VP + G::kVPWords, true);
+    // multiplier tables of the first two segment transforms (indices 2K, 3K or
+    // K, 0), or of all of them (kRecResident)
+    stage_rec_tables<K, NQ>(T, VP);
     __syncthreads();
     stamp(dbg, 1);
 
@@ -678,7 +712,7 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
     RecCtx c{T, a.shard_len, tile, rows, sh, VP, g, lane, tid, ncols, full, cqb, hb, dbg};
     rec_segments<K, NQ>(c, msk, raw, AL, AH, false);
     // ---- forward transform of size K at index 0
-    const uint32_t* vp0 = VP + ((NQ - 1) & 1) * G::kVPWords;  // segment 0's tables = FFT(K, 0)'s
+    const uint32_t* vp0 = VP + vp_slot<K, NQ>(0, NQ - 1) * G::kVPWords;  // segment 0's tables = FFT(K, 0)'s
     stamp(dbg, 26);
     hi_levels<K, false, true, 0, 0>(T, vp0, 0, AL, AH);
     stamp(dbg, 27);
@@ -807,9 +841,8 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
   }
   if constexpr (NQ > 1) {
     // multiplier tables of the first two segment transforms (indices 2K, 3K or
-    // K, 0): for NQ = 2 these are all the tables, kept for every tile
-    stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(0)) * K, VP, true);
-    stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(1)) * K, VP + G::kVPWords, true);
+    // K, 0), or of all of them (kRecResident): kept for every tile
+    stage_rec_tables<K, NQ>(T, VP);
     __syncthreads();
   }
 
@@ -829,10 +862,10 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
     const bool full = ncols == kTile && aligned;
     const uint8_t* sh = shp + 2u * static_cast<size_t>(col0);
     uint64_t* dbg = (kExp & 64) ? reinterpret_cast<uint64_t*>(a.out + static_cast<size_t>(pb) * a.out_stride +
-                                                               static_cast<size_t>(nsyms) * 2 * K + 256u * tl)
+                                                               static_cast<size_t>(nsyms) * 2 * K + ((kExp & 128) ? 4096u : 256u) * tl)
                                  : nullptr;
     stamp(dbg, 0);
-    if constexpr (NQ >= 4) {
+    if constexpr (NQ >= 4 && !kRecResident<K, NQ>) {
       if (t > 0) {  // the first two segments' tables were replaced during the previous tile
         __syncthreads();
         stage_vpools<K, G::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(0)) * K, VP, true);
@@ -846,9 +879,11 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
       const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
       uint32_t AL[16], AH[16];
       RecCtx c{T, shard_len, tile, rows, sh, VP, g, lane, tid, ncols, full, cqb, hb, dbg};
-      rec_segments<K, NQ>(c, msk, raw, AL, AH, t > 0 && NQ == 2);
+      // t > 0: step 0 waits for the previous tile's last LDS reads (its FFT's
+      // cq_read, the copy-out) before writing the tile
+      rec_segments<K, NQ>(c, msk, raw, AL, AH, t > 0 && (NQ == 2 || kRecResident<K, NQ>));
       // ---- forward transform of size K at index 0
-      const uint32_t* vp0 = VP + ((NQ - 1) & 1) * G::kVPWords;  // segment 0's tables = FFT(K, 0)'s
+      const uint32_t* vp0 = VP + vp_slot<K, NQ>(0, NQ - 1) * G::kVPWords;  // segment 0's tables = FFT(K, 0)'s
       stamp(dbg, 26);
       hi_levels<K, false, true, 0, 0>(T, vp0, 0, AL, AH);
       stamp(dbg, 27);
@@ -971,7 +1006,7 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     const bool full =
         ncols == kTile && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
     uint64_t* dbg = (kExp & 64) ? reinterpret_cast<uint64_t*>(a.out + static_cast<size_t>(pb) * a.out_stride +
-                                                               static_cast<size_t>(nsyms) * 2 * K + 256u * tl0)
+                                                               static_cast<size_t>(nsyms) * 2 * K + ((kExp & 128) ? 4096u : 256u) * tl0)
                                  : nullptr;
     if constexpr (SERVE >= 4) {
       if (nq == SERVE) rec_tile<K, SERVE>(T, a, sh, pres, rows, smem, pb, col0, ncols, full, dbg);
@@ -1091,7 +1126,7 @@ size_t encode_multi_lds_bytes() {
 
 template <int K, int NQ>
 size_t reconstruct_lds_bytes() {
-  return static_cast<size_t>(Geo<K>::kTileBytes) + 2u * 4u * Geo<K>::kVPWords;
+  return static_cast<size_t>(Geo<K>::kTileBytes) + (kRecResident<K, NQ> ? NQ : 2) * 4u * Geo<K>::kVPWords;
 }
 
 // Tiles per workgroup (kMultiTile): as many as keep >= kWorkgroups
