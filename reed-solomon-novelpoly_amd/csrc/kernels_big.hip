@@ -97,45 +97,60 @@ __device__ __forceinline__ void qx(uint2& x, const uint2& y) {
   x.y ^= y.y;
 }
 
-// Top inverse levels of a size-(256 SUBS) transform at index 256 SUBS q, on one
-// position quad of each sub-segment: level 8 (groups t, skew Cantor(q SUBS + 2t)),
-// then level 9 (SUBS = 4, skew Cantor(2q)); inverse butterfly hi ^= lo; lo ^= c hi.
-// q is a compile-time constant at every call, so the zero skews of q = 0 fold.
+// The multipliers of the top levels of a size-(256 SUBS) transform at index
+// 256 SUBS q: level 8 group t skew Cantor(q SUBS + 2t), level 9 (SUBS = 4)
+// skew Cantor(2q); all in GF(2^8).  Loaded once per pass over the 16 quads.
 template <int SUBS>
-__device__ __forceinline__ void top_inverse(const DevTables& T, uint2 (&y)[SUBS], uint32_t q) {
+struct TopMults {
+  Mult m8[SUBS / 2];
+  Mult m9;
+};
+template <int SUBS>
+__device__ __forceinline__ TopMults<SUBS> top_mults(const DevTables& T, uint32_t q) {
+  TopMults<SUBS> m;
+#pragma unroll
+  for (int t = 0; t < SUBS / 2; ++t)
+    if (q * SUBS + 2u * t) m.m8[t] = tmult(T, q * SUBS + 2u * t);
+  if constexpr (SUBS == 4) {
+    if (q) m.m9 = tmult(T, 2u * q);
+  }
+  return m;
+}
+
+// Top inverse levels (8, then 9 for SUBS = 4) on one position quad of each
+// sub-segment: inverse butterfly hi ^= lo; lo ^= c hi.  q is a compile-time
+// constant at the q = 0 calls, so their zero skews fold.
+template <int SUBS>
+__device__ __forceinline__ void top_inverse(uint2 (&y)[SUBS], uint32_t q, const TopMults<SUBS>& m) {
 #pragma unroll
   for (int t = 0; t < SUBS / 2; ++t) {
     qx(y[2 * t + 1], y[2 * t]);
-    const uint32_t c = q * SUBS + 2u * t;
-    if (c) qm(y[2 * t], y[2 * t + 1], tmult(T, c));
+    if (q * SUBS + 2u * t) qm(y[2 * t], y[2 * t + 1], m.m8[t]);
   }
   if constexpr (SUBS == 4) {
     qx(y[2], y[0]);
     qx(y[3], y[1]);
     if (q) {
-      const Mult m9 = tmult(T, 2u * q);
-      qm(y[0], y[2], m9);
-      qm(y[1], y[3], m9);
+      qm(y[0], y[2], m.m9);
+      qm(y[1], y[3], m.m9);
     }
   }
 }
 
 // Top forward levels at index 256 SUBS c (level 9, then 8): lo ^= c hi; hi ^= lo.
 template <int SUBS>
-__device__ __forceinline__ void top_forward(const DevTables& T, uint2 (&w)[SUBS], uint32_t c) {
+__device__ __forceinline__ void top_forward(uint2 (&w)[SUBS], uint32_t c, const TopMults<SUBS>& m) {
   if constexpr (SUBS == 4) {
     if (c) {
-      const Mult m9 = tmult(T, 2u * c);
-      qm(w[0], w[2], m9);
-      qm(w[1], w[3], m9);
+      qm(w[0], w[2], m.m9);
+      qm(w[1], w[3], m.m9);
     }
     qx(w[2], w[0]);
     qx(w[3], w[1]);
   }
 #pragma unroll
   for (int t = 0; t < SUBS / 2; ++t) {
-    const uint32_t c8 = c * SUBS + 2u * t;
-    if (c8) qm(w[2 * t], w[2 * t + 1], tmult(T, c8));
+    if (c * SUBS + 2u * t) qm(w[2 * t], w[2 * t + 1], m.m8[t]);
     qx(w[2 * t + 1], w[2 * t]);
   }
 }
@@ -152,17 +167,10 @@ __device__ __forceinline__ void top_forward(const DevTables& T, uint2 (&w)[SUBS]
 // run in Cantor coordinates.
 constexpr int kEncBigMaxGen = 4;
 
-// Quads per thread whose scratch loads the top-level passes issue together.
-// Measured at config 4: 4 is +4 % on the encode (the passes are bound by
-// scratch traffic, not load latency), so 1.
-#ifndef NP_ENC_JB
-#define NP_ENC_JB 1
-#endif
-constexpr int kEncJB = NP_ENC_JB;
 
 template <int KB>
 constexpr size_t enc_scratch() {
-  return 2u * (KB / kS) * kSegScr;  // M (SUBS sub-segments) + W (SUBS sub-segments)
+  return (2u * (KB / kS) - 1u) * kSegScr;  // M (SUBS sub-segments) + W_1.. (SUBS - 1)
 }
 
 template <int KB>
@@ -181,7 +189,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   const uint8_t* pay = a.payloads + static_cast<size_t>(pb) * a.payload_stride;
   uint8_t* out = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(ch0);
   uint8_t* scrM = scratch + static_cast<size_t>(blockIdx.x) * enc_scratch<KB>();
-  uint8_t* scrW = scrM + SUBS * kSegScr;
+  uint8_t* scrW = scrM + (SUBS - 1) * kSegScr;  // W_s at scrW + s slots, s >= 1
   const uint32_t tid = threadIdx.x, lane = tid & 63u, g = uniform(tid >> 6);
   const bool full =
       ncols == kTile && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
@@ -239,54 +247,59 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       constexpr int GEN = decltype(gc)::value;
       hi_levels<kS, true, GEN == 0, 0, GEN>(T, VP, index, XL, XH);
     });
-    scr_store<false>(scrM + s * kSegScr, tid, XL, XH);
+    if (s + 1 < static_cast<uint32_t>(SUBS)) {
+      scr_store<false>(scrM + s * kSegScr, tid, XL, XH);
+    } else {  // the last sub-segment waits in the LDS tile (thread order), not in the scratch
+      __syncthreads();  // every wave has read the tile
+      scr_store<false>(tile, tid, XL, XH);
+    }
   }
-
   // ---- phase 2: top inverse levels at index 0 -> coefficients M (in place;
-  // sub-segment 0 is unchanged: every level-8/9 butterfly at index 0 keeps lo)
+  // sub-segment 0 is unchanged: every level-8/9 butterfly at index 0 keeps lo).
+  // Each thread reads back only what it wrote: no barrier.
+  {
+    const TopMults<SUBS> tm = top_mults<SUBS>(T, 0u);
 #pragma unroll 1
-  for (uint32_t j0 = 0; j0 < 16; j0 += kEncJB) {
-    uint2 x[kEncJB][SUBS];  // kEncJB quads' loads in flight at once
+    for (uint32_t j = 0; j < 16; ++j) {
+      uint2 x[SUBS];
 #pragma unroll
-    for (int u = 0; u < kEncJB; ++u)
+      for (int r = 0; r + 1 < SUBS; ++r) x[r] = scr_q<false>(scrM + r * kSegScr, j, tid);
+      x[SUBS - 1] = scr_q<false>(tile, j, tid);
+      top_inverse<SUBS>(x, 0u, tm);
 #pragma unroll
-      for (int s = 0; s < SUBS; ++s) x[u][s] = scr_q<false>(scrM + s * kSegScr, j0 + u, tid);
-#pragma unroll
-    for (int u = 0; u < kEncJB; ++u) {
-      top_inverse<SUBS>(T, x[u], 0u);
-#pragma unroll
-      for (int s = 1; s < SUBS; ++s) scr_q_store<false>(scrM + s * kSegScr, j0 + u, tid, x[u][s]);
+      for (int r = 1; r < SUBS; ++r) scr_q_store<false>(scrM + r * kSegScr, j, tid, x[r]);
     }
   }
 
-  // ---- phase 3: every shift c = 1.. : top forward levels, then SUBS x FFT(256)
+  // ---- phase 3: every shift c = 1.. : top forward levels, then SUBS x FFT(256).
+  // W_0 waits in the LDS tile (thread order) for the first sub-segment's
+  // transform, W_1.. in the scratch: the kernel is bound by its scratch traffic.
   const uint32_t nshift = a.n / KB;
 #pragma unroll 1
   for (uint32_t c = 1; c < nshift; ++c) {
     if (c * KB >= a.wanted_n) break;
+    const TopMults<SUBS> tm = top_mults<SUBS>(T, c);
+    __syncthreads();  // the previous transform is done with the tile
 #pragma unroll 1
-    for (uint32_t j0 = 0; j0 < 16; j0 += kEncJB) {
-      uint2 w[kEncJB][SUBS];
+    for (uint32_t j = 0; j < 16; ++j) {
+      uint2 w[SUBS];
 #pragma unroll
-      for (int u = 0; u < kEncJB; ++u)
+      for (int r = 0; r < SUBS; ++r) w[r] = scr_q<false>(scrM + r * kSegScr, j, tid);
+      top_forward<SUBS>(w, c, tm);
+      scr_q_store<false>(tile, j, tid, w[0]);
 #pragma unroll
-        for (int s = 0; s < SUBS; ++s) w[u][s] = scr_q<false>(scrM + s * kSegScr, j0 + u, tid);
-#pragma unroll
-      for (int u = 0; u < kEncJB; ++u) {
-        top_forward<SUBS>(T, w[u], c);
-#pragma unroll
-        for (int s = 0; s < SUBS; ++s) scr_q_store<NP_W_NT>(scrW + s * kSegScr, j0 + u, tid, w[u][s]);
-      }
+      for (int r = 1; r < SUBS; ++r) scr_q_store<NP_W_NT>(scrW + r * kSegScr, j, tid, w[r]);
     }
 #pragma unroll 1
     for (uint32_t s = 0; s < SUBS; ++s) {
       const uint32_t index = c * KB + 256u * s;
       if (index >= a.wanted_n) break;
-      __syncthreads();  // the tile and the tables are free
+      uint32_t XL[16], XH[16];
+      if (s == 0) scr_load<false>(tile, tid, XL, XH);  // this thread's own W_0
+      __syncthreads();  // the tile (W_0 read) and the tables are free
       stage_vpools<kS, kTB>(T, index, VP, gen_of(index) <= kEncBigMaxGen);
       __syncthreads();
-      uint32_t XL[16], XH[16];
-      scr_load<NP_W_NT>(scrW + s * kSegScr, tid, XL, XH);
+      if (s != 0) scr_load<NP_W_NT>(scrW + s * kSegScr, tid, XL, XH);
       with_gen<1, kEncBigMaxGen, true>(index, [&](auto gc) __attribute__((always_inline)) {
         constexpr int GEN = decltype(gc)::value;
         if constexpr (GEN < 0) tower_convert(T, XL, XH);  // a far shift: Cantor coordinates
@@ -512,11 +525,12 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   // D's slots)
   // One quad position j: x0, z = D_256(y_0.) and the other segments' quads in,
   // e_s out.
+  const TopMults<SUBS> tm0 = top_mults<SUBS>(T, 0u);  // index 0: beta for SUBS = 4, nothing else
   auto fold = [&](uint32_t j, uint2 (&x0)[SUBS], uint2 (&z)[SUBS], uint2 (&yq)[NQ - 1][SUBS])
       __attribute__((always_inline)) {
     uint2 d[SUBS];
-    top_inverse<SUBS>(T, x0, 0u);
-    top_inverse<SUBS>(T, z, 0u);  // D_256 lifted
+    top_inverse<SUBS>(x0, 0u, tm0);
+    top_inverse<SUBS>(z, 0u, tm0);  // D_256 lifted
     // D_KB(x0)_s = (lifted D_256)_s ^ x0_{s | 2^m} for each high bit 256 2^m < KB clear in s
 #pragma unroll
     for (int s = 0; s < SUBS; ++s) {
@@ -544,7 +558,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
         if constexpr (q == 0) {
           accumulate(x0, kq);
         } else {
-          top_inverse<SUBS>(T, yq[q - 1], static_cast<uint32_t>(q));
+          top_inverse<SUBS>(yq[q - 1], static_cast<uint32_t>(q), top_mults<SUBS>(T, static_cast<uint32_t>(q)));
           accumulate(yq[q - 1], kq);
         }
       }
@@ -558,7 +572,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
       for (int s = 0; s < SUBS; ++s) qm(d[s], acc[b][s], m);
     }
-    top_forward<SUBS>(T, d, 0u);
+    top_forward<SUBS>(d, 0u, tm0);
 #pragma unroll
     for (int s = 0; s < SUBS; ++s) scr_q_store<true>(scrD + s * kSegScr, j, tid, d[s]);
   };
