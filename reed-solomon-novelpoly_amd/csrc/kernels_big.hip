@@ -442,9 +442,10 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   const uint32_t col0 = tl * kTile;
   const uint32_t ncols = min(static_cast<uint32_t>(kTile), nsyms - col0);
   const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);
-  // y_qs (SUBS NQ slots), then D_256(y_0s) (SUBS slots, reused for e_s)
-  uint8_t* scrY = scratch + static_cast<size_t>(blockIdx.x) * (SUBS * NQ + SUBS) * kSegScr;
-  uint8_t* scrD = scrY + SUBS * NQ * kSegScr;
+  // y_qs (SUBS NQ - 1 slots), then D_256(y_0s) (SUBS slots, reused for e_1..)
+  // (the last y slot is unused: that sub-segment waits in the LDS tile)
+  uint8_t* scrY = scratch + static_cast<size_t>(blockIdx.x) * (SUBS * NQ + SUBS - 1) * kSegScr;
+  uint8_t* scrD = scrY + (SUBS * NQ - 1) * kSegScr;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, g = uniform(tid >> 6);
   const bool full =
       ncols == kTile && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
@@ -511,7 +512,12 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       constexpr int GEN = decltype(gc)::value;
       hi_levels<kS, true, GEN == 0, 0, GEN>(T, VP, index, XL, XH);
     });
-    scr_store<true>(scrY + qs * kSegScr, tid, XL, XH);
+    if (qs + 1 < static_cast<uint32_t>(SUBS * NQ)) {
+      scr_store<true>(scrY + qs * kSegScr, tid, XL, XH);
+    } else {  // the last sub-segment waits in the LDS tile (thread order), not in the scratch
+      __syncthreads();  // every wave has read the tile
+      scr_store<false>(tile, tid, XL, XH);
+    }
     if (qs < static_cast<uint32_t>(SUBS)) {  // segment 0: also D_256(y_0s)
       uint32_t DL[16] = {0}, DH[16] = {0};
       add_derivative<kS>(DL, XL, tid % G::R);
@@ -573,8 +579,9 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       for (int s = 0; s < SUBS; ++s) qm(d[s], acc[b][s], m);
     }
     top_forward<SUBS>(d, 0u, tm0);
+    scr_q_store<false>(tile, j, tid, d[0]);  // over the slot this thread just read: e_0 waits in the tile
 #pragma unroll
-    for (int s = 0; s < SUBS; ++s) scr_q_store<true>(scrD + s * kSegScr, j, tid, d[s]);
+    for (int s = 1; s < SUBS; ++s) scr_q_store<true>(scrD + s * kSegScr, j, tid, d[s]);
   };
   constexpr int JB = kRecJB<NQ>;
 #pragma unroll 1
@@ -591,7 +598,9 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
       for (int q = 1; q < NQ; ++q)
 #pragma unroll
-        for (int s = 0; s < SUBS; ++s) yq[u][q - 1][s] = scr_q<true>(scrY + (SUBS * q + s) * kSegScr, j0 + u, tid);
+        for (int s = 0; s < SUBS; ++s)
+          yq[u][q - 1][s] = (q == NQ - 1 && s == SUBS - 1) ? scr_q<false>(tile, j0 + u, tid)  // this thread's own
+                                                           : scr_q<true>(scrY + (SUBS * q + s) * kSegScr, j0 + u, tid);
     }
 #pragma unroll
     for (int u = 0; u < JB; ++u) fold(j0 + u, x0[u], z[u], yq[u]);
@@ -601,11 +610,12 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll 1
   for (uint32_t s = 0; s < SUBS; ++s) {
     const uint32_t index = 256u * s;
-    __syncthreads();
+    uint32_t XL[16], XH[16];
+    if (s == 0) scr_load<false>(tile, tid, XL, XH);  // this thread's own e_0
+    __syncthreads();  // the tile (e_0 read) and the tables are free
     stage_vpools<kS, kTB>(T, index, VP, true);
     __syncthreads();
-    uint32_t XL[16], XH[16];
-    scr_load<true>(scrD + s * kSegScr, tid, XL, XH);
+    if (s != 0) scr_load<true>(scrD + s * kSegScr, tid, XL, XH);
     with_gen<0, 2, false>(index, [&](auto gc) __attribute__((always_inline)) {
       constexpr int GEN = decltype(gc)::value;
       hi_levels<kS, false, GEN == 0, 0, GEN>(T, VP, index, XL, XH);
@@ -722,7 +732,7 @@ bool big_reconstruct_supported(uint32_t n, uint32_t k) {
 size_t big_encode_scratch_per_tile(uint32_t k) { return k == 512 ? enc_scratch<512>() : enc_scratch<1024>(); }
 size_t big_reconstruct_scratch_per_tile(uint32_t n, uint32_t k) {
   const uint32_t subs = k / kS;
-  return static_cast<size_t>(subs) * (n / k + 1) * kSegScr;
+  return static_cast<size_t>(subs) * (n / k + 1) * kSegScr - kSegScr;
 }
 
 // Workgroups of the big kernels resident on the device at once (one per CU:
