@@ -482,6 +482,12 @@ __device__ __forceinline__ void copy_out_cq(uint8_t* out_tile, uint32_t lane, ui
   }
 }
 
+// The merge's systematic rows (4- and 8-segment decodes) load: 0 at the
+// merge, 1 before the forward transform's cq pass, 2 before its high pass.
+#ifndef NP_MERGE_EARLY
+#define NP_MERGE_EARLY 1  // measured: decode 0 to -2 % at config 3 (box to box), -4 % at n/k = 8, k = 64; 2: -0.9 %
+#endif
+
 // Row loads run one step ahead of their use where the registers allow it
 // (prefixes of up to 2 segments); the 4-segment decode, which keeps more
 // state live, loads each step's rows where it uses them.
@@ -501,9 +507,13 @@ constexpr bool kRowPrefetch = NQ <= 2;
 #ifndef NP_REC_RESIDENT
 #define NP_REC_RESIDENT 1
 #endif
+// Only where it keeps the workgroups per CU (4K threads each, four waves per
+// SIMD): K = 64 / 128 with NQ = 8 would lose one of four / two (measured +24 %
+// / +65 % decode time).
 template <int K, int NQ>
 constexpr bool kRecResident =
-    NP_REC_RESIDENT && NQ > 1 && Geo<K>::kTileBytes + NQ * 4u * Geo<K>::kVPWords <= 160u * 1024u;
+    NP_REC_RESIDENT && NQ > 1 &&
+    Geo<K>::kTileBytes + NQ * 4u * Geo<K>::kVPWords <= 160u * 1024u * Geo<K>::kThreads / 1024u;
 // LDS buffer of segment q's tables at decode step `step`.
 template <int K, int NQ>
 __device__ __forceinline__ uint32_t vp_slot(int q, int step) {
@@ -720,6 +730,8 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
     hi_write<K>(tile, fresh_v(hb), AL, AH);
     __syncthreads();
     stamp(dbg, 28);
+    if constexpr (!kRowPrefetch<NQ> && NP_MERGE_EARLY == 1)  // the merge's rows load during the FFT's cq pass
+      issue_rows(raw, sh, a.shard_len, uniform(msk[NQ - 1]), 16 * g, T.zeros, lane, ncols, full);
     cq_read<K>(tile, fresh_v(cqb), XL, XH);
     cq_levels<K, false, true, 0>(T, vp0, 0, g, XL, XH, ~uniform(msk[NQ - 1]));  // erased rows only
     stamp(dbg, 29);
@@ -727,7 +739,8 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
   // ---- merge: received systematic rows, postmultiplied recovered ones
   const uint32_t cqbf = fresh_v(cqb);
   const uint32_t m0 = uniform(msk[NQ == 1 ? 0 : NQ - 1]);  // segment 0 = the last step's
-  if constexpr (!kRowPrefetch<NQ>) issue_rows(raw, sh, a.shard_len, m0, 16 * g, T.zeros, lane, ncols, full);
+  if constexpr (!kRowPrefetch<NQ> && NP_MERGE_EARLY != 1)
+    issue_rows(raw, sh, a.shard_len, m0, 16 * g, T.zeros, lane, ncols, full);
   if constexpr (NQ == 1) {
 #pragma unroll
     for (int p = 0; p < 16; ++p) blk_to_quad(raw[p], XL[p], XH[p]);
@@ -885,12 +898,16 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
       // ---- forward transform of size K at index 0
       const uint32_t* vp0 = VP + vp_slot<K, NQ>(0, NQ - 1) * G::kVPWords;  // segment 0's tables = FFT(K, 0)'s
       stamp(dbg, 26);
+      if constexpr (!kRowPrefetch<NQ> && NP_MERGE_EARLY == 2)  // the merge's rows load during the FFT
+        issue_rows(raw, sh, shard_len, uniform(msk[NQ - 1]), 16 * g, T.zeros, lane, ncols, full);
       hi_levels<K, false, true, 0, 0>(T, vp0, 0, AL, AH);
       stamp(dbg, 27);
       __syncthreads();
       hi_write<K>(tile, fresh_v(hb), AL, AH);
       __syncthreads();
       stamp(dbg, 28);
+      if constexpr (!kRowPrefetch<NQ> && NP_MERGE_EARLY == 1)  // the merge's rows load during the FFT's cq pass
+        issue_rows(raw, sh, shard_len, uniform(msk[NQ - 1]), 16 * g, T.zeros, lane, ncols, full);
       cq_read<K>(tile, fresh_v(cqb), XL, XH);
       cq_levels<K, false, true, 0>(T, vp0, 0, g, XL, XH, ~uniform(msk[NQ - 1]));  // erased rows only
       stamp(dbg, 29);
@@ -898,7 +915,7 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
     // ---- merge: received systematic rows, postmultiplied recovered ones
     const uint32_t cqbf = fresh_v(cqb);
     const uint32_t m0 = uniform(msk[NQ == 1 ? 0 : NQ - 1]);  // segment 0 = the last step's
-    if constexpr (!kRowPrefetch<NQ>) issue_rows(raw, sh, shard_len, m0, 16 * g, T.zeros, lane, ncols, full);
+    if constexpr (!kRowPrefetch<NQ> && !NP_MERGE_EARLY) issue_rows(raw, sh, shard_len, m0, 16 * g, T.zeros, lane, ncols, full);
     if constexpr (NQ == 1) {
 #pragma unroll
       for (int p = 0; p < 16; ++p) blk_to_quad(raw[p], XL[p], XH[p]);
