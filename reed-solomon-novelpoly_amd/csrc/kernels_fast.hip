@@ -435,23 +435,31 @@ __device__ __forceinline__ uint32_t row_mask16(const uint8_t* pres, uint32_t row
   return static_cast<uint32_t>(__ballot(p));
 }
 
-// Row loads keep the default policy: the merge re-reads the systematic rows
-// (streaming loads measured +0.5 % on the decode).
+// Row loads: streaming (nt) for rows read once -- the parity segments' rows
+// and the merge's final read of the systematic rows -- and the default policy
+// for segment 0's systematic rows, which the merge reads again, so that the
+// parity rows do not push them (and the payload's row-table records, re-read
+// by every tile) out of L2.  NP_ROW_STREAM 0: every load default (all-nt
+// measured +0.5 % on the decode in round 1).
 #ifndef NP_ROW_LOAD_CPOL
 #define NP_ROW_LOAD_CPOL 0
+#endif
+#ifndef NP_ROW_STREAM
+#define NP_ROW_STREAM 1
 #endif
 // Issues the loads of the lane's pieces of rows row0..row0+15; the data is
 // consumed later.  Full tiles: one buffer descriptor per row whose size is 0
 // for an absent row, so that load returns zeros with no HBM traffic and no
 // branch.  Partial tiles: absent rows read the zero page.
-__device__ __forceinline__ void issue_rows(uint2 (&raw)[16], const uint8_t* sh, size_t shard_len, uint32_t mask,
-                                           uint32_t row0, const uint8_t* zeros, uint32_t lane, uint32_t ncols,
-                                           bool full) {
+template <int CPOL>
+__device__ __forceinline__ void issue_rows_c(uint2 (&raw)[16], const uint8_t* sh, size_t shard_len, uint32_t mask,
+                                             uint32_t row0, const uint8_t* zeros, uint32_t lane, uint32_t ncols,
+                                             bool full) {
   if (full) {
 #pragma unroll
     for (int p = 0; p < 16; ++p) {
       const __amdgpu_buffer_rsrc_t r = buf_rsrc(sh + static_cast<size_t>(row0 + p) * shard_len, ((mask >> p) & 1u) ? 512u : 0u);
-      const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, 8u * lane, 0, NP_ROW_LOAD_CPOL);
+      const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, 8u * lane, 0, CPOL);
       raw[p] = make_uint2(v.x, v.y);
     }
   } else {
@@ -461,6 +469,16 @@ __device__ __forceinline__ void issue_rows(uint2 (&raw)[16], const uint8_t* sh, 
       raw[p] = load4(src, lane, ncols, false);
     }
   }
+}
+
+// reread: the rows are read again later (segment 0 before the merge).
+__device__ __forceinline__ void issue_rows(uint2 (&raw)[16], const uint8_t* sh, size_t shard_len, uint32_t mask,
+                                           uint32_t row0, const uint8_t* zeros, uint32_t lane, uint32_t ncols,
+                                           bool full, bool reread = false) {
+  if (NP_ROW_STREAM && !reread)
+    issue_rows_c<2>(raw, sh, shard_len, mask, row0, zeros, lane, ncols, full);
+  else
+    issue_rows_c<NP_ROW_LOAD_CPOL>(raw, sh, shard_len, mask, row0, zeros, lane, ncols, full);
 }
 
 // Copy-out straight from the cq registers: lane l holds columns 4l..4l+3 at
@@ -563,7 +581,7 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
     m = uniform(m);
     if constexpr (!kRowPrefetch<NQ>) {
       issue_rows(raw, (kExp & 32) ? T.zeros : sh, (kExp & 32) ? 0 : shard_len, m, index + 16 * g, T.zeros, c.lane,
-                 c.ncols, c.full);
+                 c.ncols, c.full, q == 0);
     }
     uint32_t XL[16], XH[16];
     stamp(c.dbg, 2 + 6 * step);
@@ -616,7 +634,7 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
       }
       if (step + 1 == NQ) mn = msk[NQ - 1], qn = 0;  // segment 0 is the last step's
       issue_rows(raw, (kExp & 32) ? T.zeros : sh, (kExp & 32) ? 0 : shard_len, uniform(mn), uniform(qn) * K + 16 * g,
-                 T.zeros, c.lane, c.ncols, c.full);
+                 T.zeros, c.lane, c.ncols, c.full, qn == 0 && step + 1 < NQ);
     }
     __syncthreads();
     stamp(c.dbg, 5 + 6 * step);
