@@ -18,6 +18,9 @@ pytestmark = pytest.mark.gpu
 # (n_wanted, k_wanted) -> effective k in {64, 128, 256}, n in {2k, 4k, 8k}
 SHAPES = [(1024, 342), (512, 256), (2048, 300), (256, 86), (512, 128), (256, 128), (768, 256), (300, 100),
           (700, 234)]
+# k in {512, 1024} (kernels_big.hip), n in {2k, 4k, 8k}; shorter payloads (the
+# oracle's size-8192 transforms are slow)
+SHAPES_BIG = [(2000, 667), (1024, 512), (2500, 834), (4096, 1366), (5000, 1667), (2048, 1024)]
 
 
 def _erasures(rng, n, k, mode):
@@ -31,19 +34,28 @@ def _erasures(rng, n, k, mode):
     return pres
 
 
-@pytest.mark.parametrize("case", range(12))
+@pytest.mark.parametrize("case", range(24))
 def test_fuzz_device_batch_roundtrip(gpu, oracle, monkeypatch, case):
+    _fuzz(gpu, oracle, monkeypatch, case, SHAPES, [3, 300, 900], 10)
+
+
+@pytest.mark.parametrize("case", range(16))
+def test_fuzz_big_device_batch_roundtrip(gpu, oracle, monkeypatch, case):
+    _fuzz(gpu, oracle, monkeypatch, 100 + case, SHAPES_BIG, [1, 3, 24], 5)
+
+
+def _fuzz(gpu, oracle, monkeypatch, case, shapes, chunk_counts, max_batch):
     import torch
 
     rng = np.random.default_rng(1000 + case)
-    nw, kw = SHAPES[case % len(SHAPES)]
+    nw, kw = shapes[case % len(shapes)]
     p = npa.CodeParams.derive_parameters(nw, kw)
     n, k = p.n(), p.k()
     wanted = n if case % 3 else int(rng.integers(n // 2 + 1, n + 1))
     monkeypatch.setenv("NP_ENC_TPW", str(int(rng.integers(1, 6))))
     monkeypatch.setenv("NP_REC_TPW", str(int(rng.integers(1, 6))))
-    batch = int(rng.integers(1, 10))
-    plen = int(rng.integers(1, 2 * k * int(rng.choice([3, 300, 900]))))
+    batch = int(rng.integers(1, max_batch))
+    plen = int(rng.integers(1, 2 * k * int(rng.choice(chunk_counts))))
     pstride = plen + int(rng.choice([0, 0, 1, 8, 13]))
     sl = p.make_encoder(gpu).shard_len(plen)
     # device encode writes the n-row layout; rows >= wanted are not produced
