@@ -1000,10 +1000,11 @@ __device__ __forceinline__ void add_derivative(uint32_t (&A)[16], uint32_t (&X)[
   }
 }
 
-// Cantor <-> tower coordinates of 16 quads (an involution, field_tables.hpp
+// Cantor <-> tower coordinates of NR quads (an involution, field_tables.hpp
 // HostTables::tower_a): the low plane takes A(high plane), 3 byte lookups of
 // the high plane through the b slots of tower_pools[kFieldSize].
-__device__ __forceinline__ void tower_convert(const DevTables& T, uint32_t (&L)[16], const uint32_t (&H)[16]) {
+template <int NR>
+__device__ __forceinline__ void tower_convert(const DevTables& T, uint32_t (&L)[NR], const uint32_t (&H)[NR]) {
 #ifdef NP_NO_CONVERT
   return;
 #endif
@@ -1013,7 +1014,7 @@ __device__ __forceinline__ void tower_convert(const DevTables& T, uint32_t (&L)[
   asm volatile("v_mov_b64 %0, %1" : "=v"(vv) : "s"((static_cast<uint64_t>(q[3]) << 32) | q[2]));
   const uint32_t va = static_cast<uint32_t>(vv), vb = static_cast<uint32_t>(vv >> 32);
 #pragma unroll
-  for (int p = 0; p < 16; ++p) {
+  for (int p = 0; p < NR; ++p) {
     uint32_t s0, s1, s2;  // one asm block: no quad's selectors are computed far ahead of its lookups
     asm volatile(
         "v_and_b32 %0, 0x07070707, %3\n\t"

@@ -1238,11 +1238,12 @@ hipError_t by_nq(const ReconstructArgs& a, F f) {
 }  // namespace
 
 bool fast_encode_supported(uint32_t n, uint32_t k) {
-  return (k == 64 || k == 128 || k == 256) && n >= 2 * k && n <= 65536;
+  return ((k == 64 || k == 128 || k == 256) && n >= 2 * k && n <= 65536) || small_encode_supported(n, k);
 }
 
 bool fast_reconstruct_supported(uint32_t n, uint32_t k) {
-  return (k == 64 || k == 128 || k == 256) && (n == 2 * k || n == 4 * k || n == 8 * k);
+  return ((k == 64 || k == 128 || k == 256) && (n == 2 * k || n == 4 * k || n == 8 * k)) ||
+         small_reconstruct_supported(n, k);
 }
 
 hipError_t launch_encode_fast(const DevTables& T, const EncodeArgs& a, hipStream_t s) {
@@ -1250,6 +1251,9 @@ hipError_t launch_encode_fast(const DevTables& T, const EncodeArgs& a, hipStream
     case 64: return launch_encode_k<64>(T, a, s);
     case 128: return launch_encode_k<128>(T, a, s);
     case 256: return launch_encode_k<256>(T, a, s);
+    case 8:
+    case 16:
+    case 32: return launch_encode_small(T, a, s);
     default: return hipErrorNotSupported;
   }
 }
@@ -1261,6 +1265,9 @@ hipError_t launch_prefix_locator(const DevTables& T, const ReconstructArgs& a, u
     case 64: return by_nq<64>(a, [&](auto K, auto NQ) { return launch_prefix_k<K.value, NQ.value>(T, a, out, s); });
     case 128: return by_nq<128>(a, [&](auto K, auto NQ) { return launch_prefix_k<K.value, NQ.value>(T, a, out, s); });
     case 256: return by_nq<256>(a, [&](auto K, auto NQ) { return launch_prefix_k<K.value, NQ.value>(T, a, out, s); });
+    case 8: return by_nq<8>(a, [&](auto K, auto NQ) { return launch_prefix_k<K.value, NQ.value>(T, a, out, s); });
+    case 16: return by_nq<16>(a, [&](auto K, auto NQ) { return launch_prefix_k<K.value, NQ.value>(T, a, out, s); });
+    case 32: return by_nq<32>(a, [&](auto K, auto NQ) { return launch_prefix_k<K.value, NQ.value>(T, a, out, s); });
     default: return hipErrorNotSupported;
   }
 }
@@ -1270,6 +1277,9 @@ hipError_t launch_reconstruct_fast(const DevTables& T, const ReconstructArgs& a,
     case 64: return by_nq<64>(a, [&](auto K, auto NQ) { return launch_reconstruct_k<K.value, NQ.value>(T, a, s); });
     case 128: return by_nq<128>(a, [&](auto K, auto NQ) { return launch_reconstruct_k<K.value, NQ.value>(T, a, s); });
     case 256: return by_nq<256>(a, [&](auto K, auto NQ) { return launch_reconstruct_k<K.value, NQ.value>(T, a, s); });
+    case 8:
+    case 16:
+    case 32: return launch_reconstruct_small(T, a, s);
     default: return hipErrorNotSupported;
   }
 }

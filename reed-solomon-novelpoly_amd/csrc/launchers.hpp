@@ -86,6 +86,13 @@ hipError_t launch_reconstruct_fast(const DevTables& T, const ReconstructArgs& a,
 size_t prefix_stride(uint32_t n, uint32_t k);
 hipError_t launch_prefix_locator(const DevTables& T, const ReconstructArgs& a, uint8_t* out, hipStream_t s);
 
+// ---- k in {8, 16, 32} (kernels_small.hip), served through the fast-path entry
+// points above (the same per-payload records from launch_prefix_locator) ----
+bool small_encode_supported(uint32_t n, uint32_t k);       // 2k <= n <= 8k
+bool small_reconstruct_supported(uint32_t n, uint32_t k);  // n / k in {2, 4, 8}
+hipError_t launch_encode_small(const DevTables& T, const EncodeArgs& a, hipStream_t s);
+hipError_t launch_reconstruct_small(const DevTables& T, const ReconstructArgs& a, hipStream_t s);
+
 // ---- k = 512, 1024 (kernels_big.hip): per-workgroup scratch, launches split to fit it ----
 bool big_encode_supported(uint32_t n, uint32_t k);
 bool big_reconstruct_supported(uint32_t n, uint32_t k);  // n / k in {2, 4, 8}

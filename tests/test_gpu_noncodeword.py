@@ -23,11 +23,14 @@ pytestmark = pytest.mark.gpu
 # (n_wanted, k_wanted, shard_len): config 2 (n256 k64), config 3 (n1024 k256),
 # config 4 (n4096 k1024), n/k = 8 (n512 k64, n1024 k128, n2048 k256), n/k = 2
 # (n1024 k256 with wanted_n 600; n2048 k1024), k = 512 (n1024, n2048, n4096)
-# and n/k = 8 at k = 1024 (n8192); shard lengths of one full 256-column tile
+# and n/k = 8 at k = 1024 (n8192); k in {8, 16, 32} (n128 k32, n256 k32, n64
+# k16, n64 k8, n16 k8, n64 k32); shard lengths of one full 256-column tile
 # plus a partial one
 SHAPES = [(256, 86, 2 * 300), (1024, 342, 2 * 300), (4096, 1366, 2 * 260), (300, 100, 2 * 270),
           (700, 234, 2 * 300), (1200, 400, 2 * 290), (600, 256, 2 * 280), (2048, 1024, 2 * 270),
-          (1024, 512, 2 * 270), (2000, 667, 2 * 260), (2500, 834, 2 * 270), (5000, 1667, 2 * 260)]
+          (1024, 512, 2 * 270), (2000, 667, 2 * 260), (2500, 834, 2 * 270), (5000, 1667, 2 * 260),
+          (100, 34, 2 * 300), (150, 50, 2 * 270), (60, 20, 2 * 260), (40, 14, 2 * 280), (16, 8, 2 * 300),
+          (64, 32, 2 * 257)]
 
 
 def _dev(a):
@@ -170,7 +173,8 @@ def test_device_need_more_shards_status(gpu, oracle, nw, kw, sl):
     assert o2[0].tobytes() == want and (o2[1:] == 0x5A).all()
 
 
-@pytest.mark.parametrize("nw,kw,plen", [(1024, 342, 512 * 300 + 1), (256, 86, 128 * 256), (512, 128, 256 * 257)])
+@pytest.mark.parametrize("nw,kw,plen", [(1024, 342, 512 * 300 + 1), (256, 86, 128 * 256), (512, 128, 256 * 257),
+                                        (100, 34, 64 * 300 + 1), (60, 20, 32 * 257)])
 def test_codewords_entry_on_codewords(gpu, oracle, nw, kw, plen):
     """The opt-in np_reconstruct_codewords_batch_dev (2k-row prefix decode on
     n = 4k shapes) equals the reference on unmodified codewords, in every
@@ -191,6 +195,8 @@ def test_codewords_entry_on_codewords(gpu, oracle, nw, kw, plen):
     pres = np.ones(n, np.uint8)
     pres[rng.choice(2 * k, k + 1, replace=False)] = 0
     pats.append(pres)
+    for pres in pats:
+        pres[nw:] = 0  # rows >= wanted_n were never produced
     batch = len(pats)
     sl = p.make_encoder(gpu).shard_len(plen)
     pls = np.stack([np.frombuffer(synth.payload(77 + b, plen), np.uint8) for b in range(batch)])

@@ -355,9 +355,60 @@ def test_fast_reconstruct_shapes(gpu, oracle, nw, kw, plen, erase):
     assert got[:plen] == pl
 
 
+# k in {8, 16, 32} (kernels_small.hip): validator counts 16..190, n / k in
+# {2, 4, 8}, wanted_n < n (last shift partly kept), full / partial / tail tiles
+SMALL_ENC = [(100, 34, 64 * 256), (100, 34, 64 * 300 + 5), (150, 50, 64 * 512), (190, 63, 64 * 257 + 1),
+             (64, 32, 64 * 256), (60, 20, 32 * 256), (90, 30, 32 * 257 + 3), (40, 14, 16 * 256),
+             (16, 8, 4096), (30, 10, 999), (24, 8, 16 * 768), (48, 16, 1), (33, 11, 16 * 256 * 5 + 9)]
+
+
+@pytest.mark.parametrize("nw,kw,plen", SMALL_ENC)
+def test_small_encode_shapes(gpu, oracle, nw, kw, plen):
+    """Register-only encode kernels for k in {8, 16, 32}, bit-exact against the
+    oracle."""
+    p = npa.CodeParams.derive_parameters(nw, kw)
+    assert p.k() in (8, 16, 32) and p.is_faster8()
+    pl = synth.payload(nw + plen, plen)
+    got = p.make_encoder(gpu).encode(pl)
+    st, want = oracle.encode(pl, p.n(), p.k(), nw)
+    assert st == 0
+    bad = [v for v in range(nw) if got[v] != want[v]]
+    assert not bad, f"{len(bad)} shards differ, first {bad[:5]}"
+
+
+@pytest.mark.parametrize("nw,kw,plen,erase", [(100, 34, 64 * 256, 66), (100, 34, 64 * 300 + 5, 40),
+                                              (100, 34, 64 * 256, -1), (150, 50, 64 * 512, 100),
+                                              (190, 63, 64 * 257 + 1, 120), (190, 63, 64 * 256, -1),
+                                              (64, 32, 64 * 256, 32), (64, 32, 64 * 99, -1),
+                                              (60, 20, 32 * 256, 40), (90, 30, 32 * 257 + 3, 60),
+                                              (40, 14, 16 * 256, 26), (40, 14, 16 * 300 + 1, -1),
+                                              (16, 8, 4096, 8), (16, 8, 4096, -1), (30, 10, 999, 20),
+                                              (24, 8, 16 * 768, 16), (100, 34, 64 * 256, 0)])
+def test_small_reconstruct_shapes(gpu, oracle, nw, kw, plen, erase):
+    """Register-only reconstruct kernels for k in {8, 16, 32}, n in {2k, 4k,
+    8k}: random and worst-case erasure sets (-1: every systematic shard lost),
+    bit-exact against the oracle."""
+    p = npa.CodeParams.derive_parameters(nw, kw)
+    n, k = p.n(), p.k()
+    assert k in (8, 16, 32) and n in (2 * k, 4 * k, 8 * k)
+    pl = synth.payload(7 * nw + plen, plen)
+    shards = p.make_encoder(gpu).encode(pl)
+    if erase == -1:
+        gone = set(range(k))
+    else:
+        gone = set(synth.erasure_indices(plen + erase, nw, min(erase, nw - k)).tolist())
+    recv = [None if i in gone else s for i, s in enumerate(shards[:nw])]
+    assert sum(r is not None for r in recv) >= k
+    got = p.make_encoder(gpu).reconstruct(recv)
+    st, want = oracle.reconstruct(recv, n, k)
+    assert st == 0 and got == want
+    assert got[:plen] == pl
+
+
 @pytest.mark.parametrize("nw,kw,plen,batch", [(1024, 342, 512 * 300, 5), (256, 86, 128 * 256 + 7, 9),
                                               (512, 256, 512 * 256, 3), (2048, 512, 1024 * 40, 2),
-                                              (300, 100, 128 * 300, 4), (1200, 400, 512 * 260, 3)])
+                                              (300, 100, 128 * 300, 4), (1200, 400, 512 * 260, 3),
+                                              (100, 34, 64 * 300, 4), (60, 20, 32 * 256 + 1, 3)])
 def test_device_reconstruct_locator_modes(gpu, oracle, nw, kw, plen, batch):
     """np_reconstruct_batch_dev2 with locators from np_error_locator_dev and with
     d_locators = NULL (computed on the device: fused folded locator on the fast
@@ -421,7 +472,8 @@ def _prefix_patterns(n, k, rng):
 
 
 @pytest.mark.parametrize("nw,kw,plen", [(1024, 342, 512 * 256), (1024, 342, 512 * 37 + 3), (256, 86, 128 * 256),
-                                        (512, 256, 512 * 256), (256, 128, 256 * 99)])
+                                        (512, 256, 512 * 256), (256, 128, 256 * 99), (128, 34, 64 * 256),
+                                        (64, 14, 16 * 300 + 3), (64, 32, 64 * 257)])
 def test_reconstruct_prefix_modes(gpu, oracle, nw, kw, plen):
     """Fast reconstruct with the locator computed in the kernel picks the shortest
     row prefix (k, 2k or n rows) that holds k present rows; every mode gives the
