@@ -159,7 +159,7 @@ np::EncodeArgs enc_args(const np_code_params* p, const uint8_t* payloads, size_t
   return a;
 }
 
-constexpr size_t kBigScratchCap = size_t(1) << 30;  // bytes of big-kernel scratch per context
+constexpr size_t kBigScratchCap = size_t(2) << 30;  // bytes of big-kernel scratch per context (k = 2048 decode: 256 slots of 4.9 MiB)
 
 // Big-kernel scratch of `want` bytes (capped), ordered after every earlier
 // big launch of this context on any stream.  Caller holds the context lock.

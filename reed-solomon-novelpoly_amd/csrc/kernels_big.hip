@@ -1,10 +1,11 @@
-// Specialised gfx950 kernels for k = 512 and k = 1024 (BASELINE config 4:
-// n = 4096, k = 1024; 1,366-2,730 validators: k = 512).
+// Specialised gfx950 kernels for k = 512, 1024 and 2048 (BASELINE config 4:
+// n = 4096, k = 1024; 1,366-2,730 validators: k = 512; 6,144-8,192: k =
+// 2048).
 //
 // A 256-column tile of a size-KB transform needs KB/2 KiB, more than the LDS
 // holds, so a workgroup (1024 threads, the K = 256 register layouts of
 // fast_common.hpp) runs the transform as SUBS = KB / 256 size-256 sub-segments
-// plus the top levels (8, and 9 for KB = 1024) that mix them:
+// plus the top levels (8, 9 for KB >= 1024, 10 for KB = 2048) that mix them:
 //
 //   phase 1  per sub-segment: LDS tile -> column-quad levels 0..3 -> high-layout
 //            levels 4..7 -> registers -> per-workgroup scratch in HBM / L2;
@@ -98,60 +99,85 @@ __device__ __forceinline__ void qx(uint2& x, const uint2& y) {
 }
 
 // The multipliers of the top levels of a size-(256 SUBS) transform at index
-// 256 SUBS q: level 8 group t skew Cantor(q SUBS + 2t), level 9 (SUBS = 4)
-// skew Cantor(2q); all in GF(2^8).  Loaded once per pass over the 16 quads.
+// 256 SUBS q: level 8 + L (L < log2 SUBS) has SUBS / 2^(L+1) groups, group t
+// with skew Cantor(q SUBS / 2^L + 2t), at m[top_off(L) + t]; all in GF(2^8).
+// Loaded once per pass over the 16 quads.
+__host__ __device__ constexpr int top_off(int subs, int L) { return subs - (subs >> L); }
+__host__ __device__ constexpr uint32_t top_skew(int subs, int L, uint32_t q, int t) {
+  return q * static_cast<uint32_t>(subs >> L) + 2u * t;
+}
 template <int SUBS>
 struct TopMults {
-  Mult m8[SUBS / 2];
-  Mult m9;
+  Mult m[SUBS - 1];
 };
 template <int SUBS>
 __device__ __forceinline__ TopMults<SUBS> top_mults(const DevTables& T, uint32_t q) {
   TopMults<SUBS> m;
 #pragma unroll
-  for (int t = 0; t < SUBS / 2; ++t)
-    if (q * SUBS + 2u * t) m.m8[t] = tmult(T, q * SUBS + 2u * t);
-  if constexpr (SUBS == 4) {
-    if (q) m.m9 = tmult(T, 2u * q);
-  }
+  for (int L = 0; (1 << L) < SUBS; ++L)
+#pragma unroll
+    for (int t = 0; t < (SUBS >> (L + 1)); ++t)
+      if (top_skew(SUBS, L, q, t)) m.m[top_off(SUBS, L) + t] = tmult(T, top_skew(SUBS, L, q, t));
   return m;
 }
 
-// Top inverse levels (8, then 9 for SUBS = 4) on one position quad of each
-// sub-segment: inverse butterfly hi ^= lo; lo ^= c hi.  q is a compile-time
-// constant at the q = 0 calls, so their zero skews fold.
+// Top inverse levels (8, 9, ...) on one position quad of each sub-segment:
+// inverse butterfly hi ^= lo; lo ^= c hi.  q is a compile-time constant at
+// the q = 0 calls, so their zero skews fold.
 template <int SUBS>
 __device__ __forceinline__ void top_inverse(uint2 (&y)[SUBS], uint32_t q, const TopMults<SUBS>& m) {
 #pragma unroll
-  for (int t = 0; t < SUBS / 2; ++t) {
-    qx(y[2 * t + 1], y[2 * t]);
-    if (q * SUBS + 2u * t) qm(y[2 * t], y[2 * t + 1], m.m8[t]);
+  for (int L = 0; (1 << L) < SUBS; ++L) {
+    const int d = 1 << L;
+#pragma unroll
+    for (int t = 0; t < (SUBS >> (L + 1)); ++t)
+#pragma unroll
+      for (int u = 0; u < d; ++u) {
+        const int x = 2 * d * t + u;
+        qx(y[x + d], y[x]);
+        if (top_skew(SUBS, L, q, t)) qm(y[x], y[x + d], m.m[top_off(SUBS, L) + t]);
+      }
   }
-  if constexpr (SUBS == 4) {
-    qx(y[2], y[0]);
-    qx(y[3], y[1]);
-    if (q) {
-      qm(y[0], y[2], m.m9);
-      qm(y[1], y[3], m.m9);
+}
+
+// The same with each group's multiplier fetched where it is used (SUBS = 8:
+// holding all seven across the pass would cost 28 VGPRs); T comes from
+// fresh_tables at the call, so the fetches are not hoisted out of its loop.
+template <int SUBS>
+__device__ __forceinline__ void top_inverse_fetch(const DevTables& T, uint2 (&y)[SUBS], uint32_t q) {
+#pragma unroll
+  for (int L = 0; (1 << L) < SUBS; ++L) {
+    const int d = 1 << L;
+#pragma unroll
+    for (int t = 0; t < (SUBS >> (L + 1)); ++t) {
+      const uint32_t c = top_skew(SUBS, L, q, t);
+      Mult m;
+      if (c) m = tmult(T, c);
+#pragma unroll
+      for (int u = 0; u < d; ++u) {
+        const int x = 2 * d * t + u;
+        qx(y[x + d], y[x]);
+        if (c) qm(y[x], y[x + d], m);
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 }
 
-// Top forward levels at index 256 SUBS c (level 9, then 8): lo ^= c hi; hi ^= lo.
+// Top forward levels at index 256 SUBS c (highest first): lo ^= c hi; hi ^= lo.
 template <int SUBS>
 __device__ __forceinline__ void top_forward(uint2 (&w)[SUBS], uint32_t c, const TopMults<SUBS>& m) {
-  if constexpr (SUBS == 4) {
-    if (c) {
-      qm(w[0], w[2], m.m9);
-      qm(w[1], w[3], m.m9);
-    }
-    qx(w[2], w[0]);
-    qx(w[3], w[1]);
-  }
 #pragma unroll
-  for (int t = 0; t < SUBS / 2; ++t) {
-    if (c * SUBS + 2u * t) qm(w[2 * t], w[2 * t + 1], m.m8[t]);
-    qx(w[2 * t + 1], w[2 * t]);
+  for (int L = ilog2(SUBS) - 1; L >= 0; --L) {
+    const int d = 1 << L;
+#pragma unroll
+    for (int t = 0; t < (SUBS >> (L + 1)); ++t)
+#pragma unroll
+      for (int u = 0; u < d; ++u) {
+        const int x = 2 * d * t + u;
+        if (top_skew(SUBS, L, c, t)) qm(w[x], w[x + d], m.m[top_off(SUBS, L) + t]);
+        qx(w[x + d], w[x]);
+      }
   }
 }
 
@@ -166,6 +192,13 @@ __device__ __forceinline__ void top_forward(uint2 (&w)[SUBS], uint32_t c, const 
 // levels below gen_of(index) with the full map.  Farther shifts of larger codes
 // run in Cantor coordinates.
 constexpr int kEncBigMaxGen = 4;
+// k = 2048 (n <= 8192): every shift in tower coordinates (index < 8192).
+template <int KB>
+constexpr int kEncBigMaxGenK = KB == 2048 ? 5 : kEncBigMaxGen;
+// Highest gen_of of a sub-segment transform at index 256 s, s < SUBS (at
+// least 2: the instances the k = 512 / 1024 kernels were tuned with).
+template <int KB>
+constexpr int kSubMaxGen = gen_of(KB - 256) > 2 ? static_cast<int>(gen_of(KB - 256)) : 2;
 
 
 template <int KB>
@@ -234,7 +267,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       cq_read<kS>(tile, cq, CL, CH);
       store_rows(out, a.shard_len, index + 16 * g, a.wanted_n, CL, CH, lane, ncols, full);  // systematic rows
       tower_convert(T, CL, CH);  // the transforms run in tower coordinates
-      with_gen<0, 2, false>(index, [&](auto gc) __attribute__((always_inline)) {
+      with_gen<0, kSubMaxGen<KB>, false>(index, [&](auto gc) __attribute__((always_inline)) {
         constexpr int GEN = decltype(gc)::value;  // 0 only at index 0
         cq_levels<kS, true, GEN == 0, GEN>(T, VP, index, g, CL, CH);
       });
@@ -243,7 +276,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
     __syncthreads();
     uint32_t XL[16], XH[16];
     hi_read<kS>(tile, fresh_v(hb), XL, XH);
-    with_gen<0, 2, false>(index, [&](auto gc) __attribute__((always_inline)) {
+    with_gen<0, kSubMaxGen<KB>, false>(index, [&](auto gc) __attribute__((always_inline)) {
       constexpr int GEN = decltype(gc)::value;
       hi_levels<kS, true, GEN == 0, 0, GEN>(T, VP, index, XL, XH);
     });
@@ -297,10 +330,10 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       uint32_t XL[16], XH[16];
       if (s == 0) scr_load<false>(tile, tid, XL, XH);  // this thread's own W_0
       __syncthreads();  // the tile (W_0 read) and the tables are free
-      stage_vpools<kS, kTB>(T, index, VP, gen_of(index) <= kEncBigMaxGen);
+      stage_vpools<kS, kTB>(T, index, VP, gen_of(index) <= kEncBigMaxGenK<KB>);
       __syncthreads();
       if (s != 0) scr_load<NP_W_NT>(scrW + s * kSegScr, tid, XL, XH);
-      with_gen<1, kEncBigMaxGen, true>(index, [&](auto gc) __attribute__((always_inline)) {
+      with_gen<1, kEncBigMaxGenK<KB>, true>(index, [&](auto gc) __attribute__((always_inline)) {
         constexpr int GEN = decltype(gc)::value;
         if constexpr (GEN < 0) tower_convert(T, XL, XH);  // a far shift: Cantor coordinates
         hi_levels<kS, false, false, 0, GEN>(T, VP, index, XL, XH);
@@ -308,7 +341,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       hi_write<kS>(tile, fresh_v(hb), XL, XH);
       __syncthreads();
       cq_read<kS>(tile, fresh_v(cqb), XL, XH);
-      with_gen<1, kEncBigMaxGen, true>(index, [&](auto gc) __attribute__((always_inline)) {
+      with_gen<1, kEncBigMaxGenK<KB>, true>(index, [&](auto gc) __attribute__((always_inline)) {
         constexpr int GEN = decltype(gc)::value;
         cq_levels<kS, false, false, GEN>(T, VP, index, g, XL, XH);
         if constexpr (GEN >= 0) tower_convert(T, XL, XH);  // back to Cantor coordinates for the rows
@@ -583,6 +616,59 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
     for (int s = 1; s < SUBS; ++s) scr_q_store<true>(scrD + s * kSegScr, j, tid, d[s]);
   };
+  if constexpr (SUBS >= 8) {
+    // k = 2048: the segments stream through the fold one at a time (the
+    // per-bit sums and every segment's quads at once exceed the 128 VGPRs of
+    // a 1024-thread workgroup): d ^= kappa_q y_q, one multiply per segment.
+#pragma unroll 1
+    for (uint32_t j = 0; j < 16; ++j) {
+      uint2 d[SUBS];
+      {
+        uint2 x0[SUBS], z[SUBS];
+#pragma unroll
+        for (int s = 0; s < SUBS; ++s) {
+          x0[s] = scr_q<true>(scrY + s * kSegScr, j, tid);
+          z[s] = scr_q<true>(scrD + s * kSegScr, j, tid);
+        }
+        top_inverse<SUBS>(x0, 0u, tm0);
+        top_inverse<SUBS>(z, 0u, tm0);  // D_256 lifted
+#pragma unroll
+        for (int s = 0; s < SUBS; ++s) {
+          d[s] = z[s];
+#pragma unroll
+          for (int m = 1; m < SUBS; m <<= 1)
+            if (!(s & m)) qx(d[s], x0[s | m]);
+          if constexpr (big_kappa<NQ>(0) == 1u) qx(d[s], x0[s]);  // kappa_0 in {0, 1}
+        }
+      }
+      for_each_q(std::make_integer_sequence<int, NQ>{}, [&](auto qc) __attribute__((always_inline)) {
+        constexpr int q = decltype(qc)::value;
+        constexpr uint32_t kq = big_kappa<NQ>(q);
+        if constexpr (q > 0 && kq != 0) {
+          __builtin_amdgcn_sched_barrier(0);
+          const DevTables Tq = fresh_tables(T);
+          uint2 y[SUBS];
+#pragma unroll
+          for (int s = 0; s < SUBS; ++s)
+            y[s] = (q == NQ - 1 && s == SUBS - 1) ? scr_q<false>(tile, j, tid)  // this thread's own
+                                                   : scr_q<true>(scrY + (SUBS * q + s) * kSegScr, j, tid);
+          top_inverse_fetch<SUBS>(Tq, y, static_cast<uint32_t>(q));
+          if constexpr (kq == 1u) {
+#pragma unroll
+            for (int s = 0; s < SUBS; ++s) qx(d[s], y[s]);
+          } else {
+            const Mult m = tmult(Tq, kq);
+#pragma unroll
+            for (int s = 0; s < SUBS; ++s) qm(d[s], y[s], m);
+          }
+        }
+      });
+      top_forward<SUBS>(d, 0u, tm0);
+      scr_q_store<false>(tile, j, tid, d[0]);  // over the slot this thread just read: e_0 waits in the tile
+#pragma unroll
+      for (int s = 1; s < SUBS; ++s) scr_q_store<true>(scrD + s * kSegScr, j, tid, d[s]);
+    }
+  } else {
   constexpr int JB = kRecJB<NQ>;
 #pragma unroll 1
   for (uint32_t j0 = 0; j0 < 16; j0 += JB) {
@@ -605,6 +691,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
     for (int u = 0; u < JB; ++u) fold(j0 + u, x0[u], z[u], yq[u]);
   }
+  }
 
   // ---- phase 3: FFT(256, 256 s) of e_s, postmultiply erased rows, copy out
 #pragma unroll 1
@@ -616,7 +703,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
     stage_vpools<kS, kTB>(T, index, VP, true);
     __syncthreads();
     if (s != 0) scr_load<true>(scrD + s * kSegScr, tid, XL, XH);
-    with_gen<0, 2, false>(index, [&](auto gc) __attribute__((always_inline)) {
+    with_gen<0, kSubMaxGen<KB>, false>(index, [&](auto gc) __attribute__((always_inline)) {
       constexpr int GEN = decltype(gc)::value;
       hi_levels<kS, false, GEN == 0, 0, GEN>(T, VP, index, XL, XH);
     });
@@ -625,7 +712,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
     {
       const uint32_t gg = fresh(g), cq = fresh_v(cqb);
       cq_read<kS>(tile, cq, XL, XH);
-      with_gen<0, 2, false>(index, [&](auto gc) __attribute__((always_inline)) {
+      with_gen<0, kSubMaxGen<KB>, false>(index, [&](auto gc) __attribute__((always_inline)) {
         constexpr int GEN = decltype(gc)::value;
         cq_levels<kS, false, GEN == 0, GEN>(T, VP, index, gg, XL, XH);
       });
@@ -719,17 +806,24 @@ bool with_rec_big(uint32_t n, uint32_t k, F&& f) {
     if (n == 2048) return f(&k_reconstruct_big<1024, 2>, &k_big_records<1024, 2048>), true;
     if (n == 4096) return f(&k_reconstruct_big<1024, 4>, &k_big_records<1024, 4096>), true;
     if (n == 8192) return f(&k_reconstruct_big<1024, 8>, &k_big_records<1024, 8192>), true;
+  } else if (k == 2048) {  // n = 16384 (the records' locator would need 112 KiB of LDS): generic
+    if (n == 4096) return f(&k_reconstruct_big<2048, 2>, &k_big_records<2048, 4096>), true;
+    if (n == 8192) return f(&k_reconstruct_big<2048, 4>, &k_big_records<2048, 8192>), true;
   }
   return false;
 }
 
 }  // namespace
 
-bool big_encode_supported(uint32_t n, uint32_t k) { return (k == 512 || k == 1024) && n >= 2 * k && n <= 65536; }
+bool big_encode_supported(uint32_t n, uint32_t k) {
+  return (k == 512 || k == 1024 || k == 2048) && n >= 2 * k && n <= 65536;
+}
 bool big_reconstruct_supported(uint32_t n, uint32_t k) {
   return with_rec_big(n, k, [](auto, auto) {});
 }
-size_t big_encode_scratch_per_tile(uint32_t k) { return k == 512 ? enc_scratch<512>() : enc_scratch<1024>(); }
+size_t big_encode_scratch_per_tile(uint32_t k) {
+  return k == 512 ? enc_scratch<512>() : k == 1024 ? enc_scratch<1024>() : enc_scratch<2048>();
+}
 size_t big_reconstruct_scratch_per_tile(uint32_t n, uint32_t k) {
   const uint32_t subs = k / kS;
   return static_cast<size_t>(subs) * (n / k + 1) * kSegScr - kSegScr;
@@ -782,8 +876,11 @@ hipError_t launch_encode_big(const DevTables& T, const EncodeArgs& a, uint8_t* s
     if (a.k == 512)
       k_encode_big<512><<<blocks, kTB, enc_big_lds(), s>>>(T, a, static_cast<uint32_t>(nchunks), tiles,
                                                             static_cast<uint32_t>(t0), scratch);
-    else
+    else if (a.k == 1024)
       k_encode_big<1024><<<blocks, kTB, enc_big_lds(), s>>>(T, a, static_cast<uint32_t>(nchunks), tiles,
+                                                             static_cast<uint32_t>(t0), scratch);
+    else
+      k_encode_big<2048><<<blocks, kTB, enc_big_lds(), s>>>(T, a, static_cast<uint32_t>(nchunks), tiles,
                                                              static_cast<uint32_t>(t0), scratch);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -832,7 +929,8 @@ hipError_t configure_big_kernels() {
   };
   set(reinterpret_cast<const void*>(&k_encode_big<512>), enc_big_lds());
   set(reinterpret_cast<const void*>(&k_encode_big<1024>), enc_big_lds());
-  for (uint32_t k : {512u, 1024u})
+  set(reinterpret_cast<const void*>(&k_encode_big<2048>), enc_big_lds());
+  for (uint32_t k : {512u, 1024u, 2048u})
     for (uint32_t nq : {2u, 4u, 8u})
       with_rec_big(nq * k, k, [&](auto kern, auto) { set(reinterpret_cast<const void*>(kern), rec_big_lds(nq * k)); });
   return e;

@@ -20,7 +20,8 @@ SHAPES = [(1024, 342), (512, 256), (2048, 300), (256, 86), (512, 128), (256, 128
           (700, 234)]
 # k in {512, 1024} (kernels_big.hip), n in {2k, 4k, 8k}; shorter payloads (the
 # oracle's size-8192 transforms are slow)
-SHAPES_BIG = [(2000, 667), (1024, 512), (2500, 834), (4096, 1366), (5000, 1667), (2048, 1024)]
+SHAPES_BIG = [(2000, 667), (1024, 512), (2500, 834), (4096, 1366), (5000, 1667), (2048, 1024), (7000, 2334),
+              (4096, 2048)]
 # k in {8, 16, 32} (kernels_small.hip)
 SHAPES_SMALL = [(100, 34), (150, 50), (60, 20), (90, 30), (40, 14), (16, 8), (30, 10), (64, 32), (190, 63)]
 
@@ -41,7 +42,7 @@ def test_fuzz_device_batch_roundtrip(gpu, oracle, monkeypatch, case):
     _fuzz(gpu, oracle, monkeypatch, case, SHAPES, [3, 300, 900], 10)
 
 
-@pytest.mark.parametrize("case", range(16))
+@pytest.mark.parametrize("case", range(24))
 def test_fuzz_big_device_batch_roundtrip(gpu, oracle, monkeypatch, case):
     _fuzz(gpu, oracle, monkeypatch, 100 + case, SHAPES_BIG, [1, 3, 24], 5)
 

@@ -302,9 +302,11 @@ def test_big_path_launch_rounds(gpu, oracle, batch, plen):
                                         (2048, 1024, 2048 * 100), (3000, 1024, 5000),
                                         (1024, 512, 1024 * 100 + 3), (2000, 667, 1024 * 256),
                                         (2000, 667, 1024 * 300 + 5), (2500, 834, 1024 * 256 + 1),
-                                        (5000, 1667, 2048 * 64 + 1), (1500, 512, 999)])
+                                        (5000, 1667, 2048 * 64 + 1), (1500, 512, 999),
+                                        (7000, 2334, 4096 * 256 + 3), (4096, 2048, 4096 * 40),
+                                        (6144, 2048, 4096 * 300 + 1), (9000, 3000, 4096 * 3 + 5)])
 def test_fast_encode_shapes(gpu, oracle, nw, kw, plen):
-    """Specialised encode kernels (k in {64,128,256}; k in {512,1024} in
+    """Specialised encode kernels (k in {64,128,256}; k in {512,1024,2048} in
     kernels_big.hip): single/multi/partial tiles, odd payload tails, wanted_n < n
     and n/k in {2,4,8}."""
     p = npa.CodeParams.derive_parameters(nw, kw)
@@ -332,15 +334,17 @@ def test_fast_encode_shapes(gpu, oracle, nw, kw, plen):
                                               (2000, 667, 1024 * 257 + 9, -1), (2500, 834, 1024 * 260 + 1, 1666),
                                               (2500, 834, 1024 * 256, -1), (5000, 1667, 2048 * 40 + 3, 3333),
                                               (5000, 1667, 2048 * 33, -1), (2000, 667, 1024 * 256 + 5, 0),
-                                              (4096, 1366, 2048 * 256, 0)])
+                                              (4096, 1366, 2048 * 256, 0), (7000, 2334, 4096 * 256 + 3, 4666),
+                                              (7000, 2334, 4096 * 100, -1), (4096, 2048, 4096 * 40, 2048),
+                                              (8192, 2731, 4096 * 257, 5461), (7000, 2334, 4096 * 30, 0)])
 def test_fast_reconstruct_shapes(gpu, oracle, nw, kw, plen, erase):
-    """Specialised reconstruct kernels (k in {64,128,256} fast, {512,1024} big;
-    n in {2k,4k,8k}): full
+    """Specialised reconstruct kernels (k in {64,128,256} fast, {512,1024} big
+    with n in {2k,4k,8k}, 2048 big with n in {2k, 4k}): full
     and partial column tiles, random and worst-case erasure sets (erase = -1:
     every systematic shard lost), bit-exact against the oracle."""
     p = npa.CodeParams.derive_parameters(nw, kw)
     n, k = p.n(), p.k()
-    assert n in (2 * k, 4 * k, 8 * k) and k in (64, 128, 256, 512, 1024)
+    assert n in (2 * k, 4 * k, 8 * k) and k in (64, 128, 256, 512, 1024, 2048)
     pl = synth.payload(7 * nw + plen, plen)
     shards = p.make_encoder(gpu).encode(pl)
     if erase == -1:
