@@ -169,7 +169,8 @@ int main(int argc, char** argv) {
   for (int t = 0; t < threads; ++t) {
     Worker* w = &ws[t];
     w->payload = malloc(PLEN), w->out = malloc(2 * K * CHUNKS), w->shards = malloc(N * SHARD_LEN);
-    w->data = malloc(K * sizeof(uint16_t)), w->cw = malloc(N * sizeof(uint16_t));
+    /* data: n symbols, zero beyond k (encode_low reads n: inc_encode.rs:18, :193-196) */
+    w->data = calloc(N, sizeof(uint16_t)), w->cw = malloc(N * sizeof(uint16_t));
     w->loc = malloc(FIELD * sizeof(uint16_t)), w->erased = calloc(FIELD, sizeof(int));
     w->erased8 = calloc(FIELD, 1), w->perm = malloc(N * sizeof(uint32_t));
   }
@@ -183,5 +184,11 @@ int main(int argc, char** argv) {
   const double dt = now() - t0;
   printf("{\"kind\": \"%s\", \"payloads\": %ld, \"seconds\": %.3f, \"threads\": %d, \"gib_s\": %.6f, \"failures\": %d}\n",
          KIND, done, dt, threads, done * (double)PLEN / dt / (1024.0 * 1024.0 * 1024.0), atomic_load(&failures));
+  for (int t = 0; t < threads; ++t) {
+    Worker* w = &ws[t];
+    free(w->payload), free(w->out), free(w->shards), free(w->data), free(w->cw);
+    free(w->loc), free(w->erased), free(w->erased8), free(w->perm);
+  }
+  free(ws), free(th);
   return atomic_load(&failures) ? 1 : 0;
 }

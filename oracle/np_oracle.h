@@ -59,6 +59,7 @@ void npo_walsh(uint16_t* data, size_t size);
 void npo_afft(uint16_t* data, size_t size, size_t index);
 void npo_inverse_afft(uint16_t* data, size_t size, size_t index);
 void npo_formal_derivative(uint16_t* data, size_t size);
+/* data holds n symbols (the message zero-padded from k to n, inc_encode.rs:18) */
 void npo_encode_low(const uint16_t* data, size_t k, uint16_t* codeword, size_t n);
 int  npo_encode_sub(const uint8_t* bytes, size_t len, size_t n, size_t k, uint16_t* codeword_out);
 void npo_eval_error_polynomial(const uint8_t* erasures, size_t n_erasures, uint16_t* locator_out /*65536*/);

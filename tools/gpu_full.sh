@@ -3,7 +3,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
 tail -2 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ]; then grep -E "FAILED|Error|assert" gpurun_out/pytest_gpu.log | head -20; exit $rc; fi
 timeout -k 10 300 python bench.py --steps 5 --warmup 2 --cpu-seconds 3 > gpurun_out/bench.log 2>&1 || exit $?
