@@ -849,6 +849,12 @@ __device__ __forceinline__ void with_gen(uint32_t index, F&& f) {
   with_gen_from<(MING > 0 ? MING : 0), MAXG, FALLBACK>(g, f);
 }
 
+#ifndef NP_CQ_LIVE_ALL
+#define NP_CQ_LIVE_ALL 1  // measured: encode -2 % (no phi copies around the g == 0 skip branches; the zero element's table yields 0)
+#endif
+#ifndef NP_CQ_NO_SKIP
+#define NP_CQ_NO_SKIP 0
+#endif
 // GEN: coordinates and subfield levels (kSubLevel).
 template <int K, bool INVERSE, bool INDEX0, int GEN = -1>
 __device__ __forceinline__ void cq_levels(const DevTables& T, const uint32_t* VP, uint32_t index, uint32_t g,
@@ -865,9 +871,9 @@ __device__ __forceinline__ void cq_levels(const DevTables& T, const uint32_t* VP
   auto group = [&](auto fc, const Mult& p) __attribute__((always_inline)) {
     constexpr GroupRef r = cq_group<INVERSE>(decltype(fc)::value);
     constexpr int d = 1 << r.b;
-    const bool live = !INDEX0 || r.t != 0 || g != 0;  // c == 0: the skew sentinel, no product
+    const bool live = NP_CQ_LIVE_ALL || !INDEX0 || r.t != 0 || g != 0;  // c == 0: the skew sentinel, no product
     constexpr uint32_t span = ((1u << (2 * d)) - 1u) << (r.t * 2 * d);  // the group's rows
-    if ((rows & span) == 0) return;
+    if (!NP_CQ_NO_SKIP && (rows & span) == 0) return;
     auto body = [&](auto sub_c) __attribute__((always_inline)) {
       constexpr bool SUB = decltype(sub_c)::value;
 #pragma unroll
