@@ -291,7 +291,10 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
   const uint32_t ncols = min(static_cast<uint32_t>(kTile), nchunks - ch0);
   const uint8_t* pay = a.payloads + static_cast<size_t>(pb) * a.payload_stride;
   uint8_t* out = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(ch0);
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, g = uniform(tid >> 6);
+  // opaque per tile: otherwise the lane-derived addresses of the loads, DMA and
+  // row guards are hoisted out of the tile loop and spilled, and each reload
+  // (a VMEM op) waits with vmcnt(0) for the DMA and every row store before it
+  const uint32_t tid = fresh_v(threadIdx.x), lane = tid & 63u, g = uniform(tid >> 6);
   const bool full =
       ncols == kTile && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
   const bool aligned_pay = (reinterpret_cast<uintptr_t>(pay) & 7u) == 0;
@@ -556,6 +559,26 @@ __device__ __forceinline__ void stage_rec_tables(const DevTables& T, uint32_t* V
   }
 }
 
+// msk[step] (16-bit row masks, wave-uniform) through shifts of packed scalars:
+// a select chain over msk[] becomes a dynamically indexed private array, i.e.
+// a scratch load whose vmcnt(0) wait also waits for every row load and store
+// issued before it.
+template <int NQ>
+__device__ __forceinline__ uint32_t seg_mask(const uint32_t (&msk)[NQ], int step) {
+  if constexpr (NQ <= 2) return step == 0 ? msk[0] : msk[NQ - 1];  // one select (the packed form spills here)
+  uint64_t lo = 0, hi = 0;
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    const uint64_t v = static_cast<uint64_t>(msk[i] & 0xffffu);
+    if (i < 4)
+      lo |= v << (16 * i);
+    else
+      hi |= v << (16 * (i - 4));
+  }
+  const uint32_t sh = 16u * static_cast<uint32_t>(step & 3);
+  return static_cast<uint32_t>(((step < 4 ? lo : hi) >> sh) & 0xffffu);
+}
+
 // The segment sweep: x_q = IFFT(K, qK)(premultiplied segment q), folded into
 // A.  With kRowPrefetch `raw` holds segment seg_of(0)'s rows on entry and the
 // systematic rows (for the merge) on exit.  A runtime loop keeps
@@ -575,10 +598,7 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
     const uint32_t* R = fresh(c.R);
     const size_t shard_len = fresh(c.shard_len);
     const uint32_t cqb = fresh_v(c.cqb), hb = fresh_v(c.hb);
-    uint32_t m = msk[0];
-#pragma unroll
-    for (int i = 1; i < NQ; ++i) m = step == i ? msk[i] : m;
-    m = uniform(m);
+    uint32_t m = uniform(seg_mask<NQ>(msk, step));
     if constexpr (!kRowPrefetch<NQ>) {
       issue_rows(raw, (kExp & 32) ? T.zeros : sh, (kExp & 32) ? 0 : shard_len, m, index + 16 * g, T.zeros, c.lane,
                  c.ncols, c.full, q == 0);
