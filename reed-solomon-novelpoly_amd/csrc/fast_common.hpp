@@ -754,8 +754,10 @@ __host__ __device__ constexpr uint32_t vslot(int b, uint32_t t) {
 // tw: tower_pools (the transform runs in tower coordinates), else perm_pools.
 template <int K, int NT>
 __device__ __forceinline__ void stage_vpools(const DevTables& T, uint32_t index, uint32_t* VP, bool tw = false) {
-  const uint32_t* pools = tw ? T.tower_pools : T.perm_pools;
-  for (uint32_t i = threadIdx.x; i < 2u * (K - 1); i += NT) {
+  // scalar base (a select the compiler may otherwise do per lane, in a VGPR
+  // pair that gets spilled across the callers' loops)
+  const uint32_t* pools = fresh(tw ? T.tower_pools : T.perm_pools);
+  for (uint32_t i = fresh_v(threadIdx.x); i < 2u * (K - 1); i += NT) {
     const uint32_t slot = i >> 1, half = i & 1u;
     uint32_t b = 0;
     while (slot >= static_cast<uint32_t>(K - (K >> (b + 1)))) ++b;

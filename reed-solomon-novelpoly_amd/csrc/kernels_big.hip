@@ -234,6 +234,8 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   // ---- phase 1: x_s = IFFT(256, 256 s)(sub-segment s of every chunk)
 #pragma unroll 1
   for (uint32_t s = 0; s < SUBS; ++s) {
+    // per iteration, opaque: lane-derived addresses are not hoisted and spilled
+    const uint32_t tid = fresh_v(threadIdx.x), lane = tid & 63u;
     const uint32_t index = 256u * s;
     __syncthreads();  // previous sub-segment is done with the tile and the tables
     stage_vpools<kS, kTB>(T, index, VP, true);
@@ -294,6 +296,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
     const TopMults<SUBS> tm = top_mults<SUBS>(T, 0u);
 #pragma unroll 1
     for (uint32_t j = 0; j < 16; ++j) {
+      const uint32_t tid = fresh_v(threadIdx.x);
       uint2 x[SUBS];
 #pragma unroll
       for (int r = 0; r + 1 < SUBS; ++r) x[r] = scr_q<false>(scrM + r * kSegScr, j, tid);
@@ -315,6 +318,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
     __syncthreads();  // the previous transform is done with the tile
 #pragma unroll 1
     for (uint32_t j = 0; j < 16; ++j) {
+      const uint32_t tid = fresh_v(threadIdx.x);
       uint2 w[SUBS];
 #pragma unroll
       for (int r = 0; r < SUBS; ++r) w[r] = scr_q<false>(scrM + r * kSegScr, j, tid);
@@ -327,6 +331,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
     for (uint32_t s = 0; s < SUBS; ++s) {
       const uint32_t index = c * KB + 256u * s;
       if (index >= a.wanted_n) break;
+      const uint32_t tid = fresh_v(threadIdx.x), lane = tid & 63u;
       uint32_t XL[16], XH[16];
       if (s == 0) scr_load<false>(tile, tid, XL, XH);  // this thread's own W_0
       __syncthreads();  // the tile (W_0 read) and the tables are free
@@ -407,14 +412,17 @@ __device__ __forceinline__ void tile_copy_out(const ReconstructArgs& a, const ui
   using G = Geo<kS>;
   uint8_t* outp = a.out + static_cast<size_t>(pb) * a.out_stride + static_cast<size_t>(col0) * 2 * KB + 512u * s;
   const bool al_o = ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 7u) == 0;
-  const uint32_t tid = threadIdx.x, c0 = tid / G::Q, m0 = tid % G::Q;
+  // opaque thread id, one output pointer stepped per column: otherwise the 16
+  // per-lane 64-bit column addresses are hoisted out of the callers' loops and
+  // spilled, and every reload waits (vmcnt(0)) for the stores before it
+  const uint32_t tid = fresh_v(threadIdx.x), c0 = tid / G::Q, m0 = tid % G::Q;
   const uint32_t base = col_base<kS>(c0) ^ (8u * m0);
+  uint8_t* o = outp + static_cast<size_t>(c0) * 2 * KB + 8u * m0;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
+  for (int i = 0; i < 16; ++i, o += 16u * 2 * KB) {
     const uint32_t c = c0 + 16u * i;
     if (c >= ncols) break;
     const uint2 v = *reinterpret_cast<const uint2*>(tile + (base ^ col_base_c<kS>(16u * i)));
-    uint8_t* o = outp + static_cast<size_t>(c) * 2 * KB + 8u * m0;
     if (al_o) {
       store_once(o, v);
     } else {
@@ -501,6 +509,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   for (uint32_t qs = 0; qs < static_cast<uint32_t>(SUBS * NQ); ++qs) {
     const uint32_t index = 256u * qs;  // = KB q + 256 s
     const uint32_t gg = fresh(g);
+    const uint32_t tid = fresh_v(threadIdx.x), lane = tid & 63u;  // opaque: not hoisted and spilled
     // the sub-segment's present rows load while the tables are staged
     uint2 rows[2][8];
 #pragma unroll
@@ -567,6 +576,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   const TopMults<SUBS> tm0 = top_mults<SUBS>(T, 0u);  // index 0: beta for SUBS = 4, nothing else
   auto fold = [&](uint32_t j, uint2 (&x0)[SUBS], uint2 (&z)[SUBS], uint2 (&yq)[NQ - 1][SUBS])
       __attribute__((always_inline)) {
+    const uint32_t tid = fresh_v(threadIdx.x);
     uint2 d[SUBS];
     top_inverse<SUBS>(x0, 0u, tm0);
     top_inverse<SUBS>(z, 0u, tm0);  // D_256 lifted
@@ -622,6 +632,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
     // a 1024-thread workgroup): d ^= kappa_q y_q, one multiply per segment.
 #pragma unroll 1
     for (uint32_t j = 0; j < 16; ++j) {
+      const uint32_t tid = fresh_v(threadIdx.x);
       uint2 d[SUBS];
       {
         uint2 x0[SUBS], z[SUBS];
@@ -672,6 +683,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   constexpr int JB = kRecJB<NQ>;
 #pragma unroll 1
   for (uint32_t j0 = 0; j0 < 16; j0 += JB) {
+    const uint32_t tid = fresh_v(threadIdx.x);
     // every quad of JB positions in flight at once (one latency per JB positions)
     uint2 x0[JB][SUBS], z[JB][SUBS], yq[JB][NQ - 1][SUBS];
 #pragma unroll
@@ -697,6 +709,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll 1
   for (uint32_t s = 0; s < SUBS; ++s) {
     const uint32_t index = 256u * s;
+    const uint32_t tid = fresh_v(threadIdx.x), lane = tid & 63u;
     uint32_t XL[16], XH[16];
     if (s == 0) scr_load<false>(tile, tid, XL, XH);  // this thread's own e_0
     __syncthreads();  // the tile (e_0 read) and the tables are free
