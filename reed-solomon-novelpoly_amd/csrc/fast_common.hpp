@@ -1011,6 +1011,17 @@ __device__ __forceinline__ void add_derivative(uint32_t (&A)[16], uint32_t (&X)[
 // Cantor <-> tower coordinates of NR quads (an involution, field_tables.hpp
 // HostTables::tower_a): the low plane takes A(high plane), 3 byte lookups of
 // the high plane through the b slots of tower_pools[kFieldSize].
+// The VGPR half (dwords 2..3) of the conversion's table, by a scalar load: the
+// compiler otherwise reads it with a vector load (it cannot prove that the row
+// stores do not alias the tables), and that load's vmcnt(0) wait also waits
+// for every row store issued before it.
+__device__ __forceinline__ uint64_t tower_conv_vhalf(cpool_t q) {
+  uint64_t s23, vv;
+  asm volatile("s_load_dwordx2 %0, %1, 0x8\n\ts_waitcnt lgkmcnt(0)" : "=s"(s23) : "s"(q) : "memory");
+  asm volatile("v_mov_b64 %0, %1" : "=v"(vv) : "s"(s23));
+  return vv;
+}
+
 template <int NR>
 __device__ __forceinline__ void tower_convert(const DevTables& T, uint32_t (&L)[NR], const uint32_t (&H)[NR]) {
 #ifdef NP_NO_CONVERT
@@ -1018,8 +1029,7 @@ __device__ __forceinline__ void tower_convert(const DevTables& T, uint32_t (&L)[
 #endif
   const cpool_t q = (cpool_t)(T.tower_pools) + 65536u * kPoolWords;
   const uint32_t sa = q[8 + 3], sb = q[8 + 4], sc = q[8 + 5];
-  uint64_t vv;
-  asm volatile("v_mov_b64 %0, %1" : "=v"(vv) : "s"((static_cast<uint64_t>(q[3]) << 32) | q[2]));
+  const uint64_t vv = tower_conv_vhalf(q);
   const uint32_t va = static_cast<uint32_t>(vv), vb = static_cast<uint32_t>(vv >> 32);
 #pragma unroll
   for (int p = 0; p < NR; ++p) {

@@ -115,8 +115,7 @@ template <int NR>
 __device__ __forceinline__ void tower_convert_q(const DevTables& T, uint64_t (&Q)[NR]) {
   const cpool_t q = (cpool_t)(T.tower_pools) + 65536u * kPoolWords;
   const uint32_t sa = q[8 + 3], sb = q[8 + 4], sc = q[8 + 5];
-  uint64_t vv;
-  asm volatile("v_mov_b64 %0, %1" : "=v"(vv) : "s"((static_cast<uint64_t>(q[3]) << 32) | q[2]));
+  const uint64_t vv = tower_conv_vhalf(q);
   const uint32_t va = static_cast<uint32_t>(vv), vb = static_cast<uint32_t>(vv >> 32);
 #pragma unroll
   for (int p = 0; p < NR; ++p) {
