@@ -1142,6 +1142,47 @@ __device__ __forceinline__ void hi_write_p(uint8_t* tile, uint32_t base, const u
   for (int j = 0; j < 16; ++j) *reinterpret_cast<uint2*>(tile + (base ^ (8u * Geo<K>::R * j))) = make_uint2(L[j], H[j]);
 }
 
+// Quad exchange between the cq layout and a column-quad high layout (K = 256,
+// the multi-tile encode): LDS item (position p, column quad c) = the uint2
+// (low plane, high plane) of columns 4c..4c+3 at position p, at byte
+// 8 (64 p + c).  cq side: wave g, lane c holds positions 16 g + i.  High side:
+// wave r, lane c holds positions r + 16 j, so level b >= 4 pairs registers j
+// and j + 2^(b-4) with group j >> (b-3), as hi_levels expects, and no byte
+// transpose is needed on either side (tr4x4).  Every wave-instruction moves
+// 512 contiguous bytes.
+__device__ __forceinline__ void cq_write_q(uint8_t* tile, uint32_t g, uint32_t lane, const uint32_t (&L)[16],
+                                           const uint32_t (&H)[16]) {
+  uint8_t* b = tile + 8192u * g + fresh_v(8u * lane);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) *reinterpret_cast<uint2*>(b + 512u * i) = make_uint2(L[i], H[i]);
+}
+__device__ __forceinline__ void cq_read_q(const uint8_t* tile, uint32_t g, uint32_t lane, uint32_t (&L)[16],
+                                          uint32_t (&H)[16]) {
+  const uint8_t* b = tile + 8192u * g + fresh_v(8u * lane);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const uint2 d = *reinterpret_cast<const uint2*>(b + 512u * i);
+    L[i] = d.x;
+    H[i] = d.y;
+  }
+}
+__device__ __forceinline__ void hi_write_q(uint8_t* tile, uint32_t r, uint32_t lane, const uint32_t (&L)[16],
+                                           const uint32_t (&H)[16]) {
+  uint8_t* b = tile + 512u * r + fresh_v(8u * lane);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) *reinterpret_cast<uint2*>(b + 8192u * j) = make_uint2(L[j], H[j]);
+}
+__device__ __forceinline__ void hi_read_q(const uint8_t* tile, uint32_t r, uint32_t lane, uint32_t (&L)[16],
+                                          uint32_t (&H)[16]) {
+  const uint8_t* b = tile + 512u * r + fresh_v(8u * lane);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint2 d = *reinterpret_cast<const uint2*>(b + 8192u * j);
+    L[j] = d.x;
+    H[j] = d.y;
+  }
+}
+
 // ---------------------------------------------------------------- locator ----
 // eval_error_polynomial (inc_reconstruct.rs:90-113, called over the whole field
 // by mod.rs:217-218) for an erasure set inside [0, N), folded to N points

@@ -209,6 +209,11 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
 // live in registers across the tile loop.
 template <int K>
 constexpr bool kMultiTile = K == 256;
+// The multi-tile encode exchanges layouts through quad items (cq_write_q ..
+// hi_read_q, fast_common.hpp): no byte transposes.
+#ifndef NP_ENC_QX
+#define NP_ENC_QX 1
+#endif
 
 // Table buffers of the multi-tile encode: the inverse transform's and one per
 // shift, staged once per workgroup (n <= 4K); with the 128 KiB tile they fill
@@ -268,9 +273,15 @@ __device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArg
   const uint32_t* vp = VP + sh * G::kVPWords;  // the tables of every shift stay staged (kEncBuffers)
   shift_hi<K, SH>(T, vp, index, ML, MH, XL, XH, PL, PH);
   __syncthreads();  // the previous cq pass is done with the tile
-  hi_write_p<K>(tile, fresh_v(hb), XL, XH);
-  __syncthreads();
-  cq_read_p<K>(tile, fresh_v(cqb), XL, XH);
+  if constexpr (NP_ENC_QX) {
+    hi_write_q(tile, g, lane, XL, XH);
+    __syncthreads();
+    cq_read_q(tile, g, lane, XL, XH);
+  } else {
+    hi_write_p<K>(tile, fresh_v(hb), XL, XH);
+    __syncthreads();
+    cq_read_p<K>(tile, fresh_v(cqb), XL, XH);
+  }
   if (dma_pay) {
     __syncthreads();  // every wave has its cq registers: the tile is free
     if constexpr (!(kExp & 4)) dma_tile<K>(dma_pay, dma_ch0, tile, g, lane);
@@ -345,12 +356,18 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
     store_rows(out, a.shard_len, 16 * g, (kExp & 2) ? 0u : a.wanted_n, CL, CH, lane, ncols, full);
     tower_convert(T, CL, CH);  // transforms run in tower coordinates
     cq_levels<K, true, true, 0>(T, VP, 0, g, CL, CH);
-    cq_write_p<K>(tile, cqb, CL, CH);
+    if constexpr (NP_ENC_QX)
+      cq_write_q(tile, g, lane, CL, CH);
+    else
+      cq_write_p<K>(tile, cqb, CL, CH);
   }
   __syncthreads();
   const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
   uint32_t ML[16], MH[16];
-  hi_read_p<K>(tile, hb, ML, MH);
+  if constexpr (NP_ENC_QX)
+    hi_read_q(tile, g, lane, ML, MH);
+  else
+    hi_read_p<K>(tile, hb, ML, MH);
   hi_levels<K, true, true, 0, 0>(T, VP, 0, ML, MH);
 #pragma unroll
   for (int q = 0; q < 16; ++q) asm volatile("" : "+v"(ML[q]), "+v"(MH[q]));  // materialise M once
