@@ -100,6 +100,14 @@ __device__ __forceinline__ void shift_cq(const DevTables& T, const uint32_t* vp,
   }
 }
 
+// K = 256 encodes exchange layouts through quad items (cq_write_q ..
+// hi_read_q, fast_common.hpp): no byte transposes.
+#ifndef NP_ENC_QX
+#define NP_ENC_QX 1
+#endif
+template <int K>
+constexpr bool kEncQx = NP_ENC_QX && K == 256;
+
 // One workgroup: 256 chunks of one payload.  mod.rs:144-154 / inc_encode.rs:15-48.
 template <int K>
 __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_fast(DevTables T, EncodeArgs a, uint32_t nchunks, uint32_t tiles) {
@@ -166,13 +174,23 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     store_rows(out, a.shard_len, 16 * g, wanted_store, CL, CH, lane, ncols, full);
     tower_convert(T, CL, CH);  // transforms run in tower coordinates
     cq_levels<K, true, true, 0>(T, VP, 0, g, CL, CH);
-    cq_write_p<K>(tile, cqb, CL, CH);
+    if constexpr (kEncQx<K>) {
+      // the quad items overlay payload blocks that other waves read: wait for
+      // every wave's cq_read (cq_write_p writes back only the blocks it read)
+      __syncthreads();
+      cq_write_q(tile, g, lane, CL, CH);
+    } else {
+      cq_write_p<K>(tile, cqb, CL, CH);
+    }
   }
   __syncthreads();
   // ---- high layout: inverse levels 4.. -> coefficients M
   const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
   uint32_t ML[16], MH[16];
-  hi_read_p<K>(tile, hb, ML, MH);
+  if constexpr (kEncQx<K>)
+    hi_read_q(tile, g, lane, ML, MH);
+  else
+    hi_read_p<K>(tile, hb, ML, MH);
   hi_levels<K, true, true, 0, 0>(T, VP, 0, ML, MH);
 #pragma unroll
   for (int q = 0; q < 16; ++q) asm volatile("" : "+v"(ML[q]), "+v"(MH[q]));  // materialise M once
@@ -187,9 +205,15 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     __syncthreads();  // the previous cq pass is done with the tile and with the other table buffer
     if (!resident && sh + 1 < nshift && (sh + 1) * K < a.wanted_n)
       stage_vpools<K, G::kThreads>(T, (sh + 1) * K, VP + ((sh + 1) & 1u) * G::kVPWords, sh + 1 < 4);
-    hi_write_p<K>(tile, fresh_v(hb), XL, XH);
-    __syncthreads();
-    cq_read_p<K>(tile, fresh_v(cqb), XL, XH);
+    if constexpr (kEncQx<K>) {
+      hi_write_q(tile, g, lane, XL, XH);
+      __syncthreads();
+      cq_read_q(tile, g, lane, XL, XH);
+    } else {
+      hi_write_p<K>(tile, fresh_v(hb), XL, XH);
+      __syncthreads();
+      cq_read_p<K>(tile, fresh_v(cqb), XL, XH);
+    }
     shift_cq<K, SH>(T, vp, index, g, XL, XH);
     store_rows(out, a.shard_len, index + 16 * g, wanted_store, XL, XH, lane, ncols, full);
   };
@@ -209,11 +233,6 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
 // live in registers across the tile loop.
 template <int K>
 constexpr bool kMultiTile = K == 256;
-// The multi-tile encode exchanges layouts through quad items (cq_write_q ..
-// hi_read_q, fast_common.hpp): no byte transposes.
-#ifndef NP_ENC_QX
-#define NP_ENC_QX 1
-#endif
 
 // Table buffers of the multi-tile encode: the inverse transform's and one per
 // shift, staged once per workgroup (n <= 4K); with the 128 KiB tile they fill
@@ -273,7 +292,7 @@ __device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArg
   const uint32_t* vp = VP + sh * G::kVPWords;  // the tables of every shift stay staged (kEncBuffers)
   shift_hi<K, SH>(T, vp, index, ML, MH, XL, XH, PL, PH);
   __syncthreads();  // the previous cq pass is done with the tile
-  if constexpr (NP_ENC_QX) {
+  if constexpr (kEncQx<K>) {
     hi_write_q(tile, g, lane, XL, XH);
     __syncthreads();
     cq_read_q(tile, g, lane, XL, XH);
@@ -356,15 +375,19 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
     store_rows(out, a.shard_len, 16 * g, (kExp & 2) ? 0u : a.wanted_n, CL, CH, lane, ncols, full);
     tower_convert(T, CL, CH);  // transforms run in tower coordinates
     cq_levels<K, true, true, 0>(T, VP, 0, g, CL, CH);
-    if constexpr (NP_ENC_QX)
+    if constexpr (kEncQx<K>) {
+      // the quad items overlay payload blocks that other waves read: wait for
+      // every wave's cq_read (cq_write_p writes back only the blocks it read)
+      __syncthreads();
       cq_write_q(tile, g, lane, CL, CH);
-    else
+    } else {
       cq_write_p<K>(tile, cqb, CL, CH);
+    }
   }
   __syncthreads();
   const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
   uint32_t ML[16], MH[16];
-  if constexpr (NP_ENC_QX)
+  if constexpr (kEncQx<K>)
     hi_read_q(tile, g, lane, ML, MH);
   else
     hi_read_p<K>(tile, hb, ML, MH);
