@@ -206,6 +206,14 @@ constexpr size_t enc_scratch() {
   return (2u * (KB / kS) - 1u) * kSegScr;  // M (SUBS sub-segments) + W_1.. (SUBS - 1)
 }
 
+// The encode's sub-segment transforms exchange layouts through quad items
+// (the high layout of k_encode_multi; the top levels and the scratch are
+// per thread and position, so they follow it unchanged).  The decode keeps
+// the natural format: D_256 needs position bits 0-3 in one wave.
+#ifndef NP_BIG_ENC_QX
+#define NP_BIG_ENC_QX 1
+#endif
+
 template <int KB>
 __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_big(
     DevTables T, EncodeArgs a, uint32_t nchunks, uint32_t tiles, uint32_t tile0, uint8_t* scratch) {
@@ -273,11 +281,19 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
         constexpr int GEN = decltype(gc)::value;  // 0 only at index 0
         cq_levels<kS, true, GEN == 0, GEN>(T, VP, index, g, CL, CH);
       });
-      cq_write<kS>(tile, cq, CL, CH);
+      if constexpr (NP_BIG_ENC_QX) {  // quad items (fast_common.hpp cq_write_q): no byte transposes
+        __syncthreads();              // they overlay payload blocks that other waves read
+        cq_write_q(tile, g, lane, CL, CH);
+      } else {
+        cq_write<kS>(tile, cq, CL, CH);
+      }
     }
     __syncthreads();
     uint32_t XL[16], XH[16];
-    hi_read<kS>(tile, fresh_v(hb), XL, XH);
+    if constexpr (NP_BIG_ENC_QX)
+      hi_read_q(tile, g, lane, XL, XH);
+    else
+      hi_read<kS>(tile, fresh_v(hb), XL, XH);
     with_gen<0, kSubMaxGen<KB>, false>(index, [&](auto gc) __attribute__((always_inline)) {
       constexpr int GEN = decltype(gc)::value;
       hi_levels<kS, true, GEN == 0, 0, GEN>(T, VP, index, XL, XH);
@@ -343,9 +359,15 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
         if constexpr (GEN < 0) tower_convert(T, XL, XH);  // a far shift: Cantor coordinates
         hi_levels<kS, false, false, 0, GEN>(T, VP, index, XL, XH);
       });
-      hi_write<kS>(tile, fresh_v(hb), XL, XH);
-      __syncthreads();
-      cq_read<kS>(tile, fresh_v(cqb), XL, XH);
+      if constexpr (NP_BIG_ENC_QX) {
+        hi_write_q(tile, g, lane, XL, XH);
+        __syncthreads();
+        cq_read_q(tile, g, lane, XL, XH);
+      } else {
+        hi_write<kS>(tile, fresh_v(hb), XL, XH);
+        __syncthreads();
+        cq_read<kS>(tile, fresh_v(cqb), XL, XH);
+      }
       with_gen<1, kEncBigMaxGenK<KB>, true>(index, [&](auto gc) __attribute__((always_inline)) {
         constexpr int GEN = decltype(gc)::value;
         cq_levels<kS, false, false, GEN>(T, VP, index, g, XL, XH);
