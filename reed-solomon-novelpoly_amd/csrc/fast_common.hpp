@@ -1142,14 +1142,15 @@ __device__ __forceinline__ void hi_write_p(uint8_t* tile, uint32_t base, const u
   for (int j = 0; j < 16; ++j) *reinterpret_cast<uint2*>(tile + (base ^ (8u * Geo<K>::R * j))) = make_uint2(L[j], H[j]);
 }
 
-// Quad exchange between the cq layout and a column-quad high layout (K = 256,
-// the multi-tile encode): LDS item (position p, column quad c) = the uint2
-// (low plane, high plane) of columns 4c..4c+3 at position p, at byte
-// 8 (64 p + c).  cq side: wave g, lane c holds positions 16 g + i.  High side:
-// wave r, lane c holds positions r + 16 j, so level b >= 4 pairs registers j
-// and j + 2^(b-4) with group j >> (b-3), as hi_levels expects, and no byte
-// transpose is needed on either side (tr4x4).  Every wave-instruction moves
-// 512 contiguous bytes.
+// Quad exchange between the cq layout and a column-quad high layout (the
+// fast encodes): LDS item (position p, column quad c) = the uint2 (low plane,
+// high plane) of columns 4c..4c+3 at position p, at byte 8 (64 p + c).  cq
+// side: wave g, lane c holds positions 16 g + i.  High side (nres = 256 / K
+// residues per thread): wave w, lane c, register j' = r + nres j holds
+// position nres w + r + 16 j, so level b >= 4 pairs registers j' and
+// j' + 2^(b-2-logR) with group j' >> (b-1-logR), as hi_levels expects
+// (R = K / 64), and no byte transpose is needed on either side (tr4x4).
+// Every wave-instruction moves 512 contiguous bytes.
 __device__ __forceinline__ void cq_write_q(uint8_t* tile, uint32_t g, uint32_t lane, const uint32_t (&L)[16],
                                            const uint32_t (&H)[16]) {
   uint8_t* b = tile + 8192u * g + fresh_v(8u * lane);
@@ -1166,18 +1167,26 @@ __device__ __forceinline__ void cq_read_q(const uint8_t* tile, uint32_t g, uint3
     H[i] = d.y;
   }
 }
-__device__ __forceinline__ void hi_write_q(uint8_t* tile, uint32_t r, uint32_t lane, const uint32_t (&L)[16],
-                                           const uint32_t (&H)[16]) {
-  uint8_t* b = tile + 512u * r + fresh_v(8u * lane);
-#pragma unroll
-  for (int j = 0; j < 16; ++j) *reinterpret_cast<uint2*>(b + 8192u * j) = make_uint2(L[j], H[j]);
+// Byte offset of high-layout register j' from the thread's base (K / 64 = R).
+template <int K>
+__host__ __device__ constexpr uint32_t hi_q_off(int jj) {
+  constexpr int nres = 256 / K;
+  return 512u * static_cast<uint32_t>(jj % nres + 16 * (jj / nres));
 }
-__device__ __forceinline__ void hi_read_q(const uint8_t* tile, uint32_t r, uint32_t lane, uint32_t (&L)[16],
+template <int K = 256>
+__device__ __forceinline__ void hi_write_q(uint8_t* tile, uint32_t w, uint32_t lane, const uint32_t (&L)[16],
+                                           const uint32_t (&H)[16]) {
+  uint8_t* b = tile + 512u * (256u / K) * w + fresh_v(8u * lane);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) *reinterpret_cast<uint2*>(b + hi_q_off<K>(j)) = make_uint2(L[j], H[j]);
+}
+template <int K = 256>
+__device__ __forceinline__ void hi_read_q(const uint8_t* tile, uint32_t w, uint32_t lane, uint32_t (&L)[16],
                                           uint32_t (&H)[16]) {
-  const uint8_t* b = tile + 512u * r + fresh_v(8u * lane);
+  const uint8_t* b = tile + 512u * (256u / K) * w + fresh_v(8u * lane);
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    const uint2 d = *reinterpret_cast<const uint2*>(b + 8192u * j);
+    const uint2 d = *reinterpret_cast<const uint2*>(b + hi_q_off<K>(j));
     L[j] = d.x;
     H[j] = d.y;
   }

@@ -100,13 +100,13 @@ __device__ __forceinline__ void shift_cq(const DevTables& T, const uint32_t* vp,
   }
 }
 
-// K = 256 encodes exchange layouts through quad items (cq_write_q ..
+// The fast encodes exchange layouts through quad items (cq_write_q ..
 // hi_read_q, fast_common.hpp): no byte transposes.
 #ifndef NP_ENC_QX
 #define NP_ENC_QX 1
 #endif
 template <int K>
-constexpr bool kEncQx = NP_ENC_QX && K == 256;
+constexpr bool kEncQx = NP_ENC_QX != 0;
 
 // One workgroup: 256 chunks of one payload.  mod.rs:144-154 / inc_encode.rs:15-48.
 template <int K>
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
   const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
   uint32_t ML[16], MH[16];
   if constexpr (kEncQx<K>)
-    hi_read_q(tile, g, lane, ML, MH);
+    hi_read_q<K>(tile, g, lane, ML, MH);
   else
     hi_read_p<K>(tile, hb, ML, MH);
   hi_levels<K, true, true, 0, 0>(T, VP, 0, ML, MH);
@@ -206,7 +206,7 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     if (!resident && sh + 1 < nshift && (sh + 1) * K < a.wanted_n)
       stage_vpools<K, G::kThreads>(T, (sh + 1) * K, VP + ((sh + 1) & 1u) * G::kVPWords, sh + 1 < 4);
     if constexpr (kEncQx<K>) {
-      hi_write_q(tile, g, lane, XL, XH);
+      hi_write_q<K>(tile, g, lane, XL, XH);
       __syncthreads();
       cq_read_q(tile, g, lane, XL, XH);
     } else {
@@ -293,7 +293,7 @@ __device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArg
   shift_hi<K, SH>(T, vp, index, ML, MH, XL, XH, PL, PH);
   __syncthreads();  // the previous cq pass is done with the tile
   if constexpr (kEncQx<K>) {
-    hi_write_q(tile, g, lane, XL, XH);
+    hi_write_q<K>(tile, g, lane, XL, XH);
     __syncthreads();
     cq_read_q(tile, g, lane, XL, XH);
   } else {
@@ -388,7 +388,7 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
   const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
   uint32_t ML[16], MH[16];
   if constexpr (kEncQx<K>)
-    hi_read_q(tile, g, lane, ML, MH);
+    hi_read_q<K>(tile, g, lane, ML, MH);
   else
     hi_read_p<K>(tile, hb, ML, MH);
   hi_levels<K, true, true, 0, 0>(T, VP, 0, ML, MH);
