@@ -23,6 +23,24 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "reed-solomon-novelpoly_amd", "python"))
 
 METRIC = "payload GiB/s (device-resident) encode+reconstruct, n=1024 shards, 1 MiB msgs"
+
+
+def metric_name(n_wanted: int, payload: int) -> str:
+    """BASELINE.json's metric for its headline shape (n = 1024 shards, 1 MiB
+    payloads: configs 3 and 5); other shapes name their own (n, payload)."""
+    if n_wanted == 1024 and payload == 1 << 20:
+        return METRIC
+    size = f"{payload >> 20} MiB" if payload % (1 << 20) == 0 else (
+        f"{payload >> 10} KiB" if payload % 1024 == 0 else f"{payload} B")
+    return f"payload GiB/s (device-resident) encode+reconstruct, n={n_wanted} shards, {size} msgs"
+
+
+def workload_name(cfg_id, world: int, batch: int) -> str:
+    """The BASELINE config a run measures: config 3 on N GPUs is config 5's
+    workload (1 MiB x 1024 payloads per GPU, 8192 on 8 GPUs)."""
+    if cfg_id in (3, 5) and world > 1:
+        return f"BASELINE config 5 shape: {world * batch} payloads over {world} GPUs ({batch}/GPU)"
+    return f"BASELINE config {cfg_id}"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
@@ -85,6 +103,31 @@ def load_traffic(config: int):
     return {k: v.get("traffic_bytes") for k, v in summary.get("kernels", {}).items()}
 
 
+def host_cores():
+    """The host cores this process may run on: its CPU affinity set, capped by
+    the cgroup CPU quota where one is set (cpu.max: the lease's share of a
+    larger machine).  The CPU baseline runs one thread per such core."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            with open(path) as f:
+                parts = f.read().split()
+        except OSError:
+            continue
+        if path.endswith("cpu.max") and parts and parts[0] != "max":
+            quota = int(parts[0]) / int(parts[1])
+        elif path.endswith("cfs_quota_us") and parts and int(parts[0]) > 0:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                quota = int(parts[0]) / int(f.read().split()[0])
+        break
+    used = affinity if quota is None else max(1, min(affinity, int(quota)))
+    return {"affinity": affinity, "quota": quota, "used": used}
+
+
 def cpu_baseline(cfg, params, seconds):
     """The reference's own C implementation (oracle/_ref/cpu_bench_ref, built from
     /root/reference by oracle/Makefile) -- or, where that build is absent, the C
@@ -100,11 +143,8 @@ def cpu_baseline(cfg, params, seconds):
     exe = ref if os.path.exists(ref) else port
     if not os.path.exists(exe):
         raise RuntimeError("CPU baseline harness missing: run __graft_entry__.build()")
-    try:
-        avail = len(os.sched_getaffinity(0))
-    except AttributeError:
-        avail = os.cpu_count() or 1
-    threads = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", "16")), 16))
+    hc = host_cores()
+    threads = hc["used"]
     n, k, plen, erase = params.n(), params.k(), cfg["payload"], cfg["erase"]
 
     def run(t, secs):
@@ -120,9 +160,12 @@ def cpu_baseline(cfg, params, seconds):
         "value": round(multi["gib_s"], 6),
         "unit": "GiB/s",
         "cores": threads,
+        "cores_available": hc["affinity"],
+        "cpu_quota": hc["quota"],
         "kind": multi["kind"],
         "single_core_value": round(single["gib_s"], 6),
         "sample": f"{multi['payloads']} payloads of config {cfg['id']} in {multi['seconds']:.1f}s on {threads} threads "
+                  f"({hc['affinity']} cores in the affinity set, cgroup CPU quota {hc['quota']}) "
                   f"(+{single['payloads']} in {single['seconds']:.1f}s on 1 thread): encode + reconstruct with "
                   f"{erase} erasures, {'reference cxx/RSErasureCode.c' if multi['kind'] == 'reference' else 'oracle/np_oracle.c'} "
                   f"+ crate glue (oracle/cpu_bench.c), every payload round-trip checked",
@@ -168,7 +211,10 @@ def dry_run(args):
         ranges = [tuple(int(v) for v in o) for o in out]
         dist.destroy_process_group()
     if rank == 0:
-        print(json.dumps({"dry_run": True, "n_gpus": world, "ranges": ranges, "batch_per_gpu": batch}), flush=True)
+        cfg = synth.CONFIGS[args.config]
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranges": ranges, "batch_per_gpu": batch,
+                          "metric": metric_name(cfg["n_wanted"], cfg["payload"]),
+                          "workload": workload_name(args.config, world, batch)}), flush=True)
 
 
 def main():
@@ -280,7 +326,8 @@ def main():
     present_rows = int(present_h.sum())
     algo = {
         "encode": batch * (plen + nshard * sl),
-        "reconstruct": present_rows * sl + batch * out_len,
+        # + the present mask (batch x n bytes) the locator reads
+        "reconstruct": present_rows * sl + batch * out_len + batch * n,
     }
     # the committed PMC summaries were measured at each config's BASELINE batch:
     # other batches report traffic null
@@ -294,7 +341,7 @@ def main():
     dominant = max(kt, key=kt.get)
 
     line = {
-        "metric": METRIC,
+        "metric": metric_name(cfg["n_wanted"], plen),
         "value": round(value, 3),
         "unit": "GiB/s",
         "n_gpus": world,
@@ -306,7 +353,7 @@ def main():
         "vs_baseline": None,
         "dtype": "u16",
         "data": "synthetic",
-        "config": {"workload": f"BASELINE config {cfg['id']}: n_wanted={cfg['n_wanted']} "
+        "config": {"workload": f"{workload_name(cfg['id'], world, batch)}: n_wanted={cfg['n_wanted']} "
                                f"k_wanted={cfg['k_wanted']} (effective n={n}, k={k}), {plen} B payloads, "
                                f"batch {batch}/GPU, encode + error locator + reconstruct with {erase} "
                                f"random erasures per payload",

@@ -146,13 +146,19 @@ typedef struct np_payload_status {
  * are all present (inc_reconstruct.rs:46-50) -- bit-exact for any received
  * bytes.  d_status (device, batch entries, may be NULL) receives each
  * payload's np_payload_status; the NeedMoreShards check runs on the device. */
-int np_reconstruct_batch_dev2(np_ctx* ctx, const np_code_params* params, const uint8_t* d_shards,
+int np_reconstruct_batch_dev3(np_ctx* ctx, const np_code_params* params, const uint8_t* d_shards,
                               size_t shard_len, size_t batch_stride, const uint8_t* d_present,
                               const uint16_t* d_locators, size_t batch, uint8_t* d_out, size_t out_stride,
                               np_payload_status* d_status, void* stream);
+/* The 0.1.0 entry: np_reconstruct_batch_dev3 with d_status = NULL (kept with
+ * its original argument list, so callers built against 0.1.0 stay correct). */
+int np_reconstruct_batch_dev2(np_ctx* ctx, const np_code_params* params, const uint8_t* d_shards,
+                              size_t shard_len, size_t batch_stride, const uint8_t* d_present,
+                              const uint16_t* d_locators, size_t batch, uint8_t* d_out, size_t out_stride,
+                              void* stream);
 /* OPT-IN, not crate-equivalent: for callers whose received shards are known
  * to be an unmodified codeword (e.g. verified by a Merkle proof upstream).
- * Like np_reconstruct_batch_dev2 with d_locators = NULL, but a payload whose
+ * Like np_reconstruct_batch_dev3 with d_locators = NULL, but a payload whose
  * first 2k shards hold k present ones may be decoded from those 2k rows only
  * (n = 4k shapes of the fast path).  That equals the reference's output only
  * when the shards form a codeword; for other bytes the reference's decode
@@ -198,7 +204,7 @@ int np_reconstruct_batch_host(np_ctx* ctx, const np_code_params* params, const u
 void np_batch_split(size_t batch, size_t ndev, size_t i, size_t* begin, size_t* count);
 /* Device memory: d_payloads[i] / d_shards[i] / d_present[i] / d_out[i] /
  * d_status[i] (d_status may be NULL) are device i's buffers holding its range,
- * laid out as in np_encode_batch_dev / np_reconstruct_batch_dev2 (payload
+ * laid out as in np_encode_batch_dev / np_reconstruct_batch_dev3 (payload
  * np_batch_split(...).begin of the batch at index 0). */
 int np_encode_batch_multi(np_ctx* const* ctxs, size_t nctx, const np_code_params* params,
                           const uint8_t* const* d_payloads, size_t payload_len, size_t payload_stride, size_t batch,

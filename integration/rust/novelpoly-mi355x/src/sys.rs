@@ -129,7 +129,7 @@ extern "C" {
 		out_stride: usize,
 		stream: *mut c_void,
 	) -> c_int;
-	pub fn np_reconstruct_batch_dev2(
+	pub fn np_reconstruct_batch_dev3(
 		ctx: *mut np_ctx,
 		params: *const np_code_params,
 		d_shards: *const u8,
@@ -141,6 +141,19 @@ extern "C" {
 		d_out: *mut u8,
 		out_stride: usize,
 		d_status: *mut np_payload_status,
+		stream: *mut c_void,
+	) -> c_int;
+	pub fn np_reconstruct_batch_dev2(
+		ctx: *mut np_ctx,
+		params: *const np_code_params,
+		d_shards: *const u8,
+		shard_len: usize,
+		batch_stride: usize,
+		d_present: *const u8,
+		d_locators: *const u16,
+		batch: usize,
+		d_out: *mut u8,
+		out_stride: usize,
 		stream: *mut c_void,
 	) -> c_int;
 	pub fn np_reconstruct_codewords_batch_dev(

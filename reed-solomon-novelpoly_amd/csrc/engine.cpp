@@ -184,8 +184,8 @@ hipError_t big_done(np_ctx* c, hipStream_t s, hipError_t e) {
 }
 
 // Scratch slots of a k = 512 / 1024 launch over `tiles` tiles: one per resident workgroup.
-size_t big_slots(const np_ctx* c, size_t tiles) {
-  return std::min((tiles + 7) / 8 * 8, np::big_resident_slots(c->device));
+size_t big_slots(const np_ctx* c, size_t tiles, uint32_t n, uint32_t k, bool reconstruct) {
+  return std::min((tiles + 7) / 8 * 8, np::big_resident_slots(c->device, n, k, reconstruct));
 }
 
 // Caller holds the context lock.
@@ -195,7 +195,7 @@ hipError_t launch_encode(np_ctx* c, const np::EncodeArgs& a, hipStream_t s) {
     const size_t tiles = ((a.payload_len + 2 * a.k - 1) / (2 * a.k) + 255) / 256;
     uint8_t* scr = nullptr;
     size_t bytes = 0;
-    hipError_t e = big_scratch(c, big_slots(c, a.batch * tiles) * np::big_encode_scratch_per_tile(a.k), s, &scr, &bytes);
+    hipError_t e = big_scratch(c, big_slots(c, a.batch * tiles, a.n, a.k, false) * np::big_encode_scratch_per_tile(a.k), s, &scr, &bytes);
     if (e == hipSuccess) e = np::launch_encode_big(c->T, a, scr, bytes, s);
     return big_done(c, s, e);
   }
@@ -255,7 +255,7 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
       const size_t rec_bytes = (sub.batch * rstride + 255) / 256 * 256;
       uint8_t* scr = nullptr;
       size_t bytes = 0;
-      hipError_t e = big_scratch(c, rec_bytes + big_slots(c, sub.batch * tiles) * per_tile, s, &scr, &bytes);
+      hipError_t e = big_scratch(c, rec_bytes + big_slots(c, sub.batch * tiles, sub.n, sub.k, true) * per_tile, s, &scr, &bytes);
       if (e == hipSuccess && bytes < rec_bytes + 8 * per_tile) e = hipErrorInvalidValue;
       if (!a.status) sub.status = reinterpret_cast<uint32_t*>(scr + sub.batch * np::big_record_stride(a.n));
       sub.prefix = scr;
@@ -656,10 +656,19 @@ int reconstruct_dev2(np_ctx* c, const np_code_params* p, const uint8_t* d_shards
 
 }  // namespace
 
-int np_reconstruct_batch_dev2(np_ctx* c, const np_code_params* p, const uint8_t* d_shards, size_t shard_len,
+int np_reconstruct_batch_dev3(np_ctx* c, const np_code_params* p, const uint8_t* d_shards, size_t shard_len,
                               size_t bstride, const uint8_t* d_present, const uint16_t* d_loc, size_t batch,
                               uint8_t* d_out, size_t out_stride, np_payload_status* d_status, void* stream) {
   return reconstruct_dev2(c, p, d_shards, shard_len, bstride, d_present, d_loc, batch, d_out, out_stride, d_status,
+                          stream, false);
+}
+
+// The 0.1.0 signature (no per-payload status), kept so that a caller built
+// against the old header still passes its stream in the stream slot.
+int np_reconstruct_batch_dev2(np_ctx* c, const np_code_params* p, const uint8_t* d_shards, size_t shard_len,
+                              size_t bstride, const uint8_t* d_present, const uint16_t* d_loc, size_t batch,
+                              uint8_t* d_out, size_t out_stride, void* stream) {
+  return reconstruct_dev2(c, p, d_shards, shard_len, bstride, d_present, d_loc, batch, d_out, out_stride, nullptr,
                           stream, false);
 }
 
@@ -893,6 +902,7 @@ int np_encode_batch_multi(np_ctx* const* ctxs, size_t nctx, const np_code_params
                           const uint8_t* const* d_payloads, size_t len, size_t pstride, size_t batch,
                           uint8_t* const* d_shards, size_t bstride) {
   if (!d_payloads || !d_shards) return fail(NP_ERR_INVALID_ARGUMENT);
+  if (int st = check_params(p)) return st;
   return run_multi(ctxs, nctx, batch, [&](size_t i, size_t, size_t cnt) {
     int st = np_encode_batch_dev(ctxs[i], p, d_payloads[i], len, pstride, cnt, d_shards[i], bstride, nullptr);
     return st ? st : np_ctx_synchronize(ctxs[i]);
@@ -904,8 +914,9 @@ int np_reconstruct_batch_multi(np_ctx* const* ctxs, size_t nctx, const np_code_p
                                const uint8_t* const* d_present, size_t batch, uint8_t* const* d_out,
                                size_t out_stride, np_payload_status* const* d_status) {
   if (!d_shards || !d_present || !d_out) return fail(NP_ERR_INVALID_ARGUMENT);
+  if (int st = check_params(p)) return st;
   return run_multi(ctxs, nctx, batch, [&](size_t i, size_t, size_t cnt) {
-    int st = np_reconstruct_batch_dev2(ctxs[i], p, d_shards[i], shard_len, bstride, d_present[i], nullptr, cnt,
+    int st = np_reconstruct_batch_dev3(ctxs[i], p, d_shards[i], shard_len, bstride, d_present[i], nullptr, cnt,
                                        d_out[i], out_stride, d_status ? d_status[i] : nullptr, nullptr);
     return st ? st : np_ctx_synchronize(ctxs[i]);
   });
@@ -914,6 +925,7 @@ int np_reconstruct_batch_multi(np_ctx* const* ctxs, size_t nctx, const np_code_p
 int np_encode_batch_host_multi(np_ctx* const* ctxs, size_t nctx, const np_code_params* p, const uint8_t* payloads,
                                size_t len, size_t pstride, size_t batch, uint8_t* shards, size_t bstride) {
   if (!payloads || !shards) return fail(NP_ERR_INVALID_ARGUMENT);
+  if (int st = check_params(p)) return st;
   return run_multi(ctxs, nctx, batch, [&](size_t i, size_t b0, size_t cnt) {
     return np_encode_batch_host(ctxs[i], p, payloads + b0 * pstride, len, pstride, cnt, shards + b0 * bstride,
                                 bstride);
@@ -924,6 +936,7 @@ int np_reconstruct_batch_host_multi(np_ctx* const* ctxs, size_t nctx, const np_c
                                     const uint8_t* shards, size_t shard_len, size_t bstride, const uint8_t* present,
                                     size_t batch, uint8_t* out, size_t out_stride) {
   if (!shards || !present || !out || !p) return fail(NP_ERR_INVALID_ARGUMENT);
+  if (int st = check_params(p)) return st;
   return run_multi(ctxs, nctx, batch, [&](size_t i, size_t b0, size_t cnt) {
     return np_reconstruct_batch_host(ctxs[i], p, shards + b0 * bstride, shard_len, bstride, present + b0 * p->n,
                                      cnt, out + b0 * out_stride, out_stride);

@@ -824,10 +824,13 @@ __global__ __launch_bounds__(256) void k_big_records(DevTables T, ReconstructArg
   for (uint32_t v = tid; v < static_cast<uint32_t>(N) / 16u; v += 256) dst[v] = reinterpret_cast<const uint4*>(PR)[v];
 }
 
-size_t enc_big_lds() { return static_cast<size_t>(Geo<kS>::kTileBytes) + 4u * Geo<kS>::kVPWords; }
-size_t rec_big_lds(uint32_t n) {  // tile, tables, E (2 n bytes), PR (n bytes)
+constexpr size_t enc_big_lds() { return static_cast<size_t>(Geo<kS>::kTileBytes) + 4u * Geo<kS>::kVPWords; }
+constexpr size_t rec_big_lds(uint32_t n) {  // tile, tables, E (2 n bytes), PR (n bytes)
   return static_cast<size_t>(Geo<kS>::kTileBytes) + 4u * Geo<kS>::kVPWords + 3u * n;
 }
+// Dynamic LDS of every instance fits the CU's 160 KiB (n = 8192 exactly fills it).
+static_assert(enc_big_lds() <= 160u * 1024u, "encode LDS");
+static_assert(rec_big_lds(8192) <= 160u * 1024u, "largest reconstruct instance (k = 1024 / 2048, n = 8192) LDS");
 
 // Calls f(reconstruct kernel, record kernel) for the instances of (n, k);
 // false if none.
@@ -874,25 +877,36 @@ int current_device() {
   return hipGetDevice(&d) == hipSuccess ? d : 0;
 }
 
-// Cached per device under a lock (contexts on different threads may ask at once).
-size_t big_resident_slots(int device) {
+// Cached per (device, kernel instance) under a lock (contexts on different
+// threads may ask at once); the occupancy is that of the instance launched.
+size_t resident_slots_of(int device, const void* kern, size_t lds) {
   static std::mutex mu;
-  static std::map<int, size_t> cache;
+  static std::map<std::pair<int, const void*>, size_t> cache;
   std::lock_guard<std::mutex> g(mu);
-  const auto it = cache.find(device);
+  const auto key = std::make_pair(device, kern);
+  const auto it = cache.find(key);
   if (it != cache.end()) return it->second;
   int cus = 0, per = 0, prev = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
   // the occupancy query runs on the current device: switch to `device` for it
   const bool sw = hipGetDevice(&prev) == hipSuccess && prev != device && hipSetDevice(device) == hipSuccess;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&k_reconstruct_big<1024, 4>),
-                                                   kTB, rec_big_lds(4096)) != hipSuccess ||
-      per <= 0)
-    per = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, kTB, lds) != hipSuccess || per <= 0) per = 1;
   if (sw) (void)hipSetDevice(prev);
   const size_t slots = std::max<size_t>(8, static_cast<size_t>(cus) * per / 8 * 8);
-  cache[device] = slots;
+  cache[key] = slots;
   return slots;
+}
+
+size_t big_resident_slots(int device, uint32_t n, uint32_t k, bool reconstruct) {
+  const void* kern = nullptr;
+  if (reconstruct) {
+    with_rec_big(n, k, [&](auto kf, auto) { kern = reinterpret_cast<const void*>(kf); });
+    return kern ? resident_slots_of(device, kern, rec_big_lds(n)) : 8;
+  }
+  kern = k == 512 ? reinterpret_cast<const void*>(&k_encode_big<512>)
+         : k == 1024 ? reinterpret_cast<const void*>(&k_encode_big<1024>)
+                     : reinterpret_cast<const void*>(&k_encode_big<2048>);
+  return resident_slots_of(device, kern, enc_big_lds());
 }
 
 hipError_t launch_encode_big(const DevTables& T, const EncodeArgs& a, uint8_t* scratch, size_t scratch_bytes,
@@ -904,7 +918,10 @@ hipError_t launch_encode_big(const DevTables& T, const EncodeArgs& a, uint8_t* s
   const size_t total = a.batch * tiles;
   // multiple of 8 keeps tile0 % 8 == 0 (tile_of)
   const size_t per_tile = big_encode_scratch_per_tile(a.k);
-  const size_t per_launch = std::min(big_resident_slots(current_device()), scratch_bytes / per_tile / 8 * 8);
+  const void* kern = a.k == 512 ? reinterpret_cast<const void*>(&k_encode_big<512>)
+                     : a.k == 1024 ? reinterpret_cast<const void*>(&k_encode_big<1024>)
+                                   : reinterpret_cast<const void*>(&k_encode_big<2048>);
+  const size_t per_launch = std::min(resident_slots_of(current_device(), kern, enc_big_lds()), scratch_bytes / per_tile / 8 * 8);
   if (per_launch == 0 || total > 0xffffffffu) return hipErrorInvalidValue;
   for (size_t t0 = 0; t0 < total; t0 += per_launch) {
     const uint32_t blocks = static_cast<uint32_t>(std::min(per_launch, total - t0));
@@ -942,7 +959,10 @@ hipError_t launch_reconstruct_big(const DevTables& T, const ReconstructArgs& a, 
   const uint32_t tiles = static_cast<uint32_t>((nsyms + kTile - 1) / kTile);
   const size_t total = a.batch * tiles;
   const size_t per_tile = big_reconstruct_scratch_per_tile(a.n, a.k);
-  const size_t per_launch = std::min(big_resident_slots(current_device()), scratch_bytes / per_tile / 8 * 8);
+  const void* kern = nullptr;
+  with_rec_big(a.n, a.k, [&](auto k, auto) { kern = reinterpret_cast<const void*>(k); });
+  const size_t per_launch =
+      std::min(resident_slots_of(current_device(), kern, rec_big_lds(a.n)), scratch_bytes / per_tile / 8 * 8);
   if (per_launch == 0 || total > 0xffffffffu) return hipErrorInvalidValue;
   for (size_t t0 = 0; t0 < total; t0 += per_launch) {
     const uint32_t blocks = static_cast<uint32_t>(std::min(per_launch, total - t0));

@@ -97,7 +97,8 @@ hipError_t launch_reconstruct_small(const DevTables& T, const ReconstructArgs& a
 bool big_encode_supported(uint32_t n, uint32_t k);
 bool big_reconstruct_supported(uint32_t n, uint32_t k);  // n / k in {2, 4, 8}
 size_t big_encode_scratch_per_tile(uint32_t k);
-size_t big_resident_slots(int device);  // scratch slots a launch uses at most (multiple of 8)
+// scratch slots a launch of the (n, k) encode / reconstruct instance uses at most (multiple of 8)
+size_t big_resident_slots(int device, uint32_t n, uint32_t k, bool reconstruct);
 size_t big_reconstruct_scratch_per_tile(uint32_t n, uint32_t k);
 // Per-payload records (status, mode, row multipliers, present flags) of the
 // big reconstruct, big_record_stride(n) bytes each, into `records`; the

@@ -68,7 +68,8 @@ def lib() -> C.CDLL:
                 C.c_int, [vp, P, C.POINTER(vp), C.POINTER(_sz), _sz, vp, _sz, C.POINTER(_sz)]),
             "np_encode_batch_dev": (C.c_int, [vp, P, vp, _sz, _sz, _sz, vp, _sz, vp]),
             "np_reconstruct_batch_dev": (C.c_int, [vp, P, vp, _sz, _sz, vp, _sz, vp, _sz, vp]),
-            "np_reconstruct_batch_dev2": (C.c_int, [vp, P, vp, _sz, _sz, vp, vp, _sz, vp, _sz, vp, vp]),
+            "np_reconstruct_batch_dev3": (C.c_int, [vp, P, vp, _sz, _sz, vp, vp, _sz, vp, _sz, vp, vp]),
+            "np_reconstruct_batch_dev2": (C.c_int, [vp, P, vp, _sz, _sz, vp, vp, _sz, vp, _sz, vp]),
             "np_reconstruct_codewords_batch_dev": (C.c_int, [vp, P, vp, _sz, _sz, vp, _sz, vp, _sz, vp, vp]),
             "np_error_locator_dev": (C.c_int, [vp, _sz, vp, _sz, vp, vp]),
             "np_reconstruct_from_systematic_batch_dev": (C.c_int, [vp, P, vp, _sz, _sz, _sz, vp, _sz, vp]),
@@ -422,7 +423,7 @@ def reconstruct_batch_dev2(params: CodeParams, d_shards: int, shard_len: int, ba
     d_status: device address of ``batch`` np_payload_status entries (int32 status,
     uint32 have; see :func:`payload_errors`) or 0."""
     ctx = ctx or default_context()
-    _raise(lib().np_reconstruct_batch_dev2(ctx.handle, C.byref(params._c()), d_shards, shard_len, batch_stride,
+    _raise(lib().np_reconstruct_batch_dev3(ctx.handle, C.byref(params._c()), d_shards, shard_len, batch_stride,
                                            d_present, d_locators or None, batch, d_out, out_stride,
                                            d_status or None, stream or None))
 

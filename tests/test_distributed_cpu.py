@@ -106,3 +106,36 @@ def test_bench_rejects_mismatched_world_size():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8"], capture_output=True,
                        text=True, env=env, timeout=120)
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+def test_bench_labels_eight_gpus_as_config5():
+    """`--gpus 8` at the default config is BASELINE config 5 (8192 payloads of
+    1 MiB over 8 GPUs); its metric stays the headline one."""
+    import json
+    import subprocess
+
+    import bench
+
+    assert bench.workload_name(3, 8, 1024).startswith("BASELINE config 5")
+    assert bench.workload_name(3, 1, 1024) == "BASELINE config 3"
+    assert bench.metric_name(1024, 1 << 20) == bench.METRIC
+    assert "n=4096 shards, 4 MiB msgs" in bench.metric_name(4096, 4 << 20)
+    assert "n=256 shards, 64 KiB msgs" in bench.metric_name(256, 64 << 10)
+    env = dict(os.environ, NP_BENCH_DRYRUN="1", OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--batch", "2"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 8
+    assert line["workload"].startswith("BASELINE config 5") and "16 payloads over 8 GPUs" in line["workload"]
+    assert line["metric"] == bench.METRIC
+
+
+def test_host_cores_reports_affinity_and_quota():
+    import bench
+
+    hc = bench.host_cores()
+    assert hc["affinity"] >= 1 and 1 <= hc["used"] <= hc["affinity"]
+    if hc["quota"] is not None:
+        assert hc["used"] <= max(1, int(hc["quota"]))

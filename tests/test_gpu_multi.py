@@ -95,3 +95,36 @@ def test_multi_reports_need_more_shards(gpu):
         npa.reconstruct_batch_host_multi(ctxs, p, sh.ctypes.data, sl, n * sl, pres.ctypes.data, batch,
                                          out.ctypes.data, out.shape[1])
     assert e.value.fields == (k - 1, k, n)
+
+
+@pytest.mark.parametrize("n,k,err", [(1000, 256, npa.ParamterMustBePowerOf2), (1024, 300, npa.ParamterMustBePowerOf2)])
+def test_multi_checks_params_like_single_device(gpu, n, k, err):
+    """Bad parameters fail the multi entries exactly as the single-device entry
+    (also with batch == 0, where no per-device call runs)."""
+    ctxs = [npa.Context(0), npa.Context(0)]
+    bad = npa.CodeParams(n, k, n)
+    buf = np.zeros(64, np.uint8)
+    ptr = buf.ctypes.data
+    with pytest.raises(err):
+        npa.encode_batch_dev(bad, ptr, 16, 16, 0, ptr, 16, ctx=gpu)
+    for batch in (0, 2):
+        with pytest.raises(err):
+            npa.encode_batch_multi(ctxs, bad, [ptr, ptr], 16, 16, batch, [ptr, ptr], 16)
+        with pytest.raises(err):
+            npa.reconstruct_batch_multi(ctxs, bad, [ptr, ptr], 2, 2 * n, [ptr, ptr], batch, [ptr, ptr], 2 * k)
+        with pytest.raises(err):
+            npa.encode_batch_host_multi(ctxs, bad, ptr, 16, 16, batch, ptr, 16)
+        with pytest.raises(err):
+            npa.reconstruct_batch_host_multi(ctxs, bad, ptr, 2, 2 * n, ptr, batch, ptr, 2 * k)
+
+
+def test_multi_empty_batch_ok(gpu):
+    """batch == 0 with valid parameters: nothing to do, as the single-device entry."""
+    ctxs = [npa.Context(0), npa.Context(0)]
+    p = npa.CodeParams.derive_parameters(1024, 342)
+    buf = np.zeros(64, np.uint8)
+    ptr = buf.ctypes.data
+    bstride = p.n() * p.make_encoder(gpu).shard_len(16)
+    npa.encode_batch_dev(p, ptr, 16, 16, 0, ptr, bstride, ctx=gpu)
+    npa.encode_batch_multi(ctxs, p, [ptr, ptr], 16, 16, 0, [ptr, ptr], bstride)
+    npa.encode_batch_host_multi(ctxs, p, ptr, 16, 16, 0, ptr, bstride)

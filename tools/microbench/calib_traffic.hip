@@ -24,6 +24,55 @@ __global__ void read8(const uint2* __restrict__ in, uint32_t* __restrict__ sink,
   if (acc == 0x12345678u) sink[0] = acc;
 }
 
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+__device__ inline uint4 nt_ld(const uint4* p) { const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p)); return make_uint4(v.x, v.y, v.z, v.w); }
+__device__ inline void nt_st(uint4 v, uint4* p) { __builtin_nontemporal_store(v4u{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u*>(p)); }
+// 4 independent 16-byte loads in flight per lane before their stores
+__global__ __launch_bounds__(256) void copy16x4(const uint4* __restrict__ in, uint4* __restrict__ out, size_t n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += 4 * stride) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = (i + u * stride < n) ? in[i + u * stride] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) if (i + u * stride < n) out[i + u * stride] = v[u];
+  }
+}
+__global__ __launch_bounds__(256) void copy16x4nt(const uint4* __restrict__ in, uint4* __restrict__ out, size_t n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += 4 * stride) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = (i + u * stride < n) ? nt_ld(in + i + u * stride) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) if (i + u * stride < n) nt_st(v[u], out + i + u * stride);
+  }
+}
+__global__ __launch_bounds__(256) void copy8x8(const uint2* __restrict__ in, uint2* __restrict__ out, size_t n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += 8 * stride) {
+    uint2 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = (i + u * stride < n) ? in[i + u * stride] : make_uint2(0, 0);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) if (i + u * stride < n) out[i + u * stride] = v[u];
+  }
+}
+__global__ __launch_bounds__(256) void write16(uint4* __restrict__ out, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    out[i] = make_uint4(i, i, i, i);
+}
+__global__ __launch_bounds__(256) void read16(const uint4* __restrict__ in, uint32_t* __restrict__ sink, size_t n) {
+  uint32_t acc = 0;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += 4 * stride) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) if (i + u * stride < n) { const uint4 v = in[i + u * stride]; acc ^= v.x ^ v.y ^ v.z ^ v.w; }
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
 int main() {
   const size_t bytes = size_t(1) << 30;  // 1 GiB each
   const size_t n = bytes / 8;
@@ -43,21 +92,29 @@ int main() {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  for (int w = 8; w <= 16; w += 8) {
+  auto timed = [&](const char* name, double moved, auto launch) {
     float best = 1e30f;
     for (int it = 0; it < 5; ++it) {
       hipEventRecord(e0, 0);
-      if (w == 8)
-        hipLaunchKernelGGL(copy8, dim3(8192), dim3(256), 0, 0, a, b, n);
-      else
-        hipLaunchKernelGGL(copy16, dim3(8192), dim3(256), 0, 0, (const uint4*)a, (uint4*)b, bytes / 16);
+      launch();
       hipEventRecord(e1, 0);
       hipEventSynchronize(e1);
       float ms = 0;
       hipEventElapsedTime(&ms, e0, e1);
       if (ms < best) best = ms;
     }
-    printf("copy%d: %.3f ms for 1 GiB read + 1 GiB written -> %.0f GB/s\n", w, best, 2.0 * bytes / (best * 1e-3) / 1e9);
+    printf("%-34s %.3f ms -> %.0f GB/s\n", name, best, moved / (best * 1e-3) / 1e9);
+  };
+  const double two = 2.0 * bytes;
+  for (int grid : {8192, 2048, 1024}) {
+    printf("grid %d x 256 threads:\n", grid);
+    timed("  copy8 (1 GiB r + 1 GiB w)", two, [&] { hipLaunchKernelGGL(copy8, dim3(grid), dim3(256), 0, 0, a, b, n); });
+    timed("  copy16", two, [&] { hipLaunchKernelGGL(copy16, dim3(grid), dim3(256), 0, 0, (const uint4*)a, (uint4*)b, bytes / 16); });
+    timed("  copy16x4 (4 loads in flight)", two, [&] { hipLaunchKernelGGL(copy16x4, dim3(grid), dim3(256), 0, 0, (const uint4*)a, (uint4*)b, bytes / 16); });
+    timed("  copy16x4nt", two, [&] { hipLaunchKernelGGL(copy16x4nt, dim3(grid), dim3(256), 0, 0, (const uint4*)a, (uint4*)b, bytes / 16); });
+    timed("  copy8x8 (8 loads in flight)", two, [&] { hipLaunchKernelGGL(copy8x8, dim3(grid), dim3(256), 0, 0, a, b, n); });
+    timed("  write16 (1 GiB w)", bytes, [&] { hipLaunchKernelGGL(write16, dim3(grid), dim3(256), 0, 0, (uint4*)b, bytes / 16); });
+    timed("  read16x4 (1 GiB r)", bytes, [&] { hipLaunchKernelGGL(read16, dim3(grid), dim3(256), 0, 0, (const uint4*)a, sink, bytes / 16); });
   }
   hipFree(a);
   hipFree(b);
