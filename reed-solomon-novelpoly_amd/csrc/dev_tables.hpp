@@ -20,6 +20,7 @@ struct DevTables {
   const uint32_t* tower_pools;  // (65536 + 1) x 20 dwords: c < 256 subfield layout; [65536] = conversion
   const uint32_t* in_pools;     // 65536 x 20: Cantor -> tower
   const uint32_t* out_pools;    // 65536 x 20: tower -> Cantor
+  const uint32_t* tower_full_sub;  // 256 x 20: the full-map layout of the subfield elements (tower -> tower)
   const uint8_t* zeros;        // kZeroPageBytes of zeros (stand-in source for absent rows)
 };
 

@@ -191,6 +191,7 @@ size_t big_slots(const np_ctx* c, size_t tiles, uint32_t n, uint32_t k, bool rec
 // Caller holds the context lock.
 hipError_t launch_encode(np_ctx* c, const np::EncodeArgs& a, hipStream_t s) {
   if (np::fast_encode_supported(a.n, a.k)) return np::launch_encode_fast(c->T, a, s);
+  if (np::res_encode_supported(a.n, a.k) && np::res_enabled()) return np::launch_encode_res(c->T, a, s);
   if (np::big_encode_supported(a.n, a.k)) {
     const size_t tiles = ((a.payload_len + 2 * a.k - 1) / (2 * a.k) + 255) / 256;
     uint8_t* scr = nullptr;
@@ -224,7 +225,8 @@ constexpr size_t kStatusBytes = 2 * sizeof(uint32_t);  // per payload (launchers
 // go in slices.  Caller holds the context lock.
 hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream_t s) {
   const size_t own_status = a.status ? 0 : kStatusBytes;  // scratch bytes per payload for the status
-  if (np::fast_reconstruct_supported(a.n, a.k)) {
+  const bool res = np::res_reconstruct_supported(a.n, a.k) && np::res_enabled();
+  if (np::fast_reconstruct_supported(a.n, a.k) || res) {
     // per-payload decode rows + row multipliers and their tables (from the
     // caller's locators when given) and the status, then the decode
     const size_t stride = np::prefix_stride(a.n, a.k);
@@ -237,7 +239,7 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
       if (!a.status) sub.status = reinterpret_cast<uint32_t*>(scr + sub.batch * stride);
       if (e == hipSuccess) e = np::launch_prefix_locator(c->T, sub, scr, s);
       sub.prefix = scr;
-      if (e == hipSuccess) e = np::launch_reconstruct_fast(c->T, sub, s);
+      if (e == hipSuccess) e = res ? np::launch_reconstruct_res(c->T, sub, s) : np::launch_reconstruct_fast(c->T, sub, s);
       e = big_done(c, s, e);
       if (e != hipSuccess) return e;
     }
@@ -385,6 +387,7 @@ int np_ctx_create(int device, np_ctx** out) {
   if (e == hipSuccess) e = upload(c, t.tower_pools, &c->T.tower_pools);
   if (e == hipSuccess) e = upload(c, t.in_pools, &c->T.in_pools);
   if (e == hipSuccess) e = upload(c, t.out_pools, &c->T.out_pools);
+  if (e == hipSuccess) e = upload(c, t.tower_full_sub, &c->T.tower_full_sub);
   if (e == hipSuccess) e = upload(c, std::vector<uint8_t>(np::kZeroPageBytes, 0), &c->T.zeros);
   if (e == hipSuccess) {
     std::lock_guard<std::mutex> g(g_cfg_mu);
@@ -392,6 +395,7 @@ int np_ctx_create(int device, np_ctx** out) {
       e = np::configure_generic_kernels();
       if (e == hipSuccess) e = np::configure_fast_kernels();
       if (e == hipSuccess) e = np::configure_big_kernels();
+      if (e == hipSuccess) e = np::configure_res_kernels();
       if (e == hipSuccess) g_configured_devices.push_back(device);
     }
   }

@@ -460,6 +460,7 @@ __device__ __forceinline__ DevTables fresh_tables(const DevTables& T) {
   t.tower_pools = fresh(t.tower_pools);
   t.in_pools = fresh(t.in_pools);
   t.out_pools = fresh(t.out_pools);
+  t.tower_full_sub = fresh(t.tower_full_sub);
   t.zeros = fresh(t.zeros);
   return t;
 }

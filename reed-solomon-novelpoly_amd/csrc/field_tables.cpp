@@ -194,6 +194,12 @@ void build(HostTables& t) {
     build_pool([&](uint16_t x) { return conv(host_mul_add(t, x, cc)); }, &t.in_pools[at]);
     build_pool([&](uint16_t x) { return host_mul_add(t, conv(x), cc); }, &t.out_pools[at]);
   }
+  t.tower_full_sub.assign(256u * kPermPoolWords, 0);
+  for (uint32_t c = 0; c < 256; ++c) {
+    const uint16_t cc = static_cast<uint16_t>(c);
+    build_pool([&](uint16_t x) { return conv(host_mul_add(t, conv(x), cc)); },
+               &t.tower_full_sub[static_cast<size_t>(c) * kPermPoolWords]);
+  }
   // entry kFieldSize: the conversion's high-plane -> low-plane tables (b slots)
   build_sub_pool([](uint8_t) { return static_cast<uint8_t>(0); },
                  [&](uint8_t h) { return static_cast<uint8_t>(to_tower(t, static_cast<uint16_t>(h << 8)) & 0xff); },

@@ -44,6 +44,11 @@ struct HostTables {
   //  in_pools:    Cantor -> tower (the decode's premultiply);
   //  out_pools:   tower -> Cantor (the decode's postmultiply).
   std::vector<uint32_t> tower_pools, in_pools, out_pools;
+  // The full 16 x 16 map layout (build_pool, tower -> tower) of the 256
+  // subfield elements, whose tower_pools entries hold the subfield layout:
+  // for transforms whose levels mix skews inside and outside GF(2^8) (the
+  // k = 1024 resident kernels' level 0-1 groups at index 0).
+  std::vector<uint32_t> tower_full_sub;
 };
 
 // Built once, thread-safe.

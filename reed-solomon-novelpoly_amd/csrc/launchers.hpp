@@ -117,4 +117,15 @@ namespace np {
 hipError_t configure_generic_kernels();
 hipError_t configure_fast_kernels();
 hipError_t configure_big_kernels();
+
+// ---- k = 1024 with the whole transform of a 64-column tile resident in the
+// workgroup (kernels_res.hip); the decode reads the records of
+// launch_prefix_locator.  NP_RES=0 in the environment falls back to the
+// scratch kernels (kernels_big.hip) for A/B measurements. ----
+bool res_enabled();
+bool res_encode_supported(uint32_t n, uint32_t k);
+bool res_reconstruct_supported(uint32_t n, uint32_t k);
+hipError_t launch_encode_res(const DevTables& T, const EncodeArgs& a, hipStream_t s);
+hipError_t launch_reconstruct_res(const DevTables& T, const ReconstructArgs& a, hipStream_t s);
+hipError_t configure_res_kernels();
 }  // namespace np

@@ -97,16 +97,20 @@ def test_multi_reports_need_more_shards(gpu):
     assert e.value.fields == (k - 1, k, n)
 
 
-@pytest.mark.parametrize("n,k,err", [(1000, 256, npa.ParamterMustBePowerOf2), (1024, 300, npa.ParamterMustBePowerOf2)])
-def test_multi_checks_params_like_single_device(gpu, n, k, err):
+@pytest.mark.parametrize("n,k", [(1000, 300), (1000, 256), (1024, 300), (1024, 1024)])
+def test_multi_checks_params_like_single_device(gpu, n, k):
     """Bad parameters fail the multi entries exactly as the single-device entry
-    (also with batch == 0, where no per-device call runs)."""
+    (also with batch == 0, where no per-device call runs): ParamterMustBePowerOf2
+    when neither n nor k is a power of two (the crate's rule), an invalid
+    argument otherwise."""
     ctxs = [npa.Context(0), npa.Context(0)]
     bad = npa.CodeParams(n, k, n)
     buf = np.zeros(64, np.uint8)
     ptr = buf.ctypes.data
-    with pytest.raises(err):
+    with pytest.raises(Exception) as single:
         npa.encode_batch_dev(bad, ptr, 16, 16, 0, ptr, 16, ctx=gpu)
+    err = type(single.value)
+    assert (err is npa.ParamterMustBePowerOf2) == (n == 1000 and k == 300)
     for batch in (0, 2):
         with pytest.raises(err):
             npa.encode_batch_multi(ctxs, bad, [ptr, ptr], 16, 16, batch, [ptr, ptr], 16)

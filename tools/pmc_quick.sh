@@ -5,7 +5,7 @@ TAG=$1; shift
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pq
-timeout -s KILL 120 rocprofv3 --pmc "$@" -d gpurun_out/pq/$TAG --output-format csv -- python3 bench.py --no-cpu --steps 2 --warmup 1 > gpurun_out/pq/$TAG.log 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --pmc "$@" -d gpurun_out/pq/$TAG --output-format csv -- python3 bench.py --no-cpu --steps 2 --warmup 1 ${BENCH_ARGS} > gpurun_out/pq/$TAG.log 2>&1 || exit 1
 f=$(ls -t gpurun_out/pq/$TAG/*/*_counter_collection.csv | head -1)
 python3 - "$f" <<'PY'
 import csv, sys, collections
