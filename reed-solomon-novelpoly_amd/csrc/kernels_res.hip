@@ -637,14 +637,15 @@ __device__ __forceinline__ uint32_t lane_rows_present(const uint8_t* pres, uint3
   return m;
 }
 
-// This lane's 8 bytes of rows row0 + 64 w + 16 u + i (absent: zeros).
-__device__ __forceinline__ void load_lane_rows(uint2 (&raw)[16], const uint8_t* sh, size_t shard_len, uint32_t row0,
+// This lane's 8 bytes of rows row0 + 64 w + 16 u + i0 + i, i < NR (absent: zeros).
+template <int NR = 16>
+__device__ __forceinline__ void load_lane_rows(uint2 (&raw)[NR], const uint8_t* sh, size_t shard_len, uint32_t row0,
                                                uint32_t pm, const Res& r, uint32_t ncols, bool full,
-                                               const uint8_t* zeros) {
-  const uint8_t* base = sh + static_cast<size_t>(row0 + 64u * r.w + 16u * r.u) * shard_len;
+                                               const uint8_t* zeros, int i0 = 0) {
+  const uint8_t* base = sh + static_cast<size_t>(row0 + 64u * r.w + 16u * r.u + i0) * shard_len;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const uint8_t* src = ((pm >> i) & 1u) ? base + static_cast<size_t>(i) * shard_len : zeros;
+  for (int i = 0; i < NR; ++i) {
+    const uint8_t* src = ((pm >> (i0 + i)) & 1u) ? base + static_cast<size_t>(i) * shard_len : zeros;
     raw[i] = load4(src, r.cq, ncols, full);
   }
 }
@@ -679,86 +680,106 @@ __host__ __device__ constexpr int res_seg(int step) {  // segments 2, 3, 1, 0 (N
   return NQ == 4 ? (step == 0 ? 2 : step == 1 ? 3 : 3 - step) : 1 - step;
 }
 
+// Step STEP of the segment sweep: x_q = IFFT(1024, 1024 q)(premultiplied
+// segment q), folded into d (A, HD layout).  Steps are compile-time: each has
+// one CQ instance (its GEN) and its own fold, with no runtime branch between
+// instances (a branch over instances inside a loop made the allocator spill).
+template <int NQ, int STEP>
+__device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructArgs& a, uint8_t* tile,
+                                         const uint8_t* pools, const uint8_t* pres, const uint8_t* sh,
+                                         uint8_t* out_tile, uint32_t ncols, bool full, bool out16, uint32_t (&AL)[16],
+                                         uint32_t (&AH)[16]) {
+  constexpr int q = res_seg<NQ>(STEP);
+  constexpr uint32_t I = static_cast<uint32_t>(q) * kRK;
+  const Res rr = res_coords();  // opaque per step: lane-derived values are not hoisted across steps
+  uint32_t XL[16], XH[16];
+  {
+    const uint32_t pm = lane_rows_present(pres, I, rr);
+    uint2 raw[8];
+    load_lane_rows<8>(raw, sh, a.shard_len, I, pm, rr, ncols, full, T.zeros, 0);
+    __syncthreads();  // the previous step's HD read is done with the tile
+    stage_row_tables(tile, pools, pres, I, rr.tid, false);
+    __syncthreads();
+    // premultiply by the row multipliers (inc_reconstruct.rs:72-74; Cantor
+    // in, tower out), in two halves of 8 rows (register pressure)
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      if (half == 1) load_lane_rows<8>(raw, sh, a.shard_len, I, pm, rr, ncols, full, T.zeros, 8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        uint32_t l, h;
+        blk_to_quad(raw[i], l, h);
+        const FullT m = row_table(tile, 64u * rr.w + 16u * rr.u + 8 * half + i);
+        qmul_set_vv(XL[8 * half + i], XH[8 * half + i], l, h, m);
+      }
+    }
+  }
+  if constexpr ((kExp & 16384) != 0 && STEP == 0) {  // experiment: the first step's premultiplied rows
+    res_copy_out(out_tile, XL, XH, rr, ncols, out16);
+    return false;
+  }
+  rcq_levels<true, res_gen(I)>(T, I, rr, XL, XH);
+  if constexpr ((kExp & 32768) != 0 && STEP == 0) {  // experiment: the first step after its CQ levels
+    res_copy_out(out_tile, XL, XH, rr, ncols, out16);
+    return false;
+  }
+  __syncthreads();  // every wave has read its row tables
+  rcq_write(tile, fresh_v(rr.cqb), XL, XH);
+  __syncthreads();
+  rh_read<kHA>(tile, fresh_v(rr.hab), XL, XH);
+  ha_levels<true>(T, I, rr, XL, XH);
+  __syncthreads();
+  rh_write<kHA>(tile, fresh_v(rr.hab), XL, XH);
+  __syncthreads();
+  rh_read<kHD>(tile, fresh_v(rr.hdb), XL, XH);
+  hd_levels<true>(T, I, XL, XH);
+  // fold x_q into d (kernels_fast.hip rec_segments)
+  if constexpr (STEP == 0) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) AL[j] = XL[j], AH[j] = XH[j];
+  } else if constexpr (q == 0) {
+    if constexpr (NQ == 2) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) AL[j] ^= XL[j], AH[j] ^= XH[j];
+    }
+    add_derivative16(AL, XL, rr.l);
+    add_derivative16(AH, XH, rr.l);
+  } else if constexpr (NQ == 4 && q == 3) {  // A = x2 ^ beta (x2 ^ x3)
+    uint32_t beta[20];
+    pool_of<true>(T, 2u, beta);  // beta = Cantor(2), in GF(2^8)
+    const Mult m = make_mult(beta);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      XL[j] ^= AL[j];
+      XH[j] ^= AH[j];
+      qmul_sub(AL[j], AH[j], XL[j], XH[j], m);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) AL[j] ^= XL[j], AH[j] ^= XH[j];
+  }
+  return true;
+}
+
+template <int NQ, int... STEP>
+__device__ __forceinline__ bool res_sweep(const DevTables& T, const ReconstructArgs& a, uint8_t* tile,
+                                          const uint8_t* pools, const uint8_t* pres, const uint8_t* sh,
+                                          uint8_t* out_tile, uint32_t ncols, bool full, bool out16,
+                                          uint32_t (&AL)[16], uint32_t (&AH)[16], std::integer_sequence<int, STEP...>) {
+  return (res_step<NQ, STEP>(T, a, tile, pools, pres, sh, out_tile, ncols, full, out16, AL, AH) && ...);
+}
+
 // One tile; NQ segments of 1024 rows (a.n = NQ * 1024, or a trusted 2-segment
 // prefix of n = 4096).
 template <int NQ>
 __device__ __forceinline__ void res_decode_tile(const DevTables& T, const ReconstructArgs& a, uint8_t* tile,
                                                 const uint8_t* pools, const uint8_t* pres, const uint8_t* sh,
                                                 uint8_t* out_tile, uint32_t ncols, bool full, bool out16) {
-  const Res r = res_coords();
   uint32_t AL[16], AH[16];
-#pragma unroll 1
-  for (int step = 0; step < NQ; ++step) {
-    const uint32_t q = uniform(static_cast<uint32_t>(res_seg<NQ>(step)));
-    const uint32_t I = q * kRK;
-    const Res rr = res_coords();  // opaque per step: lane-derived values are not hoisted across the loop
-    uint32_t XL[16], XH[16];
-    {
-      const uint32_t pm = lane_rows_present(pres, I, rr);
-      uint2 raw[16];
-      load_lane_rows(raw, sh, a.shard_len, I, pm, rr, ncols, full, T.zeros);
-      __syncthreads();  // the previous step's HD read is done with the tile
-      stage_row_tables(tile, pools, pres, I, rr.tid, false);
-      __syncthreads();
-      // premultiply by the row multipliers (inc_reconstruct.rs:72-74; Cantor in, tower out)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        uint32_t l, h;
-        blk_to_quad(raw[i], l, h);
-        const FullT m = row_table(tile, 64u * rr.w + 16u * rr.u + i);
-        qmul_set_vv(XL[i], XH[i], l, h, m);
-      }
-    }
-    if constexpr ((kExp & 16384) != 0) {  // experiment: the first step's premultiplied rows
-      res_copy_out(out_tile, XL, XH, rr, ncols, out16);
-      return;
-    }
-    if (q == 0)
-      rcq_levels<true, res_gen(0)>(T, I, rr, XL, XH);
-    else if (q == 1)
-      rcq_levels<true, res_gen(1024)>(T, I, rr, XL, XH);
-    else
-      rcq_levels<true, res_gen(2048)>(T, I, rr, XL, XH);
-    if constexpr ((kExp & 32768) != 0) {  // experiment: the first step after its CQ levels
-      res_copy_out(out_tile, XL, XH, rr, ncols, out16);
-      return;
-    }
-    __syncthreads();  // every wave has read its row tables
-    rcq_write(tile, fresh_v(rr.cqb), XL, XH);
-    __syncthreads();
-    rh_read<kHA>(tile, fresh_v(rr.hab), XL, XH);
-    ha_levels<true>(T, I, rr, XL, XH);
-    __syncthreads();
-    rh_write<kHA>(tile, fresh_v(rr.hab), XL, XH);
-    __syncthreads();
-    rh_read<kHD>(tile, fresh_v(rr.hdb), XL, XH);
-    hd_levels<true>(T, I, XL, XH);
-    // fold x_q into d (kernels_fast.hip rec_segments)
-    if (step == 0) {
-#pragma unroll
-      for (int j = 0; j < 16; ++j) AL[j] = XL[j], AH[j] = XH[j];
-    } else if (q == 0) {
-      if (NQ == 2) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) AL[j] ^= XL[j], AH[j] ^= XH[j];
-      }
-      add_derivative16(AL, XL, rr.l);
-      add_derivative16(AH, XH, rr.l);
-    } else if (NQ == 4 && q == 3) {  // A = x2 ^ beta (x2 ^ x3)
-      uint32_t beta[20];
-      pool_of<true>(T, 2u, beta);  // beta = Cantor(2), in GF(2^8)
-      const Mult m = make_mult(beta);
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        XL[j] ^= AL[j];
-        XH[j] ^= AH[j];
-        qmul_sub(AL[j], AH[j], XL[j], XH[j], m);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 16; ++j) AL[j] ^= XL[j], AH[j] ^= XH[j];
-    }
-  }
+  if (!res_sweep<NQ>(T, a, tile, pools, pres, sh, out_tile, ncols, full, out16, AL, AH,
+                     std::make_integer_sequence<int, NQ>{}))
+    return;
+  const Res r = res_coords();
   if constexpr ((kExp & 8192) != 0) {  // experiment (tools/res_debug_rec.py): d in natural blocks, tower coordinates
     const uint32_t c = 4u * r.w + (r.l >> 4);
 #pragma unroll
@@ -822,12 +843,13 @@ __device__ __forceinline__ void res_copy_tile(const ReconstructArgs& a, const ui
 template <int SERVE>
 __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(4))) void k_reconstruct_res(
     DevTables T, ReconstructArgs a, uint32_t nsyms, uint32_t tiles) {
+  // SERVE = 1: copies (nq = 1); 2: 2-segment decodes; 4: 4-segment decodes
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const TileRef tr = tile_of(blockIdx.x, tiles, (a.batch & 7u) == 0);
   const uint32_t pb = tr.pb, tl = tr.tl;
   const uint8_t* rec = a.prefix + static_cast<size_t>(pb) * prefix_stride_c(a.n, a.k);
   const uint32_t nq = uniform(rec[0]);
-  if (SERVE == 4 ? nq != 4u : (nq == 0u || nq > 2u)) return;
+  if (nq != static_cast<uint32_t>(SERVE)) return;
   const uint8_t* pools = rec + prefix_pools_offset(a.n);
   const uint8_t* pres = a.present + static_cast<size_t>(pb) * a.n;
   const uint32_t col0 = tl * kRC;
@@ -837,14 +859,10 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(4))) void k
   const bool full =
       ncols == kRC && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
   const bool out16 = ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 15u) == 0;
-  if constexpr (SERVE == 4) {
-    res_decode_tile<4>(T, a, smem, pools, pres, sh, out_tile, ncols, full, out16);
-  } else {
-    if (nq == 1u)
-      res_copy_tile(a, sh, out_tile, ncols, full, out16, T);
-    else
-      res_decode_tile<2>(T, a, smem, pools, pres, sh, out_tile, ncols, full, out16);
-  }
+  if constexpr (SERVE == 1)
+    res_copy_tile(a, sh, out_tile, ncols, full, out16, T);
+  else
+    res_decode_tile<SERVE>(T, a, smem, pools, pres, sh, out_tile, ncols, full, out16);
 }
 
 }  // namespace
@@ -867,7 +885,9 @@ hipError_t launch_reconstruct_res(const DevTables& T, const ReconstructArgs& a, 
   const uint32_t tiles = static_cast<uint32_t>((nsyms + kRC - 1) / kRC);
   const size_t blocks = a.batch * tiles;
   if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
-  k_reconstruct_res<2><<<static_cast<uint32_t>(blocks), kRT, kRTileBytes, s>>>(T, a, static_cast<uint32_t>(nsyms), tiles);
+  k_reconstruct_res<1><<<static_cast<uint32_t>(blocks), kRT, 0, s>>>(T, a, static_cast<uint32_t>(nsyms), tiles);
+  if (a.n == 2048 || a.trusted)
+    k_reconstruct_res<2><<<static_cast<uint32_t>(blocks), kRT, kRTileBytes, s>>>(T, a, static_cast<uint32_t>(nsyms), tiles);
   if (a.n == 4096)
     k_reconstruct_res<4><<<static_cast<uint32_t>(blocks), kRT, kRTileBytes, s>>>(T, a, static_cast<uint32_t>(nsyms), tiles);
   return hipGetLastError();
