@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <array>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -112,7 +113,8 @@ struct np_ctx {
   // device buffers for one sub-batch; created on first use.
   static constexpr int kPipe = 3;
   hipStream_t pipe_s[kPipe] = {};
-  DevBuf pipe_in[kPipe], pipe_out[kPipe], pipe_pres[kPipe];
+  DevBuf pipe_in[kPipe], pipe_out[kPipe];
+  DevBuf pipe_pres;  // the present mask of a whole host reconstruct call
 };
 
 namespace {
@@ -421,9 +423,9 @@ void np_ctx_destroy(np_ctx* c) {
     if (c->pipe_s[i]) (void)hipStreamSynchronize(c->pipe_s[i]);
     c->pipe_in[i].release();
     c->pipe_out[i].release();
-    c->pipe_pres[i].release();
     if (c->pipe_s[i]) (void)hipStreamDestroy(c->pipe_s[i]);
   }
+  c->pipe_pres.release();
   c->h_in.release();
   c->h_out.release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -517,19 +519,43 @@ hipError_t pipe_sync(np_ctx* c, hipError_t e) {
   return e;
 }
 
-// Rows of each payload the reconstruct kernels read: on the fast path only the
-// k systematic rows when all of them are present (the output is those rows,
-// kernels_fast.hip k_prefix_locator), otherwise -- and on every other path --
-// all n rows: the reference decodes from every present row
-// (inc_reconstruct.rs:61-85).
+// Rows of each payload the reconstruct kernels read: on the fast, resident and
+// big paths only the k systematic rows when all of them are present (the
+// output is those rows: kernels_fast.hip k_prefix_locator, kernels_big.hip
+// kBigCopy), otherwise -- and on the generic path -- all n rows: the
+// reference decodes from every present row (inc_reconstruct.rs:61-85).
 size_t rows_needed(const np_code_params* p, const uint8_t* present, size_t batch) {
-  if (!np::fast_reconstruct_supported(static_cast<uint32_t>(p->n), static_cast<uint32_t>(p->k))) return p->n;
+  const uint32_t n = static_cast<uint32_t>(p->n), k = static_cast<uint32_t>(p->k);
+  if (!np::fast_reconstruct_supported(n, k) && !np::res_reconstruct_supported(n, k) &&
+      !np::big_reconstruct_supported(n, k))
+    return p->n;
   for (size_t b = 0; b < batch; ++b) {
     const uint8_t* pr = present + b * p->n;
     for (size_t v = 0; v < p->k; ++v)
       if (!pr[v]) return p->n;
   }
   return p->k;
+}
+
+// Workgroups of the present-row gather (launch_copy_rows): 32 read host
+// memory at the PCIe rate (tools/microbench/h2d_gather.hip).
+constexpr uint32_t kGatherBlocks = 32;
+
+// Device address of [p, p + bytes) when the whole range lies in one pinned host
+// allocation mapped into the device address space (hipHostMalloc, torch's
+// pin_memory, hipHostRegister), else nullptr (pageable memory).
+const uint8_t* mapped_host_range(const uint8_t* p, size_t bytes) {
+  if (bytes == 0 || std::getenv("NP_NO_GATHER")) return nullptr;
+  hipPointerAttribute_t a0{}, a1{};
+  if (hipPointerGetAttributes(&a0, p) != hipSuccess || hipPointerGetAttributes(&a1, p + bytes - 1) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (a0.type != hipMemoryTypeHost || a1.type != hipMemoryTypeHost || !a0.devicePointer || !a1.devicePointer)
+    return nullptr;
+  const uint8_t* d0 = static_cast<const uint8_t*>(a0.devicePointer);
+  if (static_cast<const uint8_t*>(a1.devicePointer) != d0 + (bytes - 1)) return nullptr;
+  return d0;
 }
 
 }  // namespace
@@ -584,28 +610,40 @@ int np_reconstruct_batch_host(np_ctx* c, const np_code_params* p, const uint8_t*
   const size_t rows = rows_needed(p, present, batch), in_bytes = rows * shard_len, dstride = p->n * shard_len;
   std::lock_guard<std::mutex> g(c->mu);
   (void)hipSetDevice(c->device);
+  // Pinned shards: a kernel reads only the present rows over PCIe (the
+  // gather: 682 of 1024 rows at config 3, 1366 of 4096 at config 4); pageable
+  // ones go by one 2-D DMA of the first `rows` rows of every payload.  The
+  // outputs go by DMA either way (the link shares badly between
+  // kernel reads of host memory and any D2H, but a DMA D2H is the best of it).
+  const uint8_t* mapped = mapped_host_range(shards, (batch - 1) * bstride + in_bytes);
   hipError_t e = pipe_init(c);
   const size_t sb = std::min(batch, std::max<size_t>(1, kPipeSlotBytes / (in_bytes + olen)));
   for (int i = 0; e == hipSuccess && i < np_ctx::kPipe; ++i) {
     e = c->pipe_in[i].ensure((sb - 1) * dstride + in_bytes);
     if (e == hipSuccess) e = c->pipe_out[i].ensure(sb * olen);
-    if (e == hipSuccess) e = c->pipe_pres[i].ensure(sb * p->n);
   }
+  // the whole present mask up front, synchronously: from pageable memory an
+  // asynchronous copy per sub-batch would wait for its stream, and with it the
+  // enqueueing of the next sub-batches
+  if (e == hipSuccess) e = c->pipe_pres.ensure(batch * p->n);
+  if (e == hipSuccess) e = hipMemcpy(c->pipe_pres.p, present, batch * p->n, hipMemcpyHostToDevice);
   size_t slot = 0;
   for (size_t b0 = 0; e == hipSuccess && b0 < batch; b0 += sb, slot = (slot + 1) % np_ctx::kPipe) {
     const size_t cnt = std::min(sb, batch - b0);
     hipStream_t s = c->pipe_s[slot];
     uint8_t* din = c->pipe_in[slot].as<uint8_t>();
     uint8_t* dout = c->pipe_out[slot].as<uint8_t>();
-    e = hipMemcpy2DAsync(din, dstride, shards + b0 * bstride, bstride, in_bytes, cnt, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(c->pipe_pres[slot].p, present + b0 * p->n, cnt * p->n, hipMemcpyHostToDevice, s);
+    const uint8_t* dpres = c->pipe_pres.as<uint8_t>() + b0 * p->n;
+    e = mapped ? np::launch_copy_rows(mapped + b0 * bstride, bstride, din, dstride, shard_len, dpres,
+                                      static_cast<uint32_t>(p->n), static_cast<uint32_t>(rows), cnt, kGatherBlocks, s)
+               : hipMemcpy2DAsync(din, dstride, shards + b0 * bstride, bstride, in_bytes, cnt, hipMemcpyHostToDevice,
+                                  s);
     if (e == hipSuccess) {
       np::ReconstructArgs a{};
       a.shards = din;
       a.shard_len = shard_len;
       a.batch_stride = dstride;
-      a.present = c->pipe_pres[slot].as<uint8_t>();
+      a.present = dpres;
       a.locators = nullptr;  // computed on the device
       a.batch = cnt;
       a.n = static_cast<uint32_t>(p->n);

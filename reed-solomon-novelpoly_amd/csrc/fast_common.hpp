@@ -27,7 +27,7 @@ constexpr int kExp = NP_EXP;
 // With bit 7 as well, lane 0 of every wave writes its own 32 stamps
 // (dbg[32 * wave + slot], tools/wave_stamps.py).
 __device__ __forceinline__ void stamp(uint64_t* dbg, int slot) {
-  if constexpr ((kExp & 64) && (kExp & 128)) {
+  if constexpr ((kExp & 64) != 0 && (kExp & 128) != 0) {
     if ((threadIdx.x & 63u) == 0) dbg[32u * (threadIdx.x >> 6) + slot] = __builtin_amdgcn_s_memtime();
   } else if constexpr (kExp & 64) {
     if (threadIdx.x == 0) dbg[slot] = __builtin_amdgcn_s_memtime();

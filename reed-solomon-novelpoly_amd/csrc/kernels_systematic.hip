@@ -4,6 +4,8 @@
 // no field arithmetic.  HBM-bound: a workgroup moves a 64 x 64 symbol tile
 // through LDS so that both the row reads (shard j, 64 symbols = 128 B) and the
 // column writes (message column c, 64 symbols = 128 B) are contiguous.
+#include <algorithm>
+
 #include "device_common.hpp"
 #include "launchers.hpp"
 
@@ -45,6 +47,55 @@ __global__ __launch_bounds__(256) void k_systematic(const uint8_t* shards, size_
   }
 }
 
+
+// Row copies between device memory and host memory mapped into the device
+// address space (pinned: hipHostMalloc, torch's pin_memory, hipHostRegister);
+// np_reconstruct_batch_host's gather of the present rows: dst[b][v] =
+// src[b][v] (row_bytes each) for b < count, v < rows, skipping rows whose
+// present flag (present[b * n + v], when given) is 0.  Absent rows of dst are
+// left as they are: the reconstruct kernels never read them (the reference
+// replaces them by zeros, inc_reconstruct.rs:61-85).  One wave per 4 KiB chunk
+// of a row, a few persistent workgroups: 32 of them already read host memory
+// at the PCIe rate (tools/microbench/h2d_gather.hip), and a small grid stays
+// resident next to the decode kernels of the other pipeline streams instead
+// of queueing behind them.
+constexpr uint32_t kXferWaves = 4;
+constexpr size_t kXferChunk = 4096;
+
+__global__ __launch_bounds__(64 * kXferWaves) void k_copy_rows(const uint8_t* __restrict__ src, size_t sstride,
+                                                              uint8_t* __restrict__ dst, size_t dstride,
+                                                              size_t row_bytes, const uint8_t* __restrict__ present,
+                                                              uint32_t n, uint32_t rows, size_t chunks, size_t total) {
+  const uint32_t lane = threadIdx.x & 63;
+  const size_t waves = static_cast<size_t>(gridDim.x) * kXferWaves;
+  const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) | sstride | dstride |
+                     row_bytes) & 15) == 0;
+  for (size_t u = static_cast<size_t>(blockIdx.x) * kXferWaves + (threadIdx.x >> 6); u < total; u += waves) {
+    const size_t r = u / chunks, ch = u - r * chunks;
+    const size_t b = r / rows, v = r - b * rows;
+    if (present && !present[b * n + v]) continue;
+    const size_t off = ch * kXferChunk, len = row_bytes - off < kXferChunk ? row_bytes - off : kXferChunk;
+    const uint8_t* s = src + b * sstride + v * row_bytes + off;
+    uint8_t* d = dst + b * dstride + v * row_bytes + off;
+    if (vec) {
+      const uint4* s4 = reinterpret_cast<const uint4*>(s);
+      uint4* d4 = reinterpret_cast<uint4*>(d);
+      const size_t q = len / 16;
+      if (q == 256) {  // a whole chunk: four 1 KiB loads in flight per wave
+        const uint4 x0 = s4[lane], x1 = s4[lane + 64], x2 = s4[lane + 128], x3 = s4[lane + 192];
+        d4[lane] = x0;
+        d4[lane + 64] = x1;
+        d4[lane + 128] = x2;
+        d4[lane + 192] = x3;
+      } else {
+        for (size_t i = lane; i < q; i += 64) d4[i] = s4[i];
+      }
+    } else {
+      for (size_t i = lane; i < len; i += 64) d[i] = s[i];
+    }
+  }
+}
+
 }  // namespace
 
 hipError_t launch_systematic(const uint8_t* shards, size_t shard_len, size_t bstride, uint32_t k, size_t batch,
@@ -58,6 +109,17 @@ hipError_t launch_systematic(const uint8_t* shards, size_t shard_len, size_t bst
                                                               static_cast<uint32_t>(syms), out, ostride,
                                                               static_cast<uint32_t>(ctiles),
                                                               static_cast<uint32_t>(jtiles));
+  return hipGetLastError();
+}
+
+hipError_t launch_copy_rows(const uint8_t* src, size_t sstride, uint8_t* dst, size_t dstride, size_t row_bytes,
+                            const uint8_t* present, uint32_t n, uint32_t rows, size_t count, uint32_t blocks,
+                            hipStream_t s) {
+  const size_t chunks = (row_bytes + kXferChunk - 1) / kXferChunk, total = count * rows * chunks;
+  if (total == 0) return hipSuccess;
+  const size_t grid = std::min<size_t>((total + kXferWaves - 1) / kXferWaves, blocks);
+  k_copy_rows<<<static_cast<uint32_t>(grid), 64 * kXferWaves, 0, s>>>(src, sstride, dst, dstride, row_bytes, present,
+                                                                     n, rows, chunks, total);
   return hipGetLastError();
 }
 

@@ -70,6 +70,12 @@ hipError_t launch_decode_main(const DevTables& T, uint16_t* codeword, uint32_t u
 // out[b][2(c*k + j) .. +2) = shards[b][j][2c .. +2) for j < k, c < shard_len / 2.
 hipError_t launch_systematic(const uint8_t* shards, size_t shard_len, size_t bstride, uint32_t k, size_t batch,
                              uint8_t* out, size_t ostride, hipStream_t s);
+// dst[b][v] = src[b][v] (row_bytes each) for b < count, v < rows, skipping rows
+// with present[b * n + v] == 0 when present is given; src or dst may be host
+// memory mapped into the device address space.  `blocks` caps the grid.
+hipError_t launch_copy_rows(const uint8_t* src, size_t sstride, uint8_t* dst, size_t dstride, size_t row_bytes,
+                            const uint8_t* present, uint32_t n, uint32_t rows, size_t count, uint32_t blocks,
+                            hipStream_t s);
 
 // ---- fast path (kernels_fast.hip) ----
 // Returns true if a specialised kernel serves (n, k).

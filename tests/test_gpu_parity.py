@@ -605,12 +605,27 @@ def test_reconstruct_from_systematic_batch_dev(gpu, oracle, nw, kw, plen, batch)
         assert want[:plen] == pls[b].tobytes()
 
 
-@pytest.mark.parametrize("nw,kw,plen,batch", [(1024, 342, 512 * 256, 9), (256, 86, 128 * 99 + 1, 7),
-                                              (300, 100, 5000, 3), (4096, 1366, 2048 * 40, 2)])
-def test_host_batch_pipeline(gpu, oracle, nw, kw, plen, batch):
+def _host_array(shape, fill, pinned, offset=0):
+    """A host array, pageable (numpy) or pinned (torch.pin_memory: mapped into
+    the device address space, so np_reconstruct_batch_host gathers its present
+    rows with a kernel), starting `offset` bytes into its allocation."""
+    if not pinned:
+        return np.full(shape, fill, dtype=np.uint8)
+    import torch
+    size = int(np.prod(shape))
+    t = torch.full((size + offset,), fill, dtype=torch.uint8).pin_memory()
+    return t.numpy()[offset:].reshape(shape)  # the view's base keeps the pinned tensor alive
+
+
+@pytest.mark.parametrize("pinned", [False, True], ids=["pageable", "pinned"])
+@pytest.mark.parametrize("nw,kw,plen,batch,offset", [(1024, 342, 512 * 256, 9, 0), (256, 86, 128 * 99 + 1, 7, 0),
+                                                     (300, 100, 5000, 3, 2), (4096, 1366, 2048 * 40, 2, 0),
+                                                     (1024, 342, 512 * 256, 3, 6)])
+def test_host_batch_pipeline(gpu, oracle, nw, kw, plen, batch, offset, pinned):
     """np_encode_batch_host / np_reconstruct_batch_host (host buffers, pipelined
     sub-batches over several streams) give the oracle's shards and payloads;
-    strided host layouts included."""
+    strided host layouts, unaligned starts, pinned host memory (present rows
+    gathered over PCIe by a kernel) and garbage in the absent rows included."""
     p = npa.CodeParams.derive_parameters(nw, kw)
     n, k = p.n(), p.k()
     sl = p.make_encoder(gpu).shard_len(plen)
@@ -620,7 +635,7 @@ def test_host_batch_pipeline(gpu, oracle, nw, kw, plen, batch):
         pay[b, :plen] = np.frombuffer(synth.payload(9100 + b, plen), dtype=np.uint8)
     wn = p.wanted_n
     bstride = n * sl + 64
-    sh = np.full((batch, bstride), 0xAB, dtype=np.uint8)
+    sh = _host_array((batch, bstride), 0xAB, pinned, offset)
     npa.encode_batch_host(p, pay.ctypes.data, plen, pstride, batch, sh.ctypes.data, bstride, ctx=gpu)
     for b in range(batch):
         st, want = oracle.encode(pay[b, :plen].tobytes(), n, k, wn)
@@ -634,13 +649,17 @@ def test_host_batch_pipeline(gpu, oracle, nw, kw, plen, batch):
         pres[b, :wn] = 1
         gone = (wn - k) if b % 2 else (wn - k) // 3
         pres[b, rng.choice(wn, gone, replace=False)] = 0
+    recvs = [[sh[b, i * sl:(i + 1) * sl].tobytes() if pres[b, i] else None for i in range(n)] for b in range(batch)]
+    for b in range(batch):  # the engine must not read absent rows
+        for i in np.flatnonzero(pres[b] == 0):
+            sh[b, i * sl:(i + 1) * sl] = 0x5C
     olen = (sl // 2) * 2 * k
     ostride = olen + 5
-    out = np.zeros((batch, ostride), dtype=np.uint8)
+    out = _host_array((batch, ostride), 0, pinned)
     npa.reconstruct_batch_host(p, sh.ctypes.data, sl, bstride, pres.ctypes.data, batch, out.ctypes.data, ostride,
                                ctx=gpu)
     for b in range(batch):
-        recv = [sh[b, i * sl:(i + 1) * sl].tobytes() if pres[b, i] else None for i in range(n)]
+        recv = recvs[b]
         st, want = oracle.reconstruct(recv, n, k)
         assert st == 0 and out[b, :olen].tobytes() == want, b
         assert want[:plen] == pay[b, :plen].tobytes()

@@ -58,20 +58,38 @@ def timed(fn):
 
 
 t_enc = timed(lambda: npa.encode_batch_host(p, h_pay.data_ptr(), plen, plen, B, h_sh.data_ptr(), n * sl, ctx=ctx))
-t_rec = timed(lambda: npa.reconstruct_batch_host(p, h_sh.data_ptr(), sl, n * sl, pres.ctypes.data, B,
-                                                 h_out.data_ptr(), olen, ctx=ctx))
-ok = torch.equal(h_out[:, :plen], h_pay)
+def rec():
+    npa.reconstruct_batch_host(p, h_sh.data_ptr(), sl, n * sl, pres.ctypes.data, B, h_out.data_ptr(), olen, ctx=ctx)
+
+
+# pinned shards: the engine gathers the present rows with a kernel reading
+# mapped host memory; NP_NO_GATHER=1 forces the pageable-memory path (one 2-D
+# DMA of the first rows_needed rows of every payload) for comparison
+os.environ["NP_NO_GATHER"] = "1"
+t_dma = timed(rec)
+ok_dma = torch.equal(h_out[:, :plen], h_pay)
+del os.environ["NP_NO_GATHER"]
+h_out.zero_()
+t_rec = timed(rec)
+ok = torch.equal(h_out[:, :plen], h_pay) and ok_dma
 # bytes crossing PCIe: encode P in + n*sl out; reconstruct the rows the engine
-# ships (engine.cpp rows_needed: the k systematic rows when every payload of the
-# batch has them all, else all n rows: exactness) in (+ flags) and 2k*sl/2 out
-rows = k if all(pres[b, :k].all() for b in range(B)) else n
+# reads (engine.cpp rows_needed: the k systematic rows when every payload of the
+# batch has them all, else all n rows), of those only the present ones on the
+# gather path, (+ flags) in, and 2k*sl/2 out
+rows_dma = k if all(pres[b, :k].all() for b in range(B)) else n
+rows = float(pres[:, :rows_dma].sum()) / B
 res = {
     "config": args.config, "batch": B, "payload_bytes": plen, "n": n, "k": k,
     "pcie_GB_s": {"h2d": round(bw_h2d, 1), "d2h": round(bw_d2h, 1)},
     "encode": {"GiB_s": round(B * plen / t_enc / 2**30, 2), "ms": round(t_enc * 1e3, 2),
                "pcie_bound_GiB_s": round(B * plen / max(B * plen / (bw_h2d * 1e9), B * n * sl / (bw_d2h * 1e9)) / 2**30, 2)},
     "reconstruct": {"GiB_s": round(B * plen / t_rec / 2**30, 2), "ms": round(t_rec * 1e3, 2), "rows_copied": rows,
-                    "pcie_bound_GiB_s": round(B * plen / max(B * rows * sl / (bw_h2d * 1e9), B * olen / (bw_d2h * 1e9)) / 2**30, 2)},
+                    "pcie_bound_GiB_s": round(B * plen / max(B * rows * sl / (bw_h2d * 1e9), B * olen / (bw_d2h * 1e9)) / 2**30, 2),
+                    # the two directions one after the other: kernel reads of host memory and a
+                    # concurrent D2H share the link badly (tools/microbench/h2d_gather.hip)
+                    "pcie_serial_bound_GiB_s": round(B * plen / (B * rows * sl / (bw_h2d * 1e9) + B * olen / (bw_d2h * 1e9)) / 2**30, 2)},
+    "reconstruct_dma": {"GiB_s": round(B * plen / t_dma / 2**30, 2), "ms": round(t_dma * 1e3, 2), "rows_copied": rows_dma,
+                        "pcie_bound_GiB_s": round(B * plen / max(B * rows_dma * sl / (bw_h2d * 1e9), B * olen / (bw_d2h * 1e9)) / 2**30, 2)},
     "roundtrip_ok": bool(ok),
 }
 print(json.dumps(res))
