@@ -426,6 +426,52 @@ constexpr uint32_t kBigDecode = 2;
 constexpr size_t kBigRecHeader = 16;
 __host__ __device__ constexpr size_t big_rec_stride(uint32_t n) { return kBigRecHeader + 3u * n; }
 
+// The decode keeps E and PR in LDS next to the tile up to n = 8192 (which
+// fills the 160 KiB exactly); beyond, it reads them from the record through
+// the scalar cache (wave-uniform rows).
+__host__ __device__ constexpr bool big_rows_global(uint32_t n) { return n > 8192u; }
+
+// Row multiplier and present flag of row r: from LDS, or (G) from the record
+// in global memory with dword scalar loads.
+template <bool G>
+struct RowView {
+  const uint16_t* E;
+  const uint8_t* PR;
+  __device__ __forceinline__ uint32_t e(uint32_t r) const {
+    if constexpr (G) {
+      const uint32_t w = ((cpool_t)(E))[r >> 1];
+      return (r & 1u) ? w >> 16 : w & 0xffffu;
+    } else {
+      return uniform(E[r]);
+    }
+  }
+  __device__ __forceinline__ bool pr(uint32_t r) const {
+    if constexpr (G) {
+      return ((((cpool_t)(PR))[r >> 2] >> (8u * (r & 3u))) & 0xffu) != 0;
+    } else {
+      return uniform(PR[r]) != 0;
+    }
+  }
+};
+
+// Shard-row pieces of rows row0..row0+NR-1 for this lane (fast_common.hpp
+// load_rows over a RowView).  Absent rows read the zero page.
+template <int NR, bool G>
+__device__ __forceinline__ void load_rows_v(uint2 (&raw)[NR], const uint8_t* sh, size_t shard_len, const RowView<G>& rv,
+                                            uint32_t row0, const uint8_t* zeros, uint32_t lane, uint32_t ncols,
+                                            bool full) {
+  const uint8_t* src[NR];
+#pragma unroll
+  for (int p = 0; p < NR; ++p) src[p] = rv.pr(row0 + p) ? sh + static_cast<size_t>(row0 + p) * shard_len : zeros;
+  if (full) {
+#pragma unroll
+    for (int p = 0; p < NR; ++p) raw[p] = *reinterpret_cast<const uint2*>(src[p] + 8u * lane);
+  } else {
+#pragma unroll
+    for (int p = 0; p < NR; ++p) raw[p] = load4(src[p], lane, ncols, false);
+  }
+}
+
 // Output column c, symbols 256 s .. 256 s + 255 (bytes [2 KB c + 512 s, +512))
 // from the tile's natural blocks.
 template <int KB>
@@ -491,6 +537,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   constexpr int SUBS = KB / kS;
   constexpr int N = NQ * KB;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr bool RG = big_rows_global(N);
   uint8_t* tile = smem;
   uint32_t* VP = reinterpret_cast<uint32_t*>(smem + G::kTileBytes);
   uint16_t* E = reinterpret_cast<uint16_t*>(smem + G::kTileBytes + 4 * G::kVPWords);
@@ -519,11 +566,13 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
     big_copy_systematic<KB>(a, sh, tile, pb, col0, ncols, full);
     return;
   }
-  {  // E (2N bytes) and PR (N bytes) are contiguous in the record and in LDS
+  if constexpr (!RG) {  // E (2N bytes) and PR (N bytes) are contiguous in the record and in LDS
     const uint4* src = reinterpret_cast<const uint4*>(rec + kBigRecHeader);
     uint4* dst = reinterpret_cast<uint4*>(E);
     for (uint32_t v = tid; v < 3u * N / 16u; v += kTB) dst[v] = src[v];
   }
+  const RowView<RG> rv{RG ? reinterpret_cast<const uint16_t*>(rec + kBigRecHeader) : E,
+                       RG ? rec + kBigRecHeader + 2u * N : PR};
 
   // ---- phase 1: y_qs for every segment q and sub-segment s
   __syncthreads();  // E, PR ready
@@ -536,7 +585,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
     uint2 rows[2][8];
 #pragma unroll
     for (int half = 0; half < 2; ++half)
-      load_rows<8>(rows[half], sh, a.shard_len, PR, index + 16 * gg + 8 * half, T.zeros, lane, ncols, full);
+      load_rows_v<8>(rows[half], sh, a.shard_len, rv, index + 16 * gg + 8 * half, T.zeros, lane, ncols, full);
     __syncthreads();  // tile / tables free
     stage_vpools<kS, kTB>(T, index, VP, true);
     __syncthreads();
@@ -549,15 +598,15 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
         // premultiply (Cantor in, tower out: in_pools) of the present rows
         pipelined_rec<8>(
             [&](auto pc) __attribute__((always_inline)) {
-              return (cpool_t)(T.in_pools) + uniform(E[r0 + decltype(pc)::value]) * kPoolWords;
+              return (cpool_t)(T.in_pools) + rv.e(r0 + decltype(pc)::value) * kPoolWords;
             },
-            [&](auto pc) __attribute__((always_inline)) { return uniform(PR[r0 + decltype(pc)::value]) != 0; },
+            [&](auto pc) __attribute__((always_inline)) { return rv.pr(r0 + decltype(pc)::value); },
             [&](auto pc, const Mult& pool) __attribute__((always_inline)) {
               constexpr int p = decltype(pc)::value;
               const int x = 8 * half + p;
               XL[x] = 0;
               XH[x] = 0;
-              if (uniform(PR[index + 16 * gg + x])) {
+              if (rv.pr(index + 16 * gg + x)) {
                 uint32_t l, h;
                 blk_to_quad(raw[p], l, h);
                 qmul_set(XL[x], XH[x], l, h, pool);
@@ -755,17 +804,17 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       for (int half = 0; half < 2; ++half) {
         uint2 raw[8];
         const uint32_t r0 = index + 16 * gg + 8 * half;
-        load_rows<8>(raw, sh, a.shard_len, PR, r0, T.zeros, lane, ncols, full);
+        load_rows_v<8>(raw, sh, a.shard_len, rv, r0, T.zeros, lane, ncols, full);
         // received symbol (present) or postmultiplied (erased; tower in, Cantor out: out_pools)
         pipelined_rec<8>(
             [&](auto pc) __attribute__((always_inline)) {
-              return (cpool_t)(T.out_pools) + uniform(E[r0 + decltype(pc)::value]) * kPoolWords;
+              return (cpool_t)(T.out_pools) + rv.e(r0 + decltype(pc)::value) * kPoolWords;
             },
-            [&](auto pc) __attribute__((always_inline)) { return uniform(PR[r0 + decltype(pc)::value]) == 0; },
+            [&](auto pc) __attribute__((always_inline)) { return !rv.pr(r0 + decltype(pc)::value); },
             [&](auto pc, const Mult& pool) __attribute__((always_inline)) {
               constexpr int p = decltype(pc)::value;
               const int x = 8 * half + p;
-              if (uniform(PR[index + 16 * gg + x])) {
+              if (rv.pr(index + 16 * gg + x)) {
                 blk_to_quad(raw[p], XL[x], XH[x]);
               } else {
                 const uint32_t l = XL[x], h = XH[x];
@@ -786,14 +835,19 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
 // inc_reconstruct.rs:90-113, folded to the n rows; or the caller's
 // locators) as row multipliers E and present flags PR.  Once per payload
 // instead of once per column tile.
+// n = 16384: the Walsh scratch W alone is 64 KiB, so E and PR go straight to
+// the record (big_rows_global) instead of through LDS.
 template <int K, int N>
 __global__ __launch_bounds__(256) void k_big_records(DevTables T, ReconstructArgs a, uint8_t* out) {
+  constexpr bool RG = big_rows_global(N);
   __shared__ uint32_t W[N];
-  __shared__ __attribute__((aligned(16))) uint16_t E[N];
-  __shared__ __attribute__((aligned(16))) uint8_t PR[N];
+  __shared__ __attribute__((aligned(16))) uint16_t El[RG ? 8 : N];
+  __shared__ __attribute__((aligned(16))) uint8_t PRl[RG ? 16 : N];
   const uint32_t pb = blockIdx.x, tid = threadIdx.x;
   const uint8_t* pres = a.present + static_cast<size_t>(pb) * N;
   uint8_t* rec = out + static_cast<size_t>(pb) * big_rec_stride(N);
+  uint16_t* E = RG ? reinterpret_cast<uint16_t*>(rec + kBigRecHeader) : El;
+  uint8_t* PR = RG ? rec + kBigRecHeader + 2u * N : PRl;
   int have1 = 0, have = 0;  // present rows in [0, K) and [0, N)
   for (int r = 0; r < N; r += 256) {
     const bool p = pres[r + static_cast<int>(tid)] != 0;
@@ -817,16 +871,18 @@ __global__ __launch_bounds__(256) void k_big_records(DevTables T, ReconstructArg
   } else {
     fused_locator<N, 256>(T, pres, W, E, PR);
   }
-  __syncthreads();
-  uint4* dst = reinterpret_cast<uint4*>(rec + kBigRecHeader);
-  for (uint32_t v = tid; v < 2u * N / 16u; v += 256) dst[v] = reinterpret_cast<const uint4*>(E)[v];
-  dst += 2u * N / 16u;
-  for (uint32_t v = tid; v < static_cast<uint32_t>(N) / 16u; v += 256) dst[v] = reinterpret_cast<const uint4*>(PR)[v];
+  if constexpr (!RG) {
+    __syncthreads();
+    uint4* dst = reinterpret_cast<uint4*>(rec + kBigRecHeader);
+    for (uint32_t v = tid; v < 2u * N / 16u; v += 256) dst[v] = reinterpret_cast<const uint4*>(E)[v];
+    dst += 2u * N / 16u;
+    for (uint32_t v = tid; v < static_cast<uint32_t>(N) / 16u; v += 256) dst[v] = reinterpret_cast<const uint4*>(PR)[v];
+  }
 }
 
 constexpr size_t enc_big_lds() { return static_cast<size_t>(Geo<kS>::kTileBytes) + 4u * Geo<kS>::kVPWords; }
-constexpr size_t rec_big_lds(uint32_t n) {  // tile, tables, E (2 n bytes), PR (n bytes)
-  return static_cast<size_t>(Geo<kS>::kTileBytes) + 4u * Geo<kS>::kVPWords + 3u * n;
+constexpr size_t rec_big_lds(uint32_t n) {  // tile, tables, E (2 n bytes), PR (n bytes) up to n = 8192
+  return static_cast<size_t>(Geo<kS>::kTileBytes) + 4u * Geo<kS>::kVPWords + (big_rows_global(n) ? 0u : 3u * n);
 }
 // Dynamic LDS of every instance fits the CU's 160 KiB (n = 8192 exactly fills it).
 static_assert(enc_big_lds() <= 160u * 1024u, "encode LDS");
@@ -844,9 +900,10 @@ bool with_rec_big(uint32_t n, uint32_t k, F&& f) {
     if (n == 2048) return f(&k_reconstruct_big<1024, 2>, &k_big_records<1024, 2048>), true;
     if (n == 4096) return f(&k_reconstruct_big<1024, 4>, &k_big_records<1024, 4096>), true;
     if (n == 8192) return f(&k_reconstruct_big<1024, 8>, &k_big_records<1024, 8192>), true;
-  } else if (k == 2048) {  // n = 16384 (the records' locator would need 112 KiB of LDS): generic
+  } else if (k == 2048) {
     if (n == 4096) return f(&k_reconstruct_big<2048, 2>, &k_big_records<2048, 4096>), true;
     if (n == 8192) return f(&k_reconstruct_big<2048, 4>, &k_big_records<2048, 8192>), true;
+    if (n == 16384) return f(&k_reconstruct_big<2048, 8>, &k_big_records<2048, 16384>), true;
   }
   return false;
 }

@@ -30,7 +30,7 @@ SHAPES = [(256, 86, 2 * 300), (1024, 342, 2 * 300), (4096, 1366, 2 * 260), (300,
           (700, 234, 2 * 300), (1200, 400, 2 * 290), (600, 256, 2 * 280), (2048, 1024, 2 * 270),
           (1024, 512, 2 * 270), (2000, 667, 2 * 260), (2500, 834, 2 * 270), (5000, 1667, 2 * 260),
           (100, 34, 2 * 300), (150, 50, 2 * 270), (60, 20, 2 * 260), (40, 14, 2 * 280), (16, 8, 2 * 300),
-          (64, 32, 2 * 257), (7000, 2334, 2 * 260), (4096, 2048, 2 * 257)]
+          (64, 32, 2 * 257), (7000, 2334, 2 * 260), (4096, 2048, 2 * 257), (10000, 3334, 2 * 260)]
 
 
 def _dev(a):

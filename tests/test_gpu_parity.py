@@ -336,10 +336,12 @@ def test_fast_encode_shapes(gpu, oracle, nw, kw, plen):
                                               (5000, 1667, 2048 * 33, -1), (2000, 667, 1024 * 256 + 5, 0),
                                               (4096, 1366, 2048 * 256, 0), (7000, 2334, 4096 * 256 + 3, 4666),
                                               (7000, 2334, 4096 * 100, -1), (4096, 2048, 4096 * 40, 2048),
-                                              (8192, 2731, 4096 * 257, 5461), (7000, 2334, 4096 * 30, 0)])
+                                              (8192, 2731, 4096 * 257, 5461), (7000, 2334, 4096 * 30, 0),
+                                              (9000, 3000, 4096 * 3 + 5, 6000), (12288, 4095, 4096 * 20, 8000),
+                                              (10000, 3334, 4096 * 2, -1), (9000, 3000, 4096 * 2 + 1, 0)])
 def test_fast_reconstruct_shapes(gpu, oracle, nw, kw, plen, erase):
-    """Specialised reconstruct kernels (k in {64,128,256} fast, {512,1024} big
-    with n in {2k,4k,8k}, 2048 big with n in {2k, 4k}): full
+    """Specialised reconstruct kernels (k in {64,128,256} fast, {512,1024,2048}
+    big with n in {2k,4k,8k}; 8,193-12,288 validators: n = 16384, k = 2048): full
     and partial column tiles, random and worst-case erasure sets (erase = -1:
     every systematic shard lost), bit-exact against the oracle."""
     p = npa.CodeParams.derive_parameters(nw, kw)
