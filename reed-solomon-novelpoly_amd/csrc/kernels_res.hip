@@ -242,6 +242,7 @@ __host__ __device__ constexpr int res_gen(uint32_t I) {
   return b;
 }
 static_assert(res_gen(0) == 2 && res_gen(1024) == 3 && res_gen(2048) == 4 && res_gen(3072) == 4, "res_gen");
+static_assert(res_gen(4096) == 5 && res_gen(7168) == 5, "res_gen, n = 8192: level 4 (HA) full");
 
 // CQ levels 0-3 of a size-1024 transform at index I.  GEN: levels b < GEN
 // have full multipliers (gen_of(I), fast_common.hpp kSubLevel).  Group t of
@@ -373,8 +374,9 @@ __host__ __device__ constexpr int rh_groups() {
 // Levels PB0 + r, R0 <= r < R1, in a register layout whose register index j
 // holds position bits PB0..PB0+3 and whose wave holds the bits above as `hi`:
 // group T = (j >> (r + 1)) + (hi << (3 - r)).  Every multiplier is
-// wave-uniform and, for I < 4096, in GF(2^8) (I >> PB0 < 256).
-template <int PB0, int R0, int R1, bool INVERSE>
+// wave-uniform; levels below GEN (res_gen(I)) hold full ones (level 4 for
+// I >= 4096, the shifts and segments of n = 8192), the others lie in GF(2^8).
+template <int PB0, int R0, int R1, bool INVERSE, int GEN = 0>
 __device__ __forceinline__ void rh_levels(const DevTables& T, uint32_t I, uint32_t hi, uint32_t (&L)[16],
                                           uint32_t (&H)[16]) {
   if constexpr (kExp & 1) return;
@@ -386,15 +388,16 @@ __device__ __forceinline__ void rh_levels(const DevTables& T, uint32_t I, uint32
   auto group = [&](auto fc, const Mult& p) __attribute__((always_inline)) {
     constexpr GroupRef g = rh_group<R0, R1, INVERSE>(decltype(fc)::value);
     constexpr int d = 1 << g.b;
+    constexpr bool SUB = PB0 + g.b >= GEN;
 #pragma unroll
     for (int v = 0; v < d; ++v) {
       const int x = g.t * 2 * d + v, y = x + d;
       if constexpr (INVERSE) {
         L[y] ^= L[x];
         H[y] ^= H[x];
-        qmul_sub(L[x], H[x], L[y], H[y], p);
+        qmul_mode<SUB>(L[x], H[x], L[y], H[y], p);
       } else {
-        qmul_sub(L[x], H[x], L[y], H[y], p);
+        qmul_mode<SUB>(L[x], H[x], L[y], H[y], p);
         L[y] ^= L[x];
         H[y] ^= H[x];
       }
@@ -405,11 +408,11 @@ __device__ __forceinline__ void rh_levels(const DevTables& T, uint32_t I, uint32
 
 // HA: levels 4-7 (hi = position bits 8-9 = w >> 2).  HD: levels 8-9 (j bits
 // 2-3 = position bits 8-9; hi = 0).
-template <bool INVERSE>
+template <bool INVERSE, int GEN = 0>
 __device__ __forceinline__ void ha_levels(const DevTables& T, uint32_t I, const Res& r, uint32_t (&L)[16],
                                           uint32_t (&H)[16]) {
   if constexpr (kExp & 512) return;
-  rh_levels<4, 0, 4, INVERSE>(T, I, r.w >> 2, L, H);
+  rh_levels<4, 0, 4, INVERSE, GEN>(T, I, r.w >> 2, L, H);
 }
 template <bool INVERSE>
 __device__ __forceinline__ void hd_levels(const DevTables& T, uint32_t I, uint32_t (&L)[16], uint32_t (&H)[16]) {
@@ -553,7 +556,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(4))) void k
     rh_write<kHD>(tile, fresh_v(r.hdb), L, H);
     __syncthreads();
     rh_read<kHA>(tile, fresh_v(r.hab), L, H);
-    ha_levels<false>(T, I, r, L, H);
+    ha_levels<false, GEN>(T, I, r, L, H);
     __syncthreads();
     rh_write<kHA>(tile, fresh_v(r.hab), L, H);
     __syncthreads();
@@ -564,13 +567,16 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(4))) void k
   };
   if (nshift > 1 && kRK < a.wanted_n) shift(Int<res_gen(1024)>{}, 1);
 #pragma unroll 1
-  for (uint32_t sh = 2; sh < nshift && sh * kRK < a.wanted_n; ++sh) shift(Int<res_gen(2048)>{}, sh);
+  for (uint32_t sh = 2; sh < 4 && sh < nshift && sh * kRK < a.wanted_n; ++sh) shift(Int<res_gen(2048)>{}, sh);
+#pragma unroll 1
+  for (uint32_t sh = 4; sh < nshift && sh * kRK < a.wanted_n; ++sh) shift(Int<res_gen(4096)>{}, sh);  // n = 8192
 }
 
 // ----------------------------------------------------------- reconstruct ----
-// n = NQ * 1024, NQ in {2, 4}.  As in k_reconstruct_fast (kernels_fast.hip,
+// n = NQ * 1024, NQ in {2, 4, 8}.  As in k_reconstruct_fast (kernels_fast.hip,
 // DESIGN.md §4.3) the first k outputs are FFT(1024, 0)(d) with
 //   NQ = 2: d = D(x0) ^ x0 ^ x1,   NQ = 4: d = D(x0) ^ x1 ^ x2 ^ beta (x2 ^ x3),
+//   NQ = 8: d = D(x0) ^ sum_q kappa_q x_q (rec8_kappa_res),
 // x_q = IFFT(1024, 1024 q)(premultiplied segment q), beta = Cantor(2) and D
 // the size-1024 formal derivative -- here every x_q is computed whole in the
 // workgroup (CQ -> HA -> HD) and d accumulates in the HD layout, where all ten
@@ -676,14 +682,21 @@ __device__ __forceinline__ void res_copy_out(uint8_t* out_tile, const uint32_t (
 }
 
 template <int NQ>
-__host__ __device__ constexpr int res_seg(int step) {  // segments 2, 3, 1, 0 (NQ = 4); 1, 0 (NQ = 2)
-  return NQ == 4 ? (step == 0 ? 2 : step == 1 ? 3 : 3 - step) : 1 - step;
+__host__ __device__ constexpr int res_seg(int step) {  // segments 2, 3, 1, 0 (NQ = 4); 1, 0 (NQ = 2); 7..0 (NQ = 8)
+  return NQ == 8 ? 7 - step : NQ == 4 ? (step == 0 ? 2 : step == 1 ? 3 : 3 - step) : 1 - step;
 }
 
 // Step STEP of the segment sweep: x_q = IFFT(1024, 1024 q)(premultiplied
 // segment q), folded into d (A, HD layout).  Steps are compile-time: each has
 // one CQ instance (its GEN) and its own fold, with no runtime branch between
 // instances (a branch over instances inside a loop made the allocator spill).
+// NQ = 8: the fold coefficients of kernels_fast.hip rec8_kappa (Cantor
+// coordinates, all in GF(16); tests/test_oracle.py::test_rec8_kappa).
+__host__ __device__ constexpr uint32_t rec8_kappa_res(int q) {
+  constexpr uint32_t k[8] = {1, 1, 3, 2, 12, 15, 10, 8};
+  return k[q];
+}
+
 template <int NQ, int STEP>
 __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructArgs& a, uint8_t* tile,
                                          const uint8_t* pools, const uint8_t* pres, const uint8_t* sh,
@@ -727,18 +740,29 @@ __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructAr
   rcq_write(tile, fresh_v(rr.cqb), XL, XH);
   __syncthreads();
   rh_read<kHA>(tile, fresh_v(rr.hab), XL, XH);
-  ha_levels<true>(T, I, rr, XL, XH);
+  ha_levels<true, res_gen(I)>(T, I, rr, XL, XH);
   __syncthreads();
   rh_write<kHA>(tile, fresh_v(rr.hab), XL, XH);
   __syncthreads();
   rh_read<kHD>(tile, fresh_v(rr.hdb), XL, XH);
   hd_levels<true>(T, I, XL, XH);
   // fold x_q into d (kernels_fast.hip rec_segments)
-  if constexpr (STEP == 0) {
+  if constexpr (NQ == 8 && q != 0 && rec8_kappa_res(q) != 1u) {  // d ^= kappa_q x_q, kappa_q in GF(16)
+    uint32_t kp[20];
+    pool_of<true>(T, rec8_kappa_res(q), kp);
+    const Mult m = make_mult(kp);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if constexpr (STEP == 0)
+        qmul_sub_set(AL[j], AH[j], XL[j], XH[j], m);
+      else
+        qmul_sub(AL[j], AH[j], XL[j], XH[j], m);
+    }
+  } else if constexpr (STEP == 0) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) AL[j] = XL[j], AH[j] = XH[j];
   } else if constexpr (q == 0) {
-    if constexpr (NQ == 2) {
+    if constexpr (NQ == 2 || NQ == 8) {
 #pragma unroll
       for (int j = 0; j < 16; ++j) AL[j] ^= XL[j], AH[j] ^= XH[j];
     }
@@ -836,10 +860,10 @@ __device__ __forceinline__ void res_copy_tile(const ReconstructArgs& a, const ui
   res_copy_out(out_tile, L, H, r, ncols, out16);
 }
 
-// One workgroup per 64-column tile.  SERVE = 2: payloads whose record says
-// copy (nq = 1) or decode from 2 segments (n = 2048, or a trusted prefix of
-// n = 4096); SERVE = 4: the 4-segment decodes.  The host launches both
-// instances over the same grid for n = 4096 (kernels_fast.hip's scheme).
+// One workgroup per 64-column tile.  SERVE = 1: payloads whose record says
+// copy (nq = 1); 2: decodes from 2 segments (n = 2048, or a trusted prefix of
+// n = 4096 / 8192); 4 / 8: the 4- / 8-segment decodes.  The host launches
+// the instances over the same grid (kernels_fast.hip's scheme).
 template <int SERVE>
 __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(4))) void k_reconstruct_res(
     DevTables T, ReconstructArgs a, uint32_t nsyms, uint32_t tiles) {
@@ -875,8 +899,8 @@ bool res_enabled() {
   return on;
 }
 
-bool res_encode_supported(uint32_t n, uint32_t k) { return k == 1024 && (n == 2048 || n == 4096); }
-bool res_reconstruct_supported(uint32_t n, uint32_t k) { return k == 1024 && (n == 2048 || n == 4096); }
+bool res_encode_supported(uint32_t n, uint32_t k) { return k == 1024 && (n == 2048 || n == 4096 || n == 8192); }
+bool res_reconstruct_supported(uint32_t n, uint32_t k) { return k == 1024 && (n == 2048 || n == 4096 || n == 8192); }
 
 hipError_t launch_reconstruct_res(const DevTables& T, const ReconstructArgs& a, hipStream_t s) {
   const size_t nsyms = a.shard_len / 2;
@@ -890,6 +914,8 @@ hipError_t launch_reconstruct_res(const DevTables& T, const ReconstructArgs& a, 
     k_reconstruct_res<2><<<static_cast<uint32_t>(blocks), kRT, kRTileBytes, s>>>(T, a, static_cast<uint32_t>(nsyms), tiles);
   if (a.n == 4096)
     k_reconstruct_res<4><<<static_cast<uint32_t>(blocks), kRT, kRTileBytes, s>>>(T, a, static_cast<uint32_t>(nsyms), tiles);
+  if (a.n == 8192)
+    k_reconstruct_res<8><<<static_cast<uint32_t>(blocks), kRT, kRTileBytes, s>>>(T, a, static_cast<uint32_t>(nsyms), tiles);
   return hipGetLastError();
 }
 
@@ -907,7 +933,8 @@ hipError_t launch_encode_res(const DevTables& T, const EncodeArgs& a, hipStream_
 hipError_t configure_res_kernels() {
   hipError_t e = hipSuccess;
   for (const void* f : {reinterpret_cast<const void*>(&k_encode_res), reinterpret_cast<const void*>(&k_reconstruct_res<2>),
-                        reinterpret_cast<const void*>(&k_reconstruct_res<4>)}) {
+                        reinterpret_cast<const void*>(&k_reconstruct_res<4>),
+                        reinterpret_cast<const void*>(&k_reconstruct_res<8>)}) {
     const hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kRTileBytes));
     if (r != hipSuccess && e == hipSuccess) e = r;
   }
