@@ -20,8 +20,9 @@ os.makedirs(dst, exist_ok=True)
 # The bench's "reconstruct" span is the prefix-locator launch plus both fast
 # reconstruct instances (prefixes of <= 2 and of 4 segments); their per-launch
 # traffic and durations add up.  Each instance is also reported on its own.
-KINDS = {"encode": ("k_encode_fast", "k_encode_multi", "k_encode_big"),
-         "reconstruct": ("k_reconstruct_fast", "k_prefix_locator", "k_reconstruct_big", "k_big_records", "k_payload_status"),
+KINDS = {"encode": ("k_encode_fast", "k_encode_multi", "k_encode_big", "k_encode_res"),
+         "reconstruct": ("k_reconstruct_fast", "k_prefix_locator", "k_reconstruct_big", "k_big_records", "k_payload_status",
+                         "k_reconstruct_res"),
          "locator": ("k_error_locator",), "calib_read8": ("read8",), "calib_copy8": ("copy8",)}
 # bench steps per profiled command (tools/profile_round.sh): PMC passes run
 # 1 warmup + 3 timed steps, the kernel-trace pass 3 + 10; per-step values are
