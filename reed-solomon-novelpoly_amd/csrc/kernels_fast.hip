@@ -1328,6 +1328,7 @@ hipError_t launch_prefix_locator(const DevTables& T, const ReconstructArgs& a, u
     case 8: return by_nq<8>(a, [&](auto K, auto NQ) { return launch_prefix_k<K.value, NQ.value>(T, a, out, s); });
     case 16: return by_nq<16>(a, [&](auto K, auto NQ) { return launch_prefix_k<K.value, NQ.value>(T, a, out, s); });
     case 32: return by_nq<32>(a, [&](auto K, auto NQ) { return launch_prefix_k<K.value, NQ.value>(T, a, out, s); });
+    case 512: return by_nq<512>(a, [&](auto K, auto NQ) { return launch_prefix_k<K.value, NQ.value>(T, a, out, s); });  // kernels_res.hip
     case 1024: return by_nq<1024>(a, [&](auto K, auto NQ) { return launch_prefix_k<K.value, NQ.value>(T, a, out, s); });  // kernels_res.hip
     default: return hipErrorNotSupported;
   }

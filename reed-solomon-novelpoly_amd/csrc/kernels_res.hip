@@ -1,12 +1,14 @@
 // k = 1024 (BASELINE config 4: n = 4096; 2,731-5,461 validators at n = 4096 /
-// 1,366-2,730 with n = 2048) with the whole size-1024 transform of a tile
+// 8,192) and k = 512 (1,534-3,070 validators: n = 2048 / 4096, the reference's
+// own 2,000-validator bench shape) with the whole size-K transform of a tile
 // resident in one workgroup: no scratch round trips.
 //
-// A tile is 64 codeword columns (encode: 64 payload chunks of 2 KiB; decode:
-// 64 symbol columns of the shards) x 1024 positions = 128 KiB, the LDS tile.
-// The 1024 threads (16 waves) hold the tile in registers, 64 symbols each, in
-// three layouts that meet in the LDS tile (position p = bits p0..p9, block
-// m = p >> 2, column c < 64):
+// A tile is 64 codeword columns (encode: 64 payload chunks of 2K bytes;
+// decode: 64 symbol columns of the shards) x K positions = 128 KiB (K = 1024)
+// or 64 KiB (K = 512, two workgroups per CU), the LDS tile.  The K threads
+// (K / 64 waves) hold the tile in registers, 64 symbols each, in three layouts
+// that meet in the LDS tile (written for K = 1024, position p = bits p0..p9,
+// block m = p >> 2, column c < 64; K = 512 where it differs):
 //
 //  * CQ (levels 0-3; the shard rows): wave w, lane 16u + cq holds positions
 //    P_i = 64 w + 16 u + i (i = 0..15) of columns 4 cq .. 4 cq + 3, byte-planar
@@ -16,7 +18,8 @@
 //    m = (w & 3) + 4 j + 64 (w >> 2), j = 0..15 (position bits 4-7 in j).
 //  * HD (levels 8-9, the decode's formal derivative): wave w, lane l holds
 //    column 4 w + (l >> 4), quads m = (l & 15) + 16 j (position bits 2-5 in the
-//    16 lanes of a DPP row, bits 6-9 in j).
+//    16 lanes of a DPP row, bits 6-9 in j).  K = 512 (level 8): column
+//    8 w + (l >> 3), quads (l & 7) + 8 j (bits 2-4 in 8 lanes, 5-8 in j).
 //
 // HA and HD see whole butterfly groups per register, so their multipliers are
 // wave-uniform (s_load tables, as in the fast kernels).  In CQ the lane's
@@ -47,13 +50,21 @@
 namespace np {
 namespace {
 
-constexpr int kRK = 1024;                        // transform size (k)
-constexpr int kRC = 64;                          // columns per tile
-constexpr int kRT = 1024;                        // threads per workgroup
-constexpr uint32_t kRTileBytes = kRC * 2 * kRK;  // 128 KiB
+constexpr int kRC = 64;  // columns per tile
+// Geometry of the size-K kernels (K = 512, 1024): K threads, K / 64 waves.
+template <int K>
+struct RGeo {
+  static_assert(K == 512 || K == 1024, "resident kernels: k = 512 or 1024");
+  static constexpr int kThreads = K;
+  static constexpr uint32_t kTileBytes = kRC * 2 * K;  // 128 / 64 KiB
+  static constexpr uint32_t kColBytes = 2 * K;
+  static constexpr uint32_t kLPC = K / 64;  // HD: lanes per column
+  static constexpr uint32_t kHD = 8 * kLPC;  // HD: item j at hdb ^ kHD j
+  static constexpr int kLogK = K == 1024 ? 10 : 9;
+};
 
 // ------------------------------------------------------------- LDS tile ----
-// Swizzle of the block index by the column, linear in the bits of c:
+// Swizzle of the block index by the column, linear in the bits of c.  K = 1024:
 // c0 -> 24, c1 -> 4, c2 -> 1, c3 -> 2, c4 -> 20, c5 -> 8.  Conflict-free for
 // ds_read_b64 (32-lane groups, bank (a / 4) mod 64) and ds_write_b64 (16-lane
 // groups, bank (a / 4) mod 32) in the three sweeps:
@@ -62,52 +73,68 @@ constexpr uint32_t kRTileBytes = kRC * 2 * kRK;  // 128 KiB
 //  HD: 16 consecutive blocks of columns c, c + 1 (v0 has bit 4);
 //  CQ: columns 4 cq + e over cq < 16 with block bit 2 (u) (rank {v2..v5, 4} =
 //      5; writes: rank {v2..v5} mod 16 = 4).
+// K = 512 (HD: 8 blocks of columns c .. c + 3): c0 -> 28, c1 -> 14, c2 -> 1,
+// c3 -> 25, c4 -> 20, c5 -> 27, found and checked over every sweep of both
+// sizes (and the payload tile's writes) by tools/res_swizzle.py.
+template <int K>
 __host__ __device__ constexpr uint32_t rsw(uint32_t c) {
-  return ((c & 1u) ? 24u : 0u) ^ ((c & 2u) ? 4u : 0u) ^ ((c & 4u) ? 1u : 0u) ^ ((c & 8u) ? 2u : 0u) ^
-         ((c & 16u) ? 20u : 0u) ^ ((c & 32u) ? 8u : 0u);
+  if constexpr (K == 1024)
+    return ((c & 1u) ? 24u : 0u) ^ ((c & 2u) ? 4u : 0u) ^ ((c & 4u) ? 1u : 0u) ^ ((c & 8u) ? 2u : 0u) ^
+           ((c & 16u) ? 20u : 0u) ^ ((c & 32u) ? 8u : 0u);
+  else
+    return ((c & 1u) ? 28u : 0u) ^ ((c & 2u) ? 14u : 0u) ^ ((c & 4u) ? 1u : 0u) ^ ((c & 8u) ? 25u : 0u) ^
+           ((c & 16u) ? 20u : 0u) ^ ((c & 32u) ? 27u : 0u);
 }
-__host__ __device__ constexpr uint32_t pq_addr(uint32_t c, uint32_t m) { return 2048u * c + 8u * (m ^ rsw(c)); }
+template <int K>
+__host__ __device__ constexpr uint32_t pq_addr(uint32_t c, uint32_t m) {
+  return RGeo<K>::kColBytes * c + 8u * (m ^ rsw<K>(c));
+}
 
 // Per-thread coordinates of the three layouts.
 struct Res {
   uint32_t tid, w, l;
   // CQ
-  uint32_t cq, u, cqb;  // cqb: pq_addr(4 cq, 16 w + 4 u); item (e, q) at (cqb | 2048 e) ^ 8 (q ^ rsw(e))
+  uint32_t cq, u, cqb;  // cqb: pq_addr(4 cq, 16 w + 4 u); item (e, q) at (cqb | 2K e) ^ 8 (q ^ rsw(e))
   // HA: item j at hab ^ 32 j
   uint32_t hab;
-  // HD: item j at hdb ^ 128 j
+  // HD: item j at hdb ^ kHD j
   uint32_t hdb;
 };
 
+template <int K>
 __device__ __forceinline__ Res res_coords() {
+  constexpr uint32_t lpc = RGeo<K>::kLPC;
   Res r;
   r.tid = fresh_v(threadIdx.x);
   r.w = uniform(r.tid >> 6);
   r.l = r.tid & 63u;
   r.cq = r.l & 15u;
   r.u = r.l >> 4;
-  r.cqb = pq_addr(4u * r.cq, 16u * r.w + 4u * r.u);
-  r.hab = pq_addr(r.l, (r.w & 3u) + 64u * (r.w >> 2));
-  r.hdb = pq_addr(4u * r.w + (r.l >> 4), r.l & 15u);
+  r.cqb = pq_addr<K>(4u * r.cq, 16u * r.w + 4u * r.u);
+  r.hab = pq_addr<K>(r.l, (r.w & 3u) + 64u * (r.w >> 2));
+  r.hdb = pq_addr<K>((64u / lpc) * r.w + r.l / lpc, r.l % lpc);
   return r;
 }
 
+template <int K>
 __device__ __forceinline__ uint32_t cq_item(uint32_t cqb, uint32_t e, uint32_t q) {
-  return (cqb | (2048u * e)) ^ (8u * (q ^ rsw(e)));
+  return (cqb | (RGeo<K>::kColBytes * e)) ^ (8u * (q ^ rsw<K>(e)));
 }
 
 // CQ from natural blocks (the payload tile).
+template <int K>
 __device__ __forceinline__ void rcq_read_nat(const uint8_t* tile, uint32_t cqb, uint32_t (&L)[16], uint32_t (&H)[16]) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     uint2 d[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) d[e] = *reinterpret_cast<const uint2*>(tile + cq_item(cqb, e, q));
+    for (int e = 0; e < 4; ++e) d[e] = *reinterpret_cast<const uint2*>(tile + cq_item<K>(cqb, e, q));
     blks_to_cq(d, &L[4 * q], &H[4 * q]);
   }
 }
 
 // CQ <-> planar items (4 x 4 byte transposes of each plane).
+template <int K>
 __device__ __forceinline__ void rcq_write(uint8_t* tile, uint32_t cqb, const uint32_t (&L)[16], const uint32_t (&H)[16]) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -115,15 +142,16 @@ __device__ __forceinline__ void rcq_write(uint8_t* tile, uint32_t cqb, const uin
     tr4x4(L[4 * q], L[4 * q + 1], L[4 * q + 2], L[4 * q + 3], l);
     tr4x4(H[4 * q], H[4 * q + 1], H[4 * q + 2], H[4 * q + 3], h);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) *reinterpret_cast<uint2*>(tile + cq_item(cqb, e, q)) = make_uint2(l[e], h[e]);
+    for (int e = 0; e < 4; ++e) *reinterpret_cast<uint2*>(tile + cq_item<K>(cqb, e, q)) = make_uint2(l[e], h[e]);
   }
 }
+template <int K>
 __device__ __forceinline__ void rcq_read(const uint8_t* tile, uint32_t cqb, uint32_t (&L)[16], uint32_t (&H)[16]) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     uint2 d[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) d[e] = *reinterpret_cast<const uint2*>(tile + cq_item(cqb, e, q));
+    for (int e = 0; e < 4; ++e) d[e] = *reinterpret_cast<const uint2*>(tile + cq_item<K>(cqb, e, q));
     tr4x4(d[0].x, d[1].x, d[2].x, d[3].x, &L[4 * q]);
     tr4x4(d[0].y, d[1].y, d[2].y, d[3].y, &H[4 * q]);
   }
@@ -143,8 +171,7 @@ __device__ __forceinline__ void rh_read(const uint8_t* tile, uint32_t base, uint
     H[j] = d.y;
   }
 }
-constexpr int kHA = 32;   // HA: item j at hab ^ 32 j (block + 4 j)
-constexpr int kHD = 128;  // HD: item j at hdb ^ 128 j (block + 16 j)
+constexpr int kHA = 32;  // HA: item j at hab ^ 32 j (block + 4 j)
 
 // ------------------------------------------------------ per-lane multiply ----
 // One output plane of c*y with all table dwords per lane (VGPRs): the subfield
@@ -231,18 +258,24 @@ __device__ __forceinline__ SubT delta_tables(const DevTables& T, uint32_t u, int
 }
 
 // ------------------------------------------------------------ transforms ----
-// Levels b < res_gen(I) of a size-1024 transform at index I hold skews
-// outside GF(2^8): Cantor(2T + (I >> b)) with 2T < 2^(10 - b) lies in GF(2^8)
-// for every group exactly when ((I + 1024) >> b) <= 256.  (fast_common.hpp
-// gen_of is the size-256 form of this rule.)  Index 0: 2; 1024: 3; 2048,
-// 3072: 4.
+// Levels b < res_gen(I) of a size-K transform at index I hold skews outside
+// GF(2^8): Cantor(2T + (I >> b)) with 2T < 2^(logK - b) lies in GF(2^8) for
+// every group exactly when ((I + K) >> b) <= 256.  (fast_common.hpp gen_of is
+// the size-256 form of this rule.)  K = 1024: index 0: 2; 1024: 3; 2048, 3072:
+// 4.  K = 512: 0: 1; 512: 2; 1024, 1536: 3; 2048-3584 (n = 4096): 4.
+template <int K>
 __host__ __device__ constexpr int res_gen(uint32_t I) {
   int b = 0;
-  while (((I + 1024u) >> b) > 256u) ++b;
+  while (((I + static_cast<uint32_t>(K)) >> b) > 256u) ++b;
   return b;
 }
-static_assert(res_gen(0) == 2 && res_gen(1024) == 3 && res_gen(2048) == 4 && res_gen(3072) == 4, "res_gen");
-static_assert(res_gen(4096) == 5 && res_gen(7168) == 5, "res_gen, n = 8192: level 4 (HA) full");
+static_assert(res_gen<1024>(0) == 2 && res_gen<1024>(1024) == 3 && res_gen<1024>(2048) == 4 &&
+                  res_gen<1024>(3072) == 4,
+              "res_gen");
+static_assert(res_gen<1024>(4096) == 5 && res_gen<1024>(7168) == 5, "res_gen, n = 8192: level 4 (HA) full");
+static_assert(res_gen<512>(0) == 1 && res_gen<512>(512) == 2 && res_gen<512>(1536) == 3 && res_gen<512>(2048) == 4 &&
+                  res_gen<512>(3584) == 4,
+              "res_gen, k = 512");
 
 // CQ levels 0-3 of a size-1024 transform at index I.  GEN: levels b < GEN
 // have full multipliers (gen_of(I), fast_common.hpp kSubLevel).  Group t of
@@ -406,26 +439,29 @@ __device__ __forceinline__ void rh_levels(const DevTables& T, uint32_t I, uint32
   tpipelined<rh_groups<R0, R1>()>(T, cval, group);
 }
 
-// HA: levels 4-7 (hi = position bits 8-9 = w >> 2).  HD: levels 8-9 (j bits
-// 2-3 = position bits 8-9; hi = 0).
+// HA: levels 4-7 (hi = position bits 8-9 = w >> 2; K = 512: bit 8).  HD:
+// the levels above 7 (register bits j hold position bits logK-4 .. logK-1:
+// K = 1024 levels 8-9 = j bits 2-3, K = 512 level 8 = j bit 3; hi = 0).
 template <bool INVERSE, int GEN = 0>
 __device__ __forceinline__ void ha_levels(const DevTables& T, uint32_t I, const Res& r, uint32_t (&L)[16],
                                           uint32_t (&H)[16]) {
   if constexpr (kExp & 512) return;
   rh_levels<4, 0, 4, INVERSE, GEN>(T, I, r.w >> 2, L, H);
 }
-template <bool INVERSE>
+template <int K, bool INVERSE>
 __device__ __forceinline__ void hd_levels(const DevTables& T, uint32_t I, uint32_t (&L)[16], uint32_t (&H)[16]) {
   if constexpr (kExp & 1024) return;
-  rh_levels<6, 2, 4, INVERSE>(T, I, 0u, L, H);
+  constexpr int pb0 = RGeo<K>::kLogK - 4;
+  rh_levels<pb0, 8 - pb0, 4, INVERSE>(T, I, 0u, L, H);
 }
 
-// A ^= D_1024(X) in the HD layout for one byte plane (inc_afft.rs:17-31,
+// A ^= D_K(X) in the HD layout for one byte plane (inc_afft.rs:17-31,
 // closed form SURVEY F7: D(x)[p] = x[p] ^ XOR over single bits l not in p of
-// x[p | l]): bits 0-1 inside the quad, bits 2-5 in the lanes of a DPP row
-// (l & 15: quad_perm for bits 2-3, row_shl 4 / 8 for bits 4-5), bits 6-9 in
-// the registers.
-__device__ __forceinline__ void add_derivative16(uint32_t (&A)[16], uint32_t (&X)[16], uint32_t lane) {
+// x[p | l]): bits 0-1 inside the quad, bits 2-5 (K = 512: 2-4) in the lanes
+// of a DPP row (l & 15: quad_perm for bits 2-3, row_shl 4 / 8 for bits 4-5),
+// the rest (6-9; K = 512: 5-8) in the registers.
+template <int K>
+__device__ __forceinline__ void add_derivative_hd(uint32_t (&A)[16], uint32_t (&X)[16], uint32_t lane) {
   const uint32_t r = lane & 15u;
   const uint32_t m0 = (r & 1u) ? 0u : ~0u, m1 = (r & 2u) ? 0u : ~0u;
   const uint32_t m2 = (r & 4u) ? 0u : ~0u, m3 = (r & 8u) ? 0u : ~0u;
@@ -436,7 +472,8 @@ __device__ __forceinline__ void add_derivative16(uint32_t (&A)[16], uint32_t (&X
     v ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0xB1, 0xF, 0xF, false)) & m0;
     v ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0x4E, 0xF, 0xF, false)) & m1;
     v ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0x104, 0xF, 0xF, false)) & m2;
-    v ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0x108, 0xF, 0xF, false)) & m3;
+    if constexpr (RGeo<K>::kLPC == 16)
+      v ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0x108, 0xF, 0xF, false)) & m3;
 #pragma unroll
     for (int jb = 0; jb < 4; ++jb)
       if (!(j & (1 << jb))) v ^= X[j | (1 << jb)];
@@ -473,11 +510,13 @@ __device__ __forceinline__ void rres_store_rows(uint8_t* out, size_t shard_len, 
 
 // ---------------------------------------------------------------- encode ----
 // One workgroup: 64 chunks of one payload.  mod.rs:144-154 /
-// inc_encode.rs:15-48: IFFT(1024, 0) of each chunk -> coefficients M (HD
-// layout, registers), then per shift s the FFT(1024, 1024 s) -> shard rows
-// 1024 s .. 1024 s + 1023; rows 0..1023 are the payload itself.
-__global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_res(
+// inc_encode.rs:15-48: IFFT(K, 0) of each chunk -> coefficients M (HD
+// layout, registers), then per shift s the FFT(K, K s) -> shard rows
+// K s .. K s + K - 1; rows 0..K-1 are the payload itself.
+template <int K>
+__global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_res(
     DevTables T, EncodeArgs a, uint32_t nchunks, uint32_t tiles) {
+  constexpr uint32_t kHD = RGeo<K>::kHD;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
   const TileRef tr = tile_of(blockIdx.x, tiles, (a.batch & 7u) == 0);
@@ -486,32 +525,32 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(4))) void k
   const uint32_t ncols = min(static_cast<uint32_t>(kRC), nchunks - ch0);
   const uint8_t* pay = a.payloads + static_cast<size_t>(pb) * a.payload_stride;
   uint8_t* out = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(ch0);
-  const Res r = res_coords();
+  const Res r = res_coords<K>();
   const bool full =
       ncols == kRC && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
   const uint32_t wanted_store = ((kExp & 2) && a.k != 12345u) ? 0u : a.wanted_n;  // experiment: no stores
 
-  // ---- payload tile: thread t moves block m = t & 255 of columns (t >> 8) + 4 i
+  // ---- payload tile: thread t moves block m = t mod K/4 of columns t / (K/4) + 4 i
   {
-    const uint32_t m = r.tid & 255u, c0 = r.tid >> 8;
+    const uint32_t m = r.tid % (K / 4), c0 = r.tid / (K / 4);
     const bool fast = ((reinterpret_cast<uintptr_t>(pay) & 7u) == 0) &&
-                      static_cast<size_t>(ch0 + kRC) * 2 * kRK <= a.payload_len;
-    const uint8_t* src = pay + static_cast<size_t>(ch0 + c0) * 2 * kRK + 8u * m;
+                      static_cast<size_t>(ch0 + kRC) * 2 * K <= a.payload_len;
+    const uint8_t* src = pay + static_cast<size_t>(ch0 + c0) * 2 * K + 8u * m;
     if (fast) {
       uint2 v[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = (kExp & 4) ? make_uint2(i, r.tid) : load_once(src + static_cast<size_t>(i) * 4 * 2 * kRK);
+      for (int i = 0; i < 16; ++i) v[i] = (kExp & 4) ? make_uint2(i, r.tid) : load_once(src + static_cast<size_t>(i) * 4 * 2 * K);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) *reinterpret_cast<uint2*>(tile + pq_addr(c0 + 4u * i, m)) = v[i];
+      for (int i = 0; i < 16; ++i) *reinterpret_cast<uint2*>(tile + pq_addr<K>(c0 + 4u * i, m)) = v[i];
     } else {
 #pragma unroll 1
       for (uint32_t i = 0; i < 16; ++i) {
-        const size_t g0 = static_cast<size_t>(ch0 + c0 + 4u * i) * 2 * kRK + 8u * m;
+        const size_t g0 = static_cast<size_t>(ch0 + c0 + 4u * i) * 2 * K + 8u * m;
         uint32_t wv[2] = {0, 0};
 #pragma unroll
         for (int e = 0; e < 8; ++e)
           if (g0 + e < a.payload_len) wv[e >> 2] |= static_cast<uint32_t>(pay[g0 + e]) << (8 * (e & 3));
-        *reinterpret_cast<uint2*>(tile + pq_addr(c0 + 4u * i, m)) = make_uint2(wv[0], wv[1]);
+        *reinterpret_cast<uint2*>(tile + pq_addr<K>(c0 + 4u * i, m)) = make_uint2(wv[0], wv[1]);
       }
     }
   }
@@ -519,12 +558,12 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(4))) void k
   // ---- CQ: systematic rows, inverse levels 0-3 (index 0: every multiplier in GF(2^8))
   {
     uint32_t L[16], H[16];
-    rcq_read_nat(tile, r.cqb, L, H);
+    rcq_read_nat<K>(tile, r.cqb, L, H);
     rres_store_rows(out, a.shard_len, 0, wanted_store, L, H, r, ncols, full);
     tower_convert(T, L, H);  // the transforms run in tower coordinates
-    rcq_levels<true, res_gen(0)>(T, 0, r, L, H);
+    rcq_levels<true, res_gen<K>(0)>(T, 0, r, L, H);
     __syncthreads();  // every wave has read its payload blocks
-    rcq_write(tile, fresh_v(r.cqb), L, H);
+    rcq_write<K>(tile, fresh_v(r.cqb), L, H);
   }
   __syncthreads();
   uint32_t ML[16], MH[16];
@@ -537,21 +576,21 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(4))) void k
     __syncthreads();
     rh_read<kHD>(tile, fresh_v(r.hdb), ML, MH);
   }
-  hd_levels<true>(T, 0, ML, MH);
+  hd_levels<K, true>(T, 0, ML, MH);
 #pragma unroll
   for (int q = 0; q < 16; ++q) asm volatile("" : "+v"(ML[q]), "+v"(MH[q]));  // materialise M once
 
-  const uint32_t nshift = a.n / kRK;
+  const uint32_t nshift = a.n / K;
   auto shift = [&](auto gc, uint32_t sh) __attribute__((always_inline)) {
     constexpr int GEN = decltype(gc)::value;
-    const uint32_t I = sh * kRK;
+    const uint32_t I = sh * K;
     uint32_t L[16], H[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       L[q] = ML[q];
       H[q] = MH[q];
     }
-    hd_levels<false>(T, I, L, H);
+    hd_levels<K, false>(T, I, L, H);
     __syncthreads();  // the previous CQ pass is done with the tile
     rh_write<kHD>(tile, fresh_v(r.hdb), L, H);
     __syncthreads();
@@ -560,32 +599,32 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(4))) void k
     __syncthreads();
     rh_write<kHA>(tile, fresh_v(r.hab), L, H);
     __syncthreads();
-    rcq_read(tile, fresh_v(r.cqb), L, H);
+    rcq_read<K>(tile, fresh_v(r.cqb), L, H);
     rcq_levels<false, GEN>(T, I, r, L, H);
     tower_convert(T, L, H);  // back to Cantor coordinates for the shard rows
     rres_store_rows(out, a.shard_len, I, wanted_store, L, H, r, ncols, full);
   };
-  if (nshift > 1 && kRK < a.wanted_n) shift(Int<res_gen(1024)>{}, 1);
+  if (nshift > 1 && K < a.wanted_n) shift(Int<res_gen<K>(K)>{}, 1);
 #pragma unroll 1
-  for (uint32_t sh = 2; sh < 4 && sh < nshift && sh * kRK < a.wanted_n; ++sh) shift(Int<res_gen(2048)>{}, sh);
+  for (uint32_t sh = 2; sh < 4 && sh < nshift && sh * K < a.wanted_n; ++sh) shift(Int<res_gen<K>(2 * K)>{}, sh);
 #pragma unroll 1
-  for (uint32_t sh = 4; sh < nshift && sh * kRK < a.wanted_n; ++sh) shift(Int<res_gen(4096)>{}, sh);  // n = 8192
+  for (uint32_t sh = 4; sh < nshift && sh * K < a.wanted_n; ++sh) shift(Int<res_gen<K>(4 * K)>{}, sh);  // n = 8K
 }
 
 // ----------------------------------------------------------- reconstruct ----
-// n = NQ * 1024, NQ in {2, 4, 8}.  As in k_reconstruct_fast (kernels_fast.hip,
-// DESIGN.md §4.3) the first k outputs are FFT(1024, 0)(d) with
+// n = NQ * K, NQ in {2, 4, 8}.  As in k_reconstruct_fast (kernels_fast.hip,
+// DESIGN.md §4.3) the first k outputs are FFT(K, 0)(d) with
 //   NQ = 2: d = D(x0) ^ x0 ^ x1,   NQ = 4: d = D(x0) ^ x1 ^ x2 ^ beta (x2 ^ x3),
 //   NQ = 8: d = D(x0) ^ sum_q kappa_q x_q (rec8_kappa_res),
-// x_q = IFFT(1024, 1024 q)(premultiplied segment q), beta = Cantor(2) and D
-// the size-1024 formal derivative -- here every x_q is computed whole in the
-// workgroup (CQ -> HA -> HD) and d accumulates in the HD layout, where all ten
-// position bits are reachable for D (add_derivative16).
+// x_q = IFFT(K, K q)(premultiplied segment q), beta = Cantor(2) and D the
+// size-K formal derivative -- here every x_q is computed whole in the
+// workgroup (CQ -> HA -> HD) and d accumulates in the HD layout, where every
+// position bit is reachable for D (add_derivative_hd).
 //
 // Row multipliers: the payload's prefix record (k_prefix_locator): one 80-byte
 // table per row (the premultiply's Cantor -> tower map for present rows, the
 // postmultiply's tower -> Cantor map for erased ones).  CQ lanes of one wave
-// hold 4 different rows per register (u), so a segment's 1024 tables are
+// hold 4 different rows per register (u), so a segment's K tables are
 // staged into the LDS tile (free between the HD read and the next exchange)
 // and read per lane; absent rows get zero tables (their rows read as zeros).
 constexpr uint32_t kRowSlot = 80;  // bytes per staged row table
@@ -594,7 +633,8 @@ constexpr uint32_t kRowSlot = 80;  // bytes per staged row table
 // rows r, r + 16, r + 32, r + 48 of one wave-instruction hit different banks.
 constexpr uint32_t kRowGroup = 16 * kRowSlot + 16;
 __host__ __device__ constexpr uint32_t row_slot(uint32_t r) { return kRowGroup * (r >> 4) + kRowSlot * (r & 15u); }
-static_assert(row_slot(1023) + kRowSlot <= kRTileBytes, "row tables fit the tile");
+static_assert(row_slot(1023) + kRowSlot <= RGeo<1024>::kTileBytes, "row tables fit the tile");
+static_assert(row_slot(511) + kRowSlot <= RGeo<512>::kTileBytes, "row tables fit the tile");
 
 // Thread t stages the table of row row0 + t (zeros for an absent row, so that
 // its premultiplied zero row stays zero without a select).
@@ -658,7 +698,8 @@ __device__ __forceinline__ void load_lane_rows(uint2 (&raw)[NR], const uint8_t* 
 
 // The merge's output: CQ registers (positions 64 w + 16 u + i of columns
 // 4 cq .. + 3) -> bytes [2 (64 w + 16 u), + 32) of each of the 4 output
-// columns (2 KiB each).
+// columns (2K bytes each).
+template <int K>
 __device__ __forceinline__ void res_copy_out(uint8_t* out_tile, const uint32_t (&L)[16], const uint32_t (&H)[16],
                                              const Res& r, uint32_t ncols, bool aligned16) {
   uint2 d[4][4];
@@ -668,7 +709,7 @@ __device__ __forceinline__ void res_copy_out(uint8_t* out_tile, const uint32_t (
   for (int e = 0; e < 4; ++e) {
     const uint32_t c = 4u * r.cq + e;
     if (c >= ncols) break;
-    uint8_t* o = out_tile + static_cast<size_t>(c) * 2 * kRK + 128u * r.w + 32u * r.u;
+    uint8_t* o = out_tile + static_cast<size_t>(c) * 2 * K + 128u * r.w + 32u * r.u;
     if (aligned16) {
       *reinterpret_cast<uint4*>(o) = make_uint4(d[0][e].x, d[0][e].y, d[1][e].x, d[1][e].y);
       *reinterpret_cast<uint4*>(o + 16) = make_uint4(d[2][e].x, d[2][e].y, d[3][e].x, d[3][e].y);
@@ -686,7 +727,7 @@ __host__ __device__ constexpr int res_seg(int step) {  // segments 2, 3, 1, 0 (N
   return NQ == 8 ? 7 - step : NQ == 4 ? (step == 0 ? 2 : step == 1 ? 3 : 3 - step) : 1 - step;
 }
 
-// Step STEP of the segment sweep: x_q = IFFT(1024, 1024 q)(premultiplied
+// Step STEP of the segment sweep: x_q = IFFT(K, K q)(premultiplied
 // segment q), folded into d (A, HD layout).  Steps are compile-time: each has
 // one CQ instance (its GEN) and its own fold, with no runtime branch between
 // instances (a branch over instances inside a loop made the allocator spill).
@@ -697,14 +738,15 @@ __host__ __device__ constexpr uint32_t rec8_kappa_res(int q) {
   return k[q];
 }
 
-template <int NQ, int STEP>
+template <int K, int NQ, int STEP>
 __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructArgs& a, uint8_t* tile,
                                          const uint8_t* pools, const uint8_t* pres, const uint8_t* sh,
                                          uint8_t* out_tile, uint32_t ncols, bool full, bool out16, uint32_t (&AL)[16],
                                          uint32_t (&AH)[16]) {
   constexpr int q = res_seg<NQ>(STEP);
-  constexpr uint32_t I = static_cast<uint32_t>(q) * kRK;
-  const Res rr = res_coords();  // opaque per step: lane-derived values are not hoisted across steps
+  constexpr uint32_t I = static_cast<uint32_t>(q) * K;
+  constexpr uint32_t kHD = RGeo<K>::kHD;
+  const Res rr = res_coords<K>();  // opaque per step: lane-derived values are not hoisted across steps
   uint32_t XL[16], XH[16];
   {
     const uint32_t pm = lane_rows_present(pres, I, rr);
@@ -728,24 +770,24 @@ __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructAr
     }
   }
   if constexpr ((kExp & 16384) != 0 && STEP == 0) {  // experiment: the first step's premultiplied rows
-    res_copy_out(out_tile, XL, XH, rr, ncols, out16);
+    res_copy_out<K>(out_tile, XL, XH, rr, ncols, out16);
     return false;
   }
-  rcq_levels<true, res_gen(I)>(T, I, rr, XL, XH);
+  rcq_levels<true, res_gen<K>(I)>(T, I, rr, XL, XH);
   if constexpr ((kExp & 32768) != 0 && STEP == 0) {  // experiment: the first step after its CQ levels
-    res_copy_out(out_tile, XL, XH, rr, ncols, out16);
+    res_copy_out<K>(out_tile, XL, XH, rr, ncols, out16);
     return false;
   }
   __syncthreads();  // every wave has read its row tables
-  rcq_write(tile, fresh_v(rr.cqb), XL, XH);
+  rcq_write<K>(tile, fresh_v(rr.cqb), XL, XH);
   __syncthreads();
   rh_read<kHA>(tile, fresh_v(rr.hab), XL, XH);
-  ha_levels<true, res_gen(I)>(T, I, rr, XL, XH);
+  ha_levels<true, res_gen<K>(I)>(T, I, rr, XL, XH);
   __syncthreads();
   rh_write<kHA>(tile, fresh_v(rr.hab), XL, XH);
   __syncthreads();
   rh_read<kHD>(tile, fresh_v(rr.hdb), XL, XH);
-  hd_levels<true>(T, I, XL, XH);
+  hd_levels<K, true>(T, I, XL, XH);
   // fold x_q into d (kernels_fast.hip rec_segments)
   if constexpr (NQ == 8 && q != 0 && rec8_kappa_res(q) != 1u) {  // d ^= kappa_q x_q, kappa_q in GF(16)
     uint32_t kp[20];
@@ -766,8 +808,8 @@ __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructAr
 #pragma unroll
       for (int j = 0; j < 16; ++j) AL[j] ^= XL[j], AH[j] ^= XH[j];
     }
-    add_derivative16(AL, XL, rr.l);
-    add_derivative16(AH, XH, rr.l);
+    add_derivative_hd<K>(AL, XL, rr.l);
+    add_derivative_hd<K>(AH, XH, rr.l);
   } else if constexpr (NQ == 4 && q == 3) {  // A = x2 ^ beta (x2 ^ x3)
     uint32_t beta[20];
     pool_of<true>(T, 2u, beta);  // beta = Cantor(2), in GF(2^8)
@@ -785,36 +827,37 @@ __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructAr
   return true;
 }
 
-template <int NQ, int... STEP>
+template <int K, int NQ, int... STEP>
 __device__ __forceinline__ bool res_sweep(const DevTables& T, const ReconstructArgs& a, uint8_t* tile,
                                           const uint8_t* pools, const uint8_t* pres, const uint8_t* sh,
                                           uint8_t* out_tile, uint32_t ncols, bool full, bool out16,
                                           uint32_t (&AL)[16], uint32_t (&AH)[16], std::integer_sequence<int, STEP...>) {
-  return (res_step<NQ, STEP>(T, a, tile, pools, pres, sh, out_tile, ncols, full, out16, AL, AH) && ...);
+  return (res_step<K, NQ, STEP>(T, a, tile, pools, pres, sh, out_tile, ncols, full, out16, AL, AH) && ...);
 }
 
-// One tile; NQ segments of 1024 rows (a.n = NQ * 1024, or a trusted 2-segment
-// prefix of n = 4096).
-template <int NQ>
+// One tile; NQ segments of K rows (a.n = NQ * K, or a trusted 2-segment
+// prefix of n = 4K).
+template <int K, int NQ>
 __device__ __forceinline__ void res_decode_tile(const DevTables& T, const ReconstructArgs& a, uint8_t* tile,
                                                 const uint8_t* pools, const uint8_t* pres, const uint8_t* sh,
                                                 uint8_t* out_tile, uint32_t ncols, bool full, bool out16) {
   uint32_t AL[16], AH[16];
-  if (!res_sweep<NQ>(T, a, tile, pools, pres, sh, out_tile, ncols, full, out16, AL, AH,
+  if (!res_sweep<K, NQ>(T, a, tile, pools, pres, sh, out_tile, ncols, full, out16, AL, AH,
                      std::make_integer_sequence<int, NQ>{}))
     return;
-  const Res r = res_coords();
+  constexpr uint32_t kHD = RGeo<K>::kHD, lpc = RGeo<K>::kLPC;
+  const Res r = res_coords<K>();
   if constexpr ((kExp & 8192) != 0) {  // experiment (tools/res_debug_rec.py): d in natural blocks, tower coordinates
-    const uint32_t c = 4u * r.w + (r.l >> 4);
+    const uint32_t c = (64u / lpc) * r.w + r.l / lpc;
 #pragma unroll
     for (int j = 0; j < 16; ++j)
       if (c < ncols)
-        *reinterpret_cast<uint2*>(out_tile + static_cast<size_t>(c) * 2 * kRK + 8u * ((r.l & 15u) + 16u * j)) =
+        *reinterpret_cast<uint2*>(out_tile + static_cast<size_t>(c) * 2 * K + 8u * (r.l % lpc + lpc * j)) =
             quad_to_blk(AL[j], AH[j]);
     return;
   }
-  // ---- out = FFT(1024, 0)(d), first k rows (inc_reconstruct.rs:80)
-  hd_levels<false>(T, 0, AL, AH);
+  // ---- out = FFT(K, 0)(d), first k rows (inc_reconstruct.rs:80)
+  hd_levels<K, false>(T, 0, AL, AH);
   __syncthreads();  // the last step's HD read is done
   rh_write<kHD>(tile, fresh_v(r.hdb), AL, AH);
   __syncthreads();
@@ -823,8 +866,8 @@ __device__ __forceinline__ void res_decode_tile(const DevTables& T, const Recons
   __syncthreads();
   rh_write<kHA>(tile, fresh_v(r.hab), AL, AH);
   __syncthreads();
-  rcq_read(tile, fresh_v(r.cqb), AL, AH);
-  rcq_levels<false, res_gen(0)>(T, 0, r, AL, AH);
+  rcq_read<K>(tile, fresh_v(r.cqb), AL, AH);
+  rcq_levels<false, res_gen<K>(0)>(T, 0, r, AL, AH);
   // ---- merge: received systematic rows, postmultiplied recovered ones
   // (inc_reconstruct.rs:46-50, :82-84; tower in, Cantor out)
   const uint32_t pm = lane_rows_present(pres, 0, r);
@@ -845,27 +888,28 @@ __device__ __forceinline__ void res_decode_tile(const DevTables& T, const Recons
     AL[i] = l;
     AH[i] = h;
   }
-  res_copy_out(out_tile, AL, AH, r, ncols, out16);
+  res_copy_out<K>(out_tile, AL, AH, r, ncols, out16);
 }
 
 // Every systematic row present: the output is those rows (inc_reconstruct.rs:46-50).
+template <int K>
 __device__ __forceinline__ void res_copy_tile(const ReconstructArgs& a, const uint8_t* sh, uint8_t* out_tile,
                                               uint32_t ncols, bool full, bool out16, const DevTables& T) {
-  const Res r = res_coords();
+  const Res r = res_coords<K>();
   uint2 raw[16];
   load_lane_rows(raw, sh, a.shard_len, 0, 0xffffu, r, ncols, full, T.zeros);
   uint32_t L[16], H[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) blk_to_quad(raw[i], L[i], H[i]);
-  res_copy_out(out_tile, L, H, r, ncols, out16);
+  res_copy_out<K>(out_tile, L, H, r, ncols, out16);
 }
 
 // One workgroup per 64-column tile.  SERVE = 1: payloads whose record says
-// copy (nq = 1); 2: decodes from 2 segments (n = 2048, or a trusted prefix of
-// n = 4096 / 8192); 4 / 8: the 4- / 8-segment decodes.  The host launches
-// the instances over the same grid (kernels_fast.hip's scheme).
-template <int SERVE>
-__global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(4))) void k_reconstruct_res(
+// copy (nq = 1); 2: decodes from 2 segments (n = 2K, or a trusted prefix of
+// n = 4K); 4 / 8: the 4- / 8-segment decodes.  The host launches the
+// instances over the same grid (kernels_fast.hip's scheme).
+template <int K, int SERVE>
+__global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4))) void k_reconstruct_res(
     DevTables T, ReconstructArgs a, uint32_t nsyms, uint32_t tiles) {
   // SERVE = 1: copies (nq = 1); 2: 2-segment decodes; 4: 4-segment decodes
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -879,14 +923,14 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(4))) void k
   const uint32_t col0 = tl * kRC;
   const uint32_t ncols = min(static_cast<uint32_t>(kRC), nsyms - col0);
   const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);
-  uint8_t* out_tile = a.out + static_cast<size_t>(pb) * a.out_stride + static_cast<size_t>(col0) * 2 * kRK;
+  uint8_t* out_tile = a.out + static_cast<size_t>(pb) * a.out_stride + static_cast<size_t>(col0) * 2 * K;
   const bool full =
       ncols == kRC && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
   const bool out16 = ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 15u) == 0;
   if constexpr (SERVE == 1)
-    res_copy_tile(a, sh, out_tile, ncols, full, out16, T);
+    res_copy_tile<K>(a, sh, out_tile, ncols, full, out16, T);
   else
-    res_decode_tile<SERVE>(T, a, smem, pools, pres, sh, out_tile, ncols, full, out16);
+    res_decode_tile<K, SERVE>(T, a, smem, pools, pres, sh, out_tile, ncols, full, out16);
 }
 
 }  // namespace
@@ -899,46 +943,68 @@ bool res_enabled() {
   return on;
 }
 
-bool res_encode_supported(uint32_t n, uint32_t k) { return k == 1024 && (n == 2048 || n == 4096 || n == 8192); }
-bool res_reconstruct_supported(uint32_t n, uint32_t k) { return k == 1024 && (n == 2048 || n == 4096 || n == 8192); }
+// k = 512 and 1024 with n / k in {2, 4, 8} (n <= 8K: res_gen <= 5).
+bool res_encode_supported(uint32_t n, uint32_t k) { return (k == 512 || k == 1024) && (n == 2 * k || n == 4 * k || n == 8 * k); }
+bool res_reconstruct_supported(uint32_t n, uint32_t k) { return res_encode_supported(n, k); }
 
-hipError_t launch_reconstruct_res(const DevTables& T, const ReconstructArgs& a, hipStream_t s) {
+namespace {
+template <int K>
+hipError_t launch_reconstruct_res_k(const DevTables& T, const ReconstructArgs& a, hipStream_t s) {
+  using G = RGeo<K>;
   const size_t nsyms = a.shard_len / 2;
   if (nsyms == 0 || a.batch == 0) return hipSuccess;
-  if (nsyms > 0xffffffffu || !res_reconstruct_supported(a.n, a.k)) return hipErrorInvalidValue;
+  if (nsyms > 0xffffffffu) return hipErrorInvalidValue;
   const uint32_t tiles = static_cast<uint32_t>((nsyms + kRC - 1) / kRC);
   const size_t blocks = a.batch * tiles;
   if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
-  k_reconstruct_res<1><<<static_cast<uint32_t>(blocks), kRT, 0, s>>>(T, a, static_cast<uint32_t>(nsyms), tiles);
-  if (a.n == 2048 || a.trusted)
-    k_reconstruct_res<2><<<static_cast<uint32_t>(blocks), kRT, kRTileBytes, s>>>(T, a, static_cast<uint32_t>(nsyms), tiles);
-  if (a.n == 4096)
-    k_reconstruct_res<4><<<static_cast<uint32_t>(blocks), kRT, kRTileBytes, s>>>(T, a, static_cast<uint32_t>(nsyms), tiles);
-  if (a.n == 8192)
-    k_reconstruct_res<8><<<static_cast<uint32_t>(blocks), kRT, kRTileBytes, s>>>(T, a, static_cast<uint32_t>(nsyms), tiles);
+  const uint32_t nb = static_cast<uint32_t>(blocks), ns = static_cast<uint32_t>(nsyms);
+  k_reconstruct_res<K, 1><<<nb, G::kThreads, 0, s>>>(T, a, ns, tiles);
+  if (a.n == 2u * K || a.trusted) k_reconstruct_res<K, 2><<<nb, G::kThreads, G::kTileBytes, s>>>(T, a, ns, tiles);
+  if (a.n == 4u * K) k_reconstruct_res<K, 4><<<nb, G::kThreads, G::kTileBytes, s>>>(T, a, ns, tiles);
+  if (a.n == 8u * K) k_reconstruct_res<K, 8><<<nb, G::kThreads, G::kTileBytes, s>>>(T, a, ns, tiles);
   return hipGetLastError();
 }
 
-hipError_t launch_encode_res(const DevTables& T, const EncodeArgs& a, hipStream_t s) {
+template <int K>
+hipError_t launch_encode_res_k(const DevTables& T, const EncodeArgs& a, hipStream_t s) {
+  using G = RGeo<K>;
   const size_t nchunks = (a.payload_len + 2 * a.k - 1) / (2 * a.k);
   if (nchunks == 0 || a.batch == 0) return hipSuccess;
   if (nchunks > 0xffffffffu) return hipErrorInvalidValue;
   const uint32_t tiles = static_cast<uint32_t>((nchunks + kRC - 1) / kRC);
   const size_t blocks = a.batch * tiles;
   if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
-  k_encode_res<<<static_cast<uint32_t>(blocks), kRT, kRTileBytes, s>>>(T, a, static_cast<uint32_t>(nchunks), tiles);
+  k_encode_res<K><<<static_cast<uint32_t>(blocks), G::kThreads, G::kTileBytes, s>>>(T, a, static_cast<uint32_t>(nchunks), tiles);
   return hipGetLastError();
 }
 
-hipError_t configure_res_kernels() {
+template <int K>
+hipError_t configure_res_k() {
   hipError_t e = hipSuccess;
-  for (const void* f : {reinterpret_cast<const void*>(&k_encode_res), reinterpret_cast<const void*>(&k_reconstruct_res<2>),
-                        reinterpret_cast<const void*>(&k_reconstruct_res<4>),
-                        reinterpret_cast<const void*>(&k_reconstruct_res<8>)}) {
-    const hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kRTileBytes));
+  for (const void* f : {reinterpret_cast<const void*>(&k_encode_res<K>), reinterpret_cast<const void*>(&k_reconstruct_res<K, 2>),
+                        reinterpret_cast<const void*>(&k_reconstruct_res<K, 4>),
+                        reinterpret_cast<const void*>(&k_reconstruct_res<K, 8>)}) {
+    const hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(RGeo<K>::kTileBytes));
     if (r != hipSuccess && e == hipSuccess) e = r;
   }
   return e;
+}
+}  // namespace
+
+hipError_t launch_reconstruct_res(const DevTables& T, const ReconstructArgs& a, hipStream_t s) {
+  if (!res_reconstruct_supported(a.n, a.k)) return hipErrorInvalidValue;
+  return a.k == 512 ? launch_reconstruct_res_k<512>(T, a, s) : launch_reconstruct_res_k<1024>(T, a, s);
+}
+
+hipError_t launch_encode_res(const DevTables& T, const EncodeArgs& a, hipStream_t s) {
+  if (!res_encode_supported(a.n, a.k)) return hipErrorInvalidValue;
+  return a.k == 512 ? launch_encode_res_k<512>(T, a, s) : launch_encode_res_k<1024>(T, a, s);
+}
+
+hipError_t configure_res_kernels() {
+  const hipError_t e = configure_res_k<1024>();
+  const hipError_t f = configure_res_k<512>();
+  return e != hipSuccess ? e : f;
 }
 
 }  // namespace np
