@@ -484,20 +484,59 @@ __device__ __forceinline__ void add_derivative_hd(uint32_t (&A)[16], uint32_t (&
 }
 
 // ------------------------------------------------------------ shard rows ----
+// A full tile's shard-row pieces move as 8-byte vector accesses, and the
+// decode's output as 16-byte ones, at any even (rows) / any (output) address:
+// the KFD runs gfx9 queues in unaligned-access mode (SH_MEM_CONFIG alignment
+// mode UNALIGNED; tools/microbench/unaligned.hip checks the bytes and the
+// rates), so odd or 2-mod-4 chunk counts -- rows 2- or 4-byte aligned, e.g.
+// the reference bench's 10 MB payloads at k = 512 -- keep the vector path
+// instead of per-symbol accesses.  The parity tests with odd chunk counts pin
+// it.  NP_RES_UNALIGNED=0 restores 8- / 16-byte alignment requirements.
+#ifndef NP_RES_UNALIGNED
+#define NP_RES_UNALIGNED 1
+#endif
+__device__ __forceinline__ bool rows_vec_ok(const void* p, size_t stride, size_t len) {
+  constexpr uintptr_t m = NP_RES_UNALIGNED ? 1u : 7u;
+  return ((reinterpret_cast<uintptr_t>(p) | stride | len) & m) == 0;
+}
+// Streaming row stores: 0 always, 1 for rows of whole 128-byte lines, 2 for
+// 8-byte aligned rows.
+#ifndef NP_RES_NT_MODE
+#define NP_RES_NT_MODE 1
+#endif
+__device__ __forceinline__ bool res_rows_nt(const void* p, size_t stride, size_t len) {
+  const uintptr_t v = reinterpret_cast<uintptr_t>(p) | stride | len;
+  return NP_RES_NT_MODE == 0 ? true : NP_RES_NT_MODE == 1 ? (v & 127u) == 0 : (v & 7u) == 0;
+}
+__device__ __forceinline__ bool out_vec_ok(const void* p, size_t stride) {
+  return NP_RES_UNALIGNED || ((reinterpret_cast<uintptr_t>(p) | stride) & 15u) == 0;
+}
+
 // This lane's 8 bytes (columns 4 cq .. 4 cq + 3) of shard rows
 // row0 + 64 w + 16 u + i, i = 0..15.  `out` = row 0, column 0 of the tile.
+// nt: streaming stores (rows of whole 128-byte lines); rows that start
+// inside a line (odd chunk counts) store with the default policy, so that L2
+// merges the pieces of a line that neighbouring waves write.
 __device__ __forceinline__ void rres_store_rows(uint8_t* out, size_t shard_len, uint32_t row0, uint32_t wanted_n,
                                                 const uint32_t (&L)[16], const uint32_t (&H)[16], const Res& r,
-                                                uint32_t ncols, bool full) {
+                                                uint32_t ncols, bool full, bool nt) {
   const uint32_t rb = row0 + 64u * fresh(r.w);  // first row of this wave
   if (full && rb + 64u <= wanted_n && 64u * shard_len < 0x7fffffffu) {
     const __amdgpu_buffer_rsrc_t rs = buf_rsrc(out + static_cast<size_t>(rb) * shard_len, 64u * static_cast<uint32_t>(shard_len));
     const uint32_t vo = fresh_v(16u * r.u * static_cast<uint32_t>(shard_len) + 8u * r.cq);
+    if (nt) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const uint2 v = cq_row(L[i], H[i]);
-      __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, rs, vo, static_cast<uint32_t>(i * shard_len),
-                                            NP_ROW_STORE_CPOL);
+      for (int i = 0; i < 16; ++i) {
+        const uint2 v = cq_row(L[i], H[i]);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, rs, vo, static_cast<uint32_t>(i * shard_len),
+                                              NP_ROW_STORE_CPOL);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const uint2 v = cq_row(L[i], H[i]);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, rs, vo, static_cast<uint32_t>(i * shard_len), 0);
+      }
     }
     return;
   }
@@ -527,13 +566,14 @@ __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4))) void k_e
   uint8_t* out = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(ch0);
   const Res r = res_coords<K>();
   const bool full =
-      ncols == kRC && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
+      ncols == kRC && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
+  const bool nt = res_rows_nt(a.shards, a.batch_stride, a.shard_len);
   const uint32_t wanted_store = ((kExp & 2) && a.k != 12345u) ? 0u : a.wanted_n;  // experiment: no stores
 
   // ---- payload tile: thread t moves block m = t mod K/4 of columns t / (K/4) + 4 i
   {
     const uint32_t m = r.tid % (K / 4), c0 = r.tid / (K / 4);
-    const bool fast = ((reinterpret_cast<uintptr_t>(pay) & 7u) == 0) &&
+    const bool fast = out_vec_ok(pay, 0) &&  // (8-byte loads at any address, see rows_vec_ok)
                       static_cast<size_t>(ch0 + kRC) * 2 * K <= a.payload_len;
     const uint8_t* src = pay + static_cast<size_t>(ch0 + c0) * 2 * K + 8u * m;
     if (fast) {
@@ -559,7 +599,7 @@ __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4))) void k_e
   {
     uint32_t L[16], H[16];
     rcq_read_nat<K>(tile, r.cqb, L, H);
-    rres_store_rows(out, a.shard_len, 0, wanted_store, L, H, r, ncols, full);
+    rres_store_rows(out, a.shard_len, 0, wanted_store, L, H, r, ncols, full, nt);
     tower_convert(T, L, H);  // the transforms run in tower coordinates
     rcq_levels<true, res_gen<K>(0)>(T, 0, r, L, H);
     __syncthreads();  // every wave has read its payload blocks
@@ -602,7 +642,7 @@ __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4))) void k_e
     rcq_read<K>(tile, fresh_v(r.cqb), L, H);
     rcq_levels<false, GEN>(T, I, r, L, H);
     tower_convert(T, L, H);  // back to Cantor coordinates for the shard rows
-    rres_store_rows(out, a.shard_len, I, wanted_store, L, H, r, ncols, full);
+    rres_store_rows(out, a.shard_len, I, wanted_store, L, H, r, ncols, full, nt);
   };
   if (nshift > 1 && K < a.wanted_n) shift(Int<res_gen<K>(K)>{}, 1);
 #pragma unroll 1
@@ -925,8 +965,8 @@ __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4))) void k_r
   const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);
   uint8_t* out_tile = a.out + static_cast<size_t>(pb) * a.out_stride + static_cast<size_t>(col0) * 2 * K;
   const bool full =
-      ncols == kRC && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
-  const bool out16 = ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 15u) == 0;
+      ncols == kRC && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
+  const bool out16 = out_vec_ok(a.out, a.out_stride);
   if constexpr (SERVE == 1)
     res_copy_tile<K>(a, sh, out_tile, ncols, full, out16, T);
   else

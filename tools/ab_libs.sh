@@ -10,7 +10,7 @@ i=0
 for r in $(seq 1 $R); do
   j=0
   for lib in "$@"; do
-    NP_LIB_PATH=$PWD/$lib timeout -k 10 120 python bench.py --no-cpu --config ${CONFIG:-3} --steps 20 --warmup 3 > gpurun_out/ab/L${j}_$r.log 2>&1 || { tail -5 gpurun_out/ab/L${j}_$r.log; exit 1; }
+    NP_LIB_PATH=$PWD/$lib timeout -k 10 120 python bench.py --no-cpu ${BENCH_ARGS:---config ${CONFIG:-3}} --steps 20 --warmup 3 > gpurun_out/ab/L${j}_$r.log 2>&1 || { tail -5 gpurun_out/ab/L${j}_$r.log; exit 1; }
     j=$((j+1))
   done
 done
