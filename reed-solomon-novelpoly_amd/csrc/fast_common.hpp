@@ -506,8 +506,15 @@ __device__ __forceinline__ void cq_to_blks(const uint32_t* cl, const uint32_t* c
   d[3] = make_uint2(vperm(r1.y, r0.y, 0x07060302u), vperm(r3.y, r2.y, 0x07060302u));
 }
 
+// NP_UNALIGNED: vector accesses at any even address (rows_vec_ok below).
+#ifndef NP_UNALIGNED
+#define NP_UNALIGNED 1
+#endif
+
 // 4 symbols (columns 4l..4l+3 of one shard row) to / from global memory.
 // `full` (wave-uniform) = whole 256-column tile present and 8-byte aligned rows.
+// Partial tiles: lanes whose four columns all exist still use one 8-byte
+// access (any even address, NP_UNALIGNED below).
 __device__ __forceinline__ void store4(uint8_t* rowp, uint2 v, uint32_t lane, uint32_t ncols, bool full) {
   if (full) {
     *reinterpret_cast<uint2*>(rowp + 8u * lane) = v;
@@ -523,7 +530,7 @@ __device__ __forceinline__ void store4(uint8_t* rowp, uint2 v, uint32_t lane, ui
 }
 
 __device__ __forceinline__ uint2 load4(const uint8_t* rowp, uint32_t lane, uint32_t ncols, bool full) {
-  if (full) return *reinterpret_cast<const uint2*>(rowp + 8u * lane);
+  if (full || (NP_UNALIGNED && 4 * lane + 4 <= ncols)) return *reinterpret_cast<const uint2*>(rowp + 8u * lane);
   uint32_t w[2] = {0, 0};
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -587,6 +594,31 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uin
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, static_cast<int>(bytes), 0x00020000);
 }
 
+// A full tile's shard-row pieces move as 8-byte vector accesses, payload
+// blocks and the decode's output as 8- / 16-byte ones, at any even (rows) / any (output) address:
+// the KFD runs gfx9 queues in unaligned-access mode (SH_MEM_CONFIG alignment
+// mode UNALIGNED; tools/microbench/unaligned.hip checks the bytes and the
+// rates), so odd or 2-mod-4 chunk counts -- rows 2- or 4-byte aligned, e.g.
+// the reference bench's 10 MB payloads at k = 512 -- keep the vector path
+// instead of per-symbol accesses.  The parity tests with odd chunk counts pin
+// it.  NP_UNALIGNED=0 restores 8- / 16-byte alignment requirements.
+__device__ __forceinline__ bool rows_vec_ok(const void* p, size_t stride, size_t len) {
+  constexpr uintptr_t m = NP_UNALIGNED ? 1u : 7u;
+  return ((reinterpret_cast<uintptr_t>(p) | stride | len) & m) == 0;
+}
+// Streaming row stores: 0 always, 1 for rows of whole 128-byte lines, 2 for
+// 8-byte aligned rows.
+#ifndef NP_ROW_NT_MODE
+#define NP_ROW_NT_MODE 1
+#endif
+__device__ __forceinline__ bool rows_nt(const void* p, size_t stride, size_t len) {
+  const uintptr_t v = reinterpret_cast<uintptr_t>(p) | stride | len;
+  return NP_ROW_NT_MODE == 0 ? true : NP_ROW_NT_MODE == 1 ? (v & 127u) == 0 : (v & 7u) == 0;
+}
+__device__ __forceinline__ bool out_vec_ok(const void* p, size_t stride) {
+  return NP_UNALIGNED || ((reinterpret_cast<uintptr_t>(p) | stride) & 15u) == 0;
+}
+
 // Shard rows row0..row0+15 (those below wanted_n) from cq registers.
 // Shard rows are written once and never read back by the encode: streaming
 // (nontemporal, the nt bit of the buffer store) stores leave L2 to the tiles
@@ -594,17 +626,30 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uin
 #ifndef NP_ROW_STORE_CPOL
 #define NP_ROW_STORE_CPOL 2
 #endif
+// nt (rows_nt): streaming stores; otherwise the default policy.
 __device__ __forceinline__ void store_rows(uint8_t* out, size_t shard_len, uint32_t row0, uint32_t wanted_n,
                                            const uint32_t (&L)[16], const uint32_t (&H)[16], uint32_t lane,
-                                           uint32_t ncols, bool full) {
+                                           uint32_t ncols, bool full, bool nt = true) {
   if (full && row0 + 16 <= wanted_n && 16 * shard_len < 0x7fffffffu) {
     const __amdgpu_buffer_rsrc_t r = buf_rsrc(out + static_cast<size_t>(row0) * shard_len, 16 * static_cast<uint32_t>(shard_len));
+    if (nt) {
 #pragma unroll
-    for (int p = 0; p < 16; ++p) {
-      const uint2 v = cq_row(L[p], H[p]);
-      __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, r, 8u * lane,
-                                            static_cast<uint32_t>(p * shard_len), NP_ROW_STORE_CPOL);
+      for (int p = 0; p < 16; ++p) {
+        const uint2 v = cq_row(L[p], H[p]);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, r, 8u * lane,
+                                              static_cast<uint32_t>(p * shard_len), NP_ROW_STORE_CPOL);
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < 16; ++p) {
+        const uint2 v = cq_row(L[p], H[p]);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, r, 8u * lane, static_cast<uint32_t>(p * shard_len), 0);
+      }
     }
+  } else if (NP_UNALIGNED && 4 * lane + 4 <= ncols) {  // partial tile, lanes with all four columns
+#pragma unroll
+    for (int p = 0; p < 16; ++p)
+      if (row0 + p < wanted_n) *reinterpret_cast<uint2*>(out + static_cast<size_t>(row0 + p) * shard_len + 8u * lane) = cq_row(L[p], H[p]);
   } else {
 #pragma unroll
     for (int p = 0; p < 16; ++p)

@@ -233,10 +233,10 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   uint8_t* scrW = scrM + (SUBS - 1) * kSegScr;  // W_s at scrW + s slots, s >= 1
   const uint32_t tid = threadIdx.x, lane = tid & 63u, g = uniform(tid >> 6);
   const bool full =
-      ncols == kTile && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
+      ncols == kTile && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
   const uint32_t cqb = col_base<kS>(4 * lane) ^ (32u * g);
   const uint32_t hb = col_base<kS>(tid / G::R) ^ (8u * (tid % G::R));
-  const bool fast_in = ((reinterpret_cast<uintptr_t>(pay) & 7u) == 0) &&
+  const bool fast_in = out_vec_ok(pay, 0) &&
                        static_cast<size_t>(ch0 + kTile) * 2 * KB <= a.payload_len;
 
   // ---- phase 1: x_s = IFFT(256, 256 s)(sub-segment s of every chunk)
@@ -275,7 +275,8 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       uint32_t CL[16], CH[16];
       const uint32_t cq = fresh_v(cqb);
       cq_read<kS>(tile, cq, CL, CH);
-      store_rows(out, a.shard_len, index + 16 * g, a.wanted_n, CL, CH, lane, ncols, full);  // systematic rows
+      store_rows(out, a.shard_len, index + 16 * g, a.wanted_n, CL, CH, lane, ncols, full,
+                 rows_nt(a.shards, a.batch_stride, a.shard_len));  // systematic rows
       tower_convert(T, CL, CH);  // the transforms run in tower coordinates
       with_gen<0, kSubMaxGen<KB>, false>(index, [&](auto gc) __attribute__((always_inline)) {
         constexpr int GEN = decltype(gc)::value;  // 0 only at index 0
@@ -373,7 +374,8 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
         cq_levels<kS, false, false, GEN>(T, VP, index, g, XL, XH);
         if constexpr (GEN >= 0) tower_convert(T, XL, XH);  // back to Cantor coordinates for the rows
       });
-      store_rows(out, a.shard_len, index + 16 * g, a.wanted_n, XL, XH, lane, ncols, full);
+      store_rows(out, a.shard_len, index + 16 * g, a.wanted_n, XL, XH, lane, ncols, full,
+                 rows_nt(a.shards, a.batch_stride, a.shard_len));
     }
   }
 }
@@ -479,7 +481,7 @@ __device__ __forceinline__ void tile_copy_out(const ReconstructArgs& a, const ui
                                               uint32_t col0, uint32_t ncols, uint32_t s) {
   using G = Geo<kS>;
   uint8_t* outp = a.out + static_cast<size_t>(pb) * a.out_stride + static_cast<size_t>(col0) * 2 * KB + 512u * s;
-  const bool al_o = ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 7u) == 0;
+  const bool al_o = NP_UNALIGNED || ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 7u) == 0;
   // opaque thread id, one output pointer stepped per column: otherwise the 16
   // per-lane 64-bit column addresses are hoisted out of the callers' loops and
   // spilled, and every reload waits (vmcnt(0)) for the stores before it
@@ -558,7 +560,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   uint8_t* scrD = scrY + (SUBS * NQ - 1) * kSegScr;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, g = uniform(tid >> 6);
   const bool full =
-      ncols == kTile && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
+      ncols == kTile && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
   const uint32_t cqb = col_base<kS>(4 * lane) ^ (32u * g);
   const uint32_t hb = col_base<kS>(tid / G::R) ^ (8u * (tid % G::R));
 

@@ -123,15 +123,14 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
   uint8_t* out = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(ch0);
   const uint32_t tid = threadIdx.x, lane = tid & 63u, g = uniform(tid >> 6);
   const bool full =
-      ncols == kTile && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
+      ncols == kTile && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
 
   // ---- tile load: thread tid moves blocks (c0 + 16 i, m0), i = 0..15
   {
     const uint32_t c0 = tid / G::Q, m0 = tid % G::Q;
     const uint32_t base = col_base<K>(c0) ^ (8u * m0);
     const size_t gbase = static_cast<size_t>(ch0 + c0) * 2 * K + 8u * m0;
-    const bool fast = ((reinterpret_cast<uintptr_t>(pay) & 7u) == 0) &&
-                      static_cast<size_t>(ch0 + kTile) * 2 * K <= a.payload_len;
+    const bool fast = out_vec_ok(pay, 0) && static_cast<size_t>(ch0 + kTile) * 2 * K <= a.payload_len;
     if (fast) {
       uint2 v[16];
 #pragma unroll
@@ -152,6 +151,7 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     }
   }
   const uint32_t nshift = a.n / K;
+  const bool nt = rows_nt(a.shards, a.batch_stride, a.shard_len);
   const uint32_t wanted_store = ((kExp & 2) && a.k != 12345u) ? 0u : a.wanted_n;  // experiment: no stores
   // n <= 4K: the tables of every transform stay staged (one buffer each, as
   // k_encode_multi: no table load inside the shift loop, where it would wait
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
   {
     uint32_t CL[16], CH[16];
     cq_read<K>(tile, cqb, CL, CH);
-    store_rows(out, a.shard_len, 16 * g, wanted_store, CL, CH, lane, ncols, full);
+    store_rows(out, a.shard_len, 16 * g, wanted_store, CL, CH, lane, ncols, full, nt);
     tower_convert(T, CL, CH);  // transforms run in tower coordinates
     cq_levels<K, true, true, 0>(T, VP, 0, g, CL, CH);
     if constexpr (kEncQx<K>) {
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
       cq_read_p<K>(tile, fresh_v(cqb), XL, XH);
     }
     shift_cq<K, SH>(T, vp, index, g, XL, XH);
-    store_rows(out, a.shard_len, index + 16 * g, wanted_store, XL, XH, lane, ncols, full);
+    store_rows(out, a.shard_len, index + 16 * g, wanted_store, XL, XH, lane, ncols, full, nt);
   };
   if (nshift > 1 && K < a.wanted_n) shift(Int<1>{}, 1);
   if (nshift > 2 && 2 * K < a.wanted_n) shift(Int<2>{}, 2);
@@ -306,7 +306,8 @@ __device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArg
     if constexpr (!(kExp & 4)) dma_tile<K>(dma_pay, dma_ch0, tile, g, lane);
   }
   shift_cq<K, SH>(T, vp, index, g, XL, XH);
-  store_rows(out, a.shard_len, index + 16 * g, (kExp & 2) ? 0u : a.wanted_n, XL, XH, lane, ncols, full);
+  store_rows(out, a.shard_len, index + 16 * g, (kExp & 2) ? 0u : a.wanted_n, XL, XH, lane, ncols, full,
+             rows_nt(a.shards, a.batch_stride, a.shard_len));
 }
 
 // One tile; returns whether the next tile's payload is on its way by DMA.
@@ -326,11 +327,14 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
   // (a VMEM op) waits with vmcnt(0) for the DMA and every row store before it
   const uint32_t tid = fresh_v(threadIdx.x), lane = tid & 63u, g = uniform(tid >> 6);
   const bool full =
-      ncols == kTile && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
+      ncols == kTile && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
+  // whole tiles load by 8-byte vector loads at any address; the LDS-DMA of the
+  // next tile's payload (4-byte pieces) only from 8-byte aligned payloads
   const bool aligned_pay = (reinterpret_cast<uintptr_t>(pay) & 7u) == 0;
-  auto tile_fast = [&](uint32_t t) __attribute__((always_inline)) {
-    return aligned_pay && static_cast<size_t>(t * kTile + kTile) * 2 * K <= a.payload_len;
+  auto tile_whole = [&](uint32_t t) __attribute__((always_inline)) {
+    return static_cast<size_t>(t * kTile + kTile) * 2 * K <= a.payload_len;
   };
+  auto tile_fast = [&](uint32_t t) __attribute__((always_inline)) { return aligned_pay && tile_whole(t); };
   if (have_dma) {
     // this wave's DMA pieces have landed; the previous tile's last 16 row
     // stores, issued after them, may still be in flight
@@ -342,7 +346,7 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
     const uint32_t c0 = tid / G::Q, m0 = tid % G::Q;
     const uint32_t base = col_base<K>(c0) ^ (8u * m0);
     const size_t gbase = static_cast<size_t>(ch0 + c0) * 2 * K + 8u * m0;
-    if (tile_fast(tl)) {
+    if (out_vec_ok(pay, 0) && tile_whole(tl)) {
       uint2 v[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i)
@@ -372,7 +376,8 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
   {
     uint32_t CL[16], CH[16];
     cq_read<K>(tile, cqb, CL, CH);
-    store_rows(out, a.shard_len, 16 * g, (kExp & 2) ? 0u : a.wanted_n, CL, CH, lane, ncols, full);
+    store_rows(out, a.shard_len, 16 * g, (kExp & 2) ? 0u : a.wanted_n, CL, CH, lane, ncols, full,
+               rows_nt(a.shards, a.batch_stride, a.shard_len));
     tower_convert(T, CL, CH);  // transforms run in tower coordinates
     cq_levels<K, true, true, 0>(T, VP, 0, g, CL, CH);
     if constexpr (kEncQx<K>) {
@@ -428,7 +433,7 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     // the previous tile's last shift stored 16 rows per wave (store_rows' full path)
     const uint32_t pch0 = (tl0 + t - 1) * kTile;
     const bool stored16 = t > 0 && pch0 + kTile <= lp->nchunks &&
-                          ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0 &&
+                          rows_vec_ok(a.shards, a.batch_stride, a.shard_len) &&
                           (min(a.n / K, (a.wanted_n + K - 1) / K) - 1) * K + 16 * 16 <= a.wanted_n &&
                           16 * a.shard_len < 0x7fffffffu;
     dma = encode_tile_multi<K>(T, a, smem, fresh(pb), fresh(tl0) + t, lp->nchunks, t == 0, dma, stored16,
@@ -841,7 +846,7 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
         });
   }
   stamp(dbg, 30);
-  if (full && ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 15u) == 0) {
+  if (full && out_vec_ok(a.out, a.out_stride)) {
     copy_out_cq<K>(a.out + static_cast<size_t>(pb) * a.out_stride + static_cast<size_t>(col0) * 2 * K, lane, g, XL, XH);
     stamp(dbg, 31);
     return;
@@ -852,7 +857,7 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
   // ---- copy-out: column c of the tile is 2K contiguous bytes of the output
   {
     uint8_t* out = a.out + static_cast<size_t>(pb) * a.out_stride + static_cast<size_t>(col0) * 2 * K;
-    const bool al_o = ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 7u) == 0;
+    const bool al_o = NP_UNALIGNED || ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 7u) == 0;
     const uint32_t c0 = tid / G::Q, m0 = tid % G::Q;
     const uint32_t base = col_base<K>(c0) ^ (8u * m0);
 #pragma unroll
@@ -902,7 +907,7 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
   uint8_t* tile = smem;
   uint32_t* VP = reinterpret_cast<uint32_t*>(smem + G::kTileBytes);  // 2 staged transforms
   const uint32_t tid0 = threadIdx.x, g0 = uniform(tid0 >> 6);
-  const bool aligned = ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
+  const bool aligned = rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
   const uint8_t* shp = a.shards + static_cast<size_t>(pb) * a.batch_stride;
 
   // presence bits of this wave's rows in every segment of the prefix (the
@@ -1026,7 +1031,7 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
                    nc == kTile && aligned);
       }
     }
-    if (full && ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 15u) == 0) {
+    if (full && out_vec_ok(a.out, a.out_stride)) {
       copy_out_cq<K>(a.out + static_cast<size_t>(pb) * a.out_stride + static_cast<size_t>(col0) * 2 * K, lane, g, XL,
                      XH);
       stamp(dbg, 31);
@@ -1038,7 +1043,7 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
     // ---- copy-out: column c of the tile is 2K contiguous bytes of the output
     {
       uint8_t* out = a.out + static_cast<size_t>(pb) * a.out_stride + static_cast<size_t>(col0) * 2 * K;
-      const bool al_o = ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 7u) == 0;
+      const bool al_o = NP_UNALIGNED || ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 7u) == 0;
       const uint32_t c0 = tid / G::Q, q0 = tid % G::Q;
       const uint32_t base = col_base<K>(c0) ^ (8u * q0);
 #pragma unroll
@@ -1099,7 +1104,7 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     const uint32_t ncols = min(static_cast<uint32_t>(kTile), nsyms - col0);
     const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);
     const bool full =
-        ncols == kTile && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
+        ncols == kTile && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
     uint64_t* dbg = (kExp & 64) ? reinterpret_cast<uint64_t*>(a.out + static_cast<size_t>(pb) * a.out_stride +
                                                                static_cast<size_t>(nsyms) * 2 * K + ((kExp & 128) ? 4096u : 256u) * tl0)
                                  : nullptr;

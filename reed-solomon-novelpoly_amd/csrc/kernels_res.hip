@@ -484,33 +484,6 @@ __device__ __forceinline__ void add_derivative_hd(uint32_t (&A)[16], uint32_t (&
 }
 
 // ------------------------------------------------------------ shard rows ----
-// A full tile's shard-row pieces move as 8-byte vector accesses, and the
-// decode's output as 16-byte ones, at any even (rows) / any (output) address:
-// the KFD runs gfx9 queues in unaligned-access mode (SH_MEM_CONFIG alignment
-// mode UNALIGNED; tools/microbench/unaligned.hip checks the bytes and the
-// rates), so odd or 2-mod-4 chunk counts -- rows 2- or 4-byte aligned, e.g.
-// the reference bench's 10 MB payloads at k = 512 -- keep the vector path
-// instead of per-symbol accesses.  The parity tests with odd chunk counts pin
-// it.  NP_RES_UNALIGNED=0 restores 8- / 16-byte alignment requirements.
-#ifndef NP_RES_UNALIGNED
-#define NP_RES_UNALIGNED 1
-#endif
-__device__ __forceinline__ bool rows_vec_ok(const void* p, size_t stride, size_t len) {
-  constexpr uintptr_t m = NP_RES_UNALIGNED ? 1u : 7u;
-  return ((reinterpret_cast<uintptr_t>(p) | stride | len) & m) == 0;
-}
-// Streaming row stores: 0 always, 1 for rows of whole 128-byte lines, 2 for
-// 8-byte aligned rows.
-#ifndef NP_RES_NT_MODE
-#define NP_RES_NT_MODE 1
-#endif
-__device__ __forceinline__ bool res_rows_nt(const void* p, size_t stride, size_t len) {
-  const uintptr_t v = reinterpret_cast<uintptr_t>(p) | stride | len;
-  return NP_RES_NT_MODE == 0 ? true : NP_RES_NT_MODE == 1 ? (v & 127u) == 0 : (v & 7u) == 0;
-}
-__device__ __forceinline__ bool out_vec_ok(const void* p, size_t stride) {
-  return NP_RES_UNALIGNED || ((reinterpret_cast<uintptr_t>(p) | stride) & 15u) == 0;
-}
 
 // This lane's 8 bytes (columns 4 cq .. 4 cq + 3) of shard rows
 // row0 + 64 w + 16 u + i, i = 0..15.  `out` = row 0, column 0 of the tile.
@@ -567,7 +540,7 @@ __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4))) void k_e
   const Res r = res_coords<K>();
   const bool full =
       ncols == kRC && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
-  const bool nt = res_rows_nt(a.shards, a.batch_stride, a.shard_len);
+  const bool nt = rows_nt(a.shards, a.batch_stride, a.shard_len);
   const uint32_t wanted_store = ((kExp & 2) && a.k != 12345u) ? 0u : a.wanted_n;  // experiment: no stores
 
   // ---- payload tile: thread t moves block m = t mod K/4 of columns t / (K/4) + 4 i

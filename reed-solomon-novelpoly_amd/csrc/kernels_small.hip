@@ -138,14 +138,18 @@ __device__ __forceinline__ void tower_convert_q(const DevTables& T, uint64_t (&Q
 // streaming stores as store_rows.
 template <int NR>
 __device__ __forceinline__ void store_rows_k(uint8_t* out, size_t shard_len, uint32_t row0, uint32_t wanted_n,
-                                             const uint64_t (&Q)[NR], uint32_t lane, uint32_t ncols, bool full) {
+                                             const uint64_t (&Q)[NR], uint32_t lane, uint32_t ncols, bool full,
+                                             bool nt) {
   if (full && row0 + NR <= wanted_n && NR * shard_len < 0x7fffffffu) {
     const __amdgpu_buffer_rsrc_t r = buf_rsrc(out + static_cast<size_t>(row0) * shard_len, NR * static_cast<uint32_t>(shard_len));
 #pragma unroll
     for (int p = 0; p < NR; ++p) {
       const uint2 v = cq_row(lo(Q[p]), hi(Q[p]));
-      __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, r, 8u * lane, static_cast<uint32_t>(p * shard_len),
-                                            NP_ROW_STORE_CPOL);
+      if (nt)
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, r, 8u * lane, static_cast<uint32_t>(p * shard_len),
+                                              NP_ROW_STORE_CPOL);
+      else
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, r, 8u * lane, static_cast<uint32_t>(p * shard_len), 0);
       __builtin_amdgcn_sched_barrier(0);  // one row at a time: no K rows of temporaries
     }
   } else {
@@ -229,13 +233,13 @@ __global__ __launch_bounds__(256) void k_encode_small(DevTables T, EncodeArgs a,
   const uint8_t* pay = a.payloads + static_cast<size_t>(pb) * a.payload_stride;
   uint8_t* out = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(ch0);
   const bool full =
-      ncols == kTile && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
+      ncols == kTile && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
 
   // ---- the lane's four columns: 2K contiguous payload bytes each
   uint64_t M[K];
   {
     const size_t c0 = static_cast<size_t>(ch0 + 4u * lane) * 2 * K;
-    const bool fast = ((reinterpret_cast<uintptr_t>(pay) & 15u) == 0) &&
+    const bool fast = out_vec_ok(pay, 0) &&  // 16-byte loads at any address (rows_vec_ok)
                       static_cast<size_t>(ch0 + kTile) * 2 * K <= a.payload_len;
     if (fast) {
 #pragma unroll
@@ -267,7 +271,7 @@ __global__ __launch_bounds__(256) void k_encode_small(DevTables T, EncodeArgs a,
       }
     }
   }
-  store_rows_k<K>(out, a.shard_len, 0, a.wanted_n, M, lane, ncols, full);
+  store_rows_k<K>(out, a.shard_len, 0, a.wanted_n, M, lane, ncols, full, rows_nt(a.shards, a.batch_stride, a.shard_len));
   tower_convert_q(T, M);  // the transforms run in tower coordinates
   reg_levels<K, true, true>(T, VP, 0, M);
 #pragma unroll
@@ -283,7 +287,7 @@ __global__ __launch_bounds__(256) void k_encode_small(DevTables T, EncodeArgs a,
     for (int p = 0; p < K; ++p) X[p] = M[p];
     reg_levels<K, false, false>(T, VP + s * G::kVPWords, index, X, uniform(rows));
     tower_convert_q(T, X);  // back to Cantor coordinates for the shard rows
-    store_rows_k<K>(out, a.shard_len, index, a.wanted_n, X, lane, ncols, full);
+    store_rows_k<K>(out, a.shard_len, index, a.wanted_n, X, lane, ncols, full, rows_nt(a.shards, a.batch_stride, a.shard_len));
   }
 }
 
@@ -323,7 +327,7 @@ __global__ __launch_bounds__(256) void k_reconstruct_small(DevTables T, Reconstr
   const uint32_t ncols = min(static_cast<uint32_t>(kTile), nsyms - col0);
   const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);
   const bool full =
-      ncols == kTile && ((reinterpret_cast<uintptr_t>(a.shards) | a.batch_stride | a.shard_len) & 7u) == 0;
+      ncols == kTile && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
   const uint32_t m0 = uniform(static_cast<uint32_t>(__ballot(lane < K && pres[lane] != 0)));
 
   uint64_t X[K];
@@ -402,8 +406,8 @@ __global__ __launch_bounds__(256) void k_reconstruct_small(DevTables T, Reconstr
   }
   // ---- copy-out: column c of the tile is 2K contiguous output bytes
   uint8_t* out = a.out + static_cast<size_t>(pb) * a.out_stride + static_cast<size_t>(col0) * 2 * K;
-  const bool al16 = full && ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 15u) == 0;
-  const bool al8 = ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 7u) == 0;
+  const bool al16 = full && out_vec_ok(a.out, a.out_stride);
+  const bool al8 = NP_UNALIGNED || ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 7u) == 0;
 #pragma unroll
   for (int u2 = 0; u2 < K / 8; ++u2) {
     uint2 d0[4], d1[4];
