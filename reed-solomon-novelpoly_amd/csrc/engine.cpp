@@ -190,10 +190,38 @@ size_t big_slots(const np_ctx* c, size_t tiles, uint32_t n, uint32_t k, bool rec
   return std::min((tiles + 7) / 8 * 8, np::big_resident_slots(c->device, n, k, reconstruct));
 }
 
+// k >= 4096 (and k = 2048 with NP_HUGE=1) on the sub-transform path of
+// kernels_huge.hip; NP_HUGE=0 keeps the big / generic kernels (A/B runs).
+bool huge_on(uint32_t k) {
+  static const int mode = [] {
+    const char* e = std::getenv("NP_HUGE");
+    return e ? (e[0] == '0' ? 0 : 2) : 1;
+  }();
+  return mode == 2 || (mode == 1 && k >= 4096);
+}
+
 // Caller holds the context lock.
 hipError_t launch_encode(np_ctx* c, const np::EncodeArgs& a, hipStream_t s) {
   if (np::fast_encode_supported(a.n, a.k)) return np::launch_encode_fast(c->T, a, s);
   if (np::res_encode_supported(a.n, a.k) && np::res_enabled()) return np::launch_encode_res(c->T, a, s);
+  const size_t huge_per = np::huge_encode_scratch_per_payload(a.shard_len, a.n, a.k);
+  if (np::huge_encode_supported(a.n, a.k) && huge_on(a.k) && huge_per <= kBigScratchCap) {
+    // slices of the batch whose tile slots fit the context scratch
+    const size_t per = std::max<size_t>(1, kBigScratchCap / std::max<size_t>(1, huge_per));
+    for (size_t b0 = 0; b0 < a.batch; b0 += per) {
+      np::EncodeArgs sub = a;
+      sub.batch = std::min(per, a.batch - b0);
+      sub.payloads = a.payloads + b0 * a.payload_stride;
+      sub.shards = a.shards + b0 * a.batch_stride;
+      uint8_t* scr = nullptr;
+      size_t bytes = 0;
+      hipError_t e = big_scratch(c, sub.batch * huge_per, s, &scr, &bytes);
+      if (e == hipSuccess) e = np::launch_encode_huge(c->T, sub, scr, s);
+      e = big_done(c, s, e);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
   if (np::big_encode_supported(a.n, a.k)) {
     const size_t tiles = ((a.payload_len + 2 * a.k - 1) / (2 * a.k) + 255) / 256;
     uint8_t* scr = nullptr;
@@ -242,6 +270,26 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
       if (e == hipSuccess) e = np::launch_prefix_locator(c->T, sub, scr, s);
       sub.prefix = scr;
       if (e == hipSuccess) e = res ? np::launch_reconstruct_res(c->T, sub, s) : np::launch_reconstruct_fast(c->T, sub, s);
+      e = big_done(c, s, e);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
+  const size_t huge_per = np::huge_reconstruct_scratch_per_payload(a.shard_len, a.n, a.k);
+  if (np::huge_reconstruct_supported(a.n, a.k) && huge_on(a.k) && huge_per <= kBigScratchCap / 2) {
+    // per payload: tile slots, mode byte, locators (unless the caller's), status
+    const size_t side = 16 + (a.locators ? 0 : 2 * static_cast<size_t>(a.n)) + own_status;
+    const size_t per = std::max<size_t>(1, kBigScratchCap / (huge_per + side));
+    for (size_t b0 = 0; b0 < a.batch; b0 += per) {
+      np::ReconstructArgs sub = slice(a, b0, std::min(per, a.batch - b0));
+      uint8_t* scr = nullptr;
+      size_t bytes = 0;
+      hipError_t e = big_scratch(c, sub.batch * (huge_per + side), s, &scr, &bytes);
+      uint8_t* side0 = scr + sub.batch * huge_per;  // huge_per is a multiple of 128 KiB
+      uint16_t* loc = reinterpret_cast<uint16_t*>(side0);
+      uint8_t* mode = side0 + (a.locators ? 0 : 2 * static_cast<size_t>(a.n) * sub.batch);
+      if (!a.status) sub.status = reinterpret_cast<uint32_t*>(mode + (sub.batch + 15) / 16 * 16);
+      if (e == hipSuccess) e = np::launch_reconstruct_huge(c->T, sub, scr, mode, loc, s);
       e = big_done(c, s, e);
       if (e != hipSuccess) return e;
     }
@@ -398,6 +446,7 @@ int np_ctx_create(int device, np_ctx** out) {
       if (e == hipSuccess) e = np::configure_fast_kernels();
       if (e == hipSuccess) e = np::configure_big_kernels();
       if (e == hipSuccess) e = np::configure_res_kernels();
+      if (e == hipSuccess) e = np::configure_huge_kernels();
       if (e == hipSuccess) g_configured_devices.push_back(device);
     }
   }
@@ -527,7 +576,7 @@ hipError_t pipe_sync(np_ctx* c, hipError_t e) {
 size_t rows_needed(const np_code_params* p, const uint8_t* present, size_t batch) {
   const uint32_t n = static_cast<uint32_t>(p->n), k = static_cast<uint32_t>(p->k);
   if (!np::fast_reconstruct_supported(n, k) && !np::res_reconstruct_supported(n, k) &&
-      !np::big_reconstruct_supported(n, k))
+      !np::big_reconstruct_supported(n, k) && !np::huge_reconstruct_supported(n, k))
     return p->n;
   for (size_t b = 0; b < batch; ++b) {
     const uint8_t* pr = present + b * p->n;

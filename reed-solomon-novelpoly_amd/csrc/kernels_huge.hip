@@ -1,0 +1,573 @@
+// k = 2048 .. 16384 (n = 4096 .. 65536; 8,193-65,536 validators): a size-k
+// transform as M = k / 1024 size-1024 sub-transforms in the resident layouts
+// of res_common.hpp plus its top log2(M) levels.
+//
+// For a size-k transform at index I (a multiple of k) and position
+// p = 1024 m + p' (sub-segment m):
+//  * a level b < 10 has the skew Cantor(2T + (I >> b)) of group T = p >> (b + 1)
+//    = (m << (9 - b)) + (p' >> (b + 1)), i.e. Cantor(2 (p' >> (b + 1)) +
+//    ((I + 1024 m) >> b)): the levels 0-9 on sub-segment m are the size-1024
+//    transform at index I + 1024 m (inc_afft.rs:139-214 / :267-332);
+//  * a level b = 10 + L >= 10 pairs sub-segments m and m + 2^L with the skew
+//    Cantor(2 (m >> (L + 1)) + (I >> b)), the same for every p', and in GF(2^8)
+//    ((I + k) >> 10 <= 64 for n <= 65536): a subfield multiply per quad.
+// So IFFT(k, I) = Top^-1_I o (IFFT(1024, I + 1024 m) per m) and FFT(k, I) =
+// (FFT(1024, I + 1024 m) per m) o Top_I.
+//
+// The sub-transforms hand their results to the top-level pass through a
+// scratch in thread order: slot s of a tile holds the HD registers of the
+// sub-transform's 1024 threads (quad j of thread t at (1024 j + t) * 8 bytes,
+// 128 KiB), so (j, t) names the same 4 positions of the same column in every
+// slot and the top-level pass runs per (j, t) with coalesced 8-byte accesses.
+//
+// Encode (mod.rs:144-154, inc_encode.rs:15-48), per batch slice:
+//   k_huge_enc_inv  per m: payload sub-tile -> systematic rows, IFFT(1024,
+//                   1024 m) -> slot m;
+//   k_huge_enc_top  per (j, t): Top^-1_0 over slots 0..M-1 -> coefficients,
+//                   then per shift s Top_{sk} -> slots s M + m;
+//   k_huge_enc_fwd  per (s, m): FFT(1024, sk + 1024 m) of slot s M + m -> shard
+//                   rows sk + 1024 m ...
+// Reconstruct (inc_reconstruct.rs:1-113, mod.rs:162-239; the fold of
+// kernels_fast.hip / DESIGN.md §4.3 with n = NQ k):
+//   k_huge_records  status and mode per payload (skip / copy / decode);
+//   locators        the generic 65536-point Walsh kernel (or the caller's);
+//   k_huge_rec_inv  per (q, m): premultiplied rows q k + 1024 m ..,
+//                   IFFT(1024, q k + 1024 m) -> slot q M + m; q = 0 also
+//                   D_1024 of it -> slot NQ M + m;
+//   k_huge_rec_top  per (j, t): x_q = Top^-1_{qk}, d = D_k(x_0) ^ sum kappa_q
+//                   x_q with D_k = (D_1024 lifted) ^ the high single-bit
+//                   terms x_0[m | 2^L] (kernels_big.hip's argument), then
+//                   Top_0 -> slots 0..M-1;
+//   k_huge_rec_fwd  per m: FFT(1024, 1024 m) of slot m, postmultiply of the
+//                   erased rows, merge with the received ones, copy-out.
+#include "res_common.hpp"
+
+namespace np {
+namespace {
+
+constexpr int kSK = 1024;                             // sub-transform size
+constexpr uint32_t kSlotBytes = 16u * 1024u * 8u;     // one sub-segment of a tile in thread order
+constexpr uint32_t kHDS = RGeo<kSK>::kHD;
+
+struct HugeArgs {
+  uint8_t* scr;         // tile slots of the slice: tile (pb, tl) at (pb tiles + tl) slots kSlotBytes
+  const uint16_t* loc;  // reconstruct: locators, batch x n (log form)
+  const uint8_t* mode;  // reconstruct: per payload kHugeSkip / kHugeCopy / kHugeDecode
+  uint32_t tiles, slots, M, K, NQ;
+  uint32_t m, q;        // this launch's sub-segment and segment (reconstruct) / shift (encode)
+};
+constexpr uint8_t kHugeSkip = 0, kHugeCopy = 1, kHugeDecode = 2;
+
+__device__ __forceinline__ uint8_t* slot_at(const HugeArgs& h, uint32_t pb, uint32_t tl, uint32_t slot) {
+  return h.scr + (static_cast<size_t>(pb) * h.tiles + tl) * h.slots * kSlotBytes + static_cast<size_t>(slot) * kSlotBytes;
+}
+__device__ __forceinline__ void slot_store(uint8_t* s, uint32_t tid, const uint32_t (&L)[16], const uint32_t (&H)[16]) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) *reinterpret_cast<uint2*>(s + (1024u * j + tid) * 8u) = make_uint2(L[j], H[j]);
+}
+__device__ __forceinline__ void slot_load(const uint8_t* s, uint32_t tid, uint32_t (&L)[16], uint32_t (&H)[16]) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint2 v = *reinterpret_cast<const uint2*>(s + (1024u * j + tid) * 8u);
+    L[j] = v.x;
+    H[j] = v.y;
+  }
+}
+
+// ---------------------------------------------------------- top levels ----
+// x ^= c y for one quad, c < 256 a Cantor index (subfield, tower coordinates).
+__device__ __forceinline__ void top_mul(const DevTables& T, uint32_t c, uint2& x, const uint2& y) {
+  uint32_t p[20];
+  pool_of<true>(T, c, p);
+  const Mult mm = make_mult(p);
+  qmul_sub(x.x, x.y, y.x, y.y, mm);
+}
+
+// Levels 10 .. 10 + log2(M) - 1 of a size-1024 M transform at index I over the
+// sub-segment quads y[m].  Inverse (ascending levels): hi ^= lo; lo ^= c hi.
+template <int M>
+__device__ __forceinline__ void top_inverse_h(const DevTables& T, uint2 (&y)[M], uint32_t I) {
+#pragma unroll
+  for (int L = 0; (1 << L) < M; ++L) {
+#pragma unroll
+    for (int g = 0; g < (M >> (L + 1)); ++g) {
+      const uint32_t c = uniform(2u * g + (I >> (10 + L)));
+#pragma unroll
+      for (int v = 0; v < (1 << L); ++v) {
+        const int lo = g * (2 << L) + v, hi = lo + (1 << L);
+        y[hi].x ^= y[lo].x;
+        y[hi].y ^= y[lo].y;
+        top_mul(T, c, y[lo], y[hi]);
+      }
+    }
+  }
+}
+// Forward (descending levels): lo ^= c hi; hi ^= lo.
+template <int M>
+__device__ __forceinline__ void top_forward_h(const DevTables& T, uint2 (&y)[M], uint32_t I) {
+#pragma unroll
+  for (int L = ilog2(M) - 1; L >= 0; --L) {
+#pragma unroll
+    for (int g = 0; g < (M >> (L + 1)); ++g) {
+      const uint32_t c = uniform(2u * g + (I >> (10 + L)));
+#pragma unroll
+      for (int v = 0; v < (1 << L); ++v) {
+        const int lo = g * (2 << L) + v, hi = lo + (1 << L);
+        top_mul(T, c, y[lo], y[hi]);
+        y[hi].x ^= y[lo].x;
+        y[hi].y ^= y[lo].y;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- encode ----
+template <int GEN>
+__global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k_huge_enc_inv(
+    DevTables T, EncodeArgs a, HugeArgs h, uint32_t nchunks) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* tile = smem;
+  const TileRef tr = tile_of(blockIdx.x, h.tiles, (a.batch & 7u) == 0);
+  const uint32_t pb = tr.pb, tl = tr.tl, ch0 = tl * kRC;
+  const uint32_t ncols = min(static_cast<uint32_t>(kRC), nchunks - ch0);
+  const uint32_t I = uniform(kSK * h.m);
+  const Res r = res_coords<kSK>();
+  const bool full = ncols == kRC && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
+  const bool nt = rows_nt(a.shards, a.batch_stride, a.shard_len);
+  load_pay_tile<kSK>(tile, a.payloads + static_cast<size_t>(pb) * a.payload_stride, a.payload_len, ch0,
+                     2 * static_cast<size_t>(h.K), 2 * static_cast<size_t>(I), r.tid);
+  __syncthreads();
+  uint32_t L[16], H[16];
+  rcq_read_nat<kSK>(tile, r.cqb, L, H);
+  rres_store_rows(a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(ch0), a.shard_len, I,
+                  a.wanted_n, L, H, r, ncols, full, nt);
+  tower_convert(T, L, H);
+  rcq_levels<true, GEN>(T, I, r, L, H);
+  __syncthreads();  // every wave has read its payload blocks
+  rcq_write<kSK>(tile, fresh_v(r.cqb), L, H);
+  __syncthreads();
+  rh_read<kHA>(tile, fresh_v(r.hab), L, H);
+  ha_levels<true, GEN>(T, I, r, L, H);
+  __syncthreads();
+  rh_write<kHA>(tile, fresh_v(r.hab), L, H);
+  __syncthreads();
+  rh_read<kHDS>(tile, fresh_v(r.hdb), L, H);
+  hd_levels<kSK, true>(T, I, L, H);
+  slot_store(slot_at(h, pb, tl, h.m), r.tid, L, H);
+}
+
+// Thread (tile, j, t): the coefficients of its quads, then every shift's
+// top-level outputs W_s (only sub-segments with wanted rows).
+template <int M>
+__global__ __launch_bounds__(256) void k_huge_enc_top(DevTables T, HugeArgs h, uint32_t nshift, uint32_t wanted_n,
+                                                      size_t units) {
+  const size_t gid = static_cast<size_t>(blockIdx.x) * 256u + threadIdx.x;
+  if (gid >= units) return;
+  uint8_t* base = h.scr + (gid >> 14) * h.slots * kSlotBytes + (gid & 16383u) * 8u;
+  uint2 c[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) c[m] = *reinterpret_cast<const uint2*>(base + m * static_cast<size_t>(kSlotBytes));
+  top_inverse_h<M>(T, c, 0u);
+#pragma unroll 1
+  for (uint32_t s = 1; s < nshift && s * h.K < wanted_n; ++s) {
+    uint2 w[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) w[m] = c[m];
+    top_forward_h<M>(T, w, uniform(s * h.K));
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+      if (s * h.K + kSK * m < wanted_n)
+        *reinterpret_cast<uint2*>(base + (s * M + m) * static_cast<size_t>(kSlotBytes)) = w[m];
+  }
+}
+
+template <int GEN>
+__global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k_huge_enc_fwd(
+    DevTables T, EncodeArgs a, HugeArgs h, uint32_t nchunks) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* tile = smem;
+  const TileRef tr = tile_of(blockIdx.x, h.tiles, (a.batch & 7u) == 0);
+  const uint32_t pb = tr.pb, tl = tr.tl, ch0 = tl * kRC;
+  const uint32_t ncols = min(static_cast<uint32_t>(kRC), nchunks - ch0);
+  const uint32_t I = uniform(h.q * h.K + kSK * h.m);
+  const Res r = res_coords<kSK>();
+  const bool full = ncols == kRC && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
+  const bool nt = rows_nt(a.shards, a.batch_stride, a.shard_len);
+  uint32_t L[16], H[16];
+  slot_load(slot_at(h, pb, tl, h.q * h.M + h.m), r.tid, L, H);
+  hd_levels<kSK, false>(T, I, L, H);
+  rh_write<kHDS>(tile, fresh_v(r.hdb), L, H);
+  __syncthreads();
+  rh_read<kHA>(tile, fresh_v(r.hab), L, H);
+  ha_levels<false, GEN>(T, I, r, L, H);
+  __syncthreads();
+  rh_write<kHA>(tile, fresh_v(r.hab), L, H);
+  __syncthreads();
+  rcq_read<kSK>(tile, fresh_v(r.cqb), L, H);
+  rcq_levels<false, GEN>(T, I, r, L, H);
+  tower_convert(T, L, H);  // back to Cantor coordinates for the shard rows
+  rres_store_rows(a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(ch0), a.shard_len, I,
+                  a.wanted_n, L, H, r, ncols, full, nt);
+}
+
+// ----------------------------------------------------------- reconstruct ----
+// Status (mod.rs:178-180) and mode of each payload: fewer than k present rows:
+// skip; all k systematic rows present: their copy (inc_reconstruct.rs:46-50);
+// else the full decode from every present row.
+__global__ __launch_bounds__(256) void k_huge_records(ReconstructArgs a, uint8_t* mode) {
+  const uint32_t pb = blockIdx.x;
+  const uint8_t* pres = a.present + static_cast<size_t>(pb) * a.n;
+  int have1 = 0, have = 0;
+  for (uint32_t r = 0; r < a.n; r += 256) {
+    const uint32_t v = r + threadIdx.x;
+    const bool p = pres[v] != 0;  // n is a multiple of 256
+    if (r < a.k) have1 += __syncthreads_count(p);
+    have += __syncthreads_count(p);
+  }
+  const bool ok = have >= static_cast<int>(a.k);
+  if (threadIdx.x == 0) {
+    if (a.status) {
+      a.status[2 * pb] = ok ? 0u : kStatusNeedMoreShards;
+      a.status[2 * pb + 1] = static_cast<uint32_t>(have);
+    }
+    mode[pb] = !ok ? kHugeSkip : have1 == static_cast<int>(a.k) ? kHugeCopy : kHugeDecode;
+  }
+}
+
+template <int GEN>
+__global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k_huge_rec_inv(
+    DevTables T, ReconstructArgs a, HugeArgs h, uint32_t nsyms) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* tile = smem;
+  const TileRef tr = tile_of(blockIdx.x, h.tiles, (a.batch & 7u) == 0);
+  const uint32_t pb = tr.pb, tl = tr.tl;
+  if (uniform(h.mode[pb]) != kHugeDecode) return;
+  const uint32_t col0 = tl * kRC, ncols = min(static_cast<uint32_t>(kRC), nsyms - col0);
+  const uint32_t I = uniform(h.q * h.K + kSK * h.m);  // the segment's rows I .. I + 1023
+  const uint8_t* pres = a.present + static_cast<size_t>(pb) * a.n;
+  const uint16_t* loc = h.loc + static_cast<size_t>(pb) * a.n;
+  const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);
+  const bool full = ncols == kRC && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
+  const Res r = res_coords<kSK>();
+  uint32_t XL[16], XH[16];
+  {
+    const uint32_t pm = lane_rows_present(pres, I, r);
+    uint2 raw[8];
+    load_lane_rows<8>(raw, sh, a.shard_len, I, pm, r, ncols, full, T.zeros, 0);
+    stage_row_tables_loc(tile, T, loc, pres, I, r.tid, false);
+    __syncthreads();
+    // premultiply (inc_reconstruct.rs:72-74; Cantor in, tower out), two halves
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      if (half == 1) load_lane_rows<8>(raw, sh, a.shard_len, I, pm, r, ncols, full, T.zeros, 8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        uint32_t l, hh;
+        blk_to_quad(raw[i], l, hh);
+        const FullT m = row_table(tile, 64u * r.w + 16u * r.u + 8 * half + i);
+        qmul_set_vv(XL[8 * half + i], XH[8 * half + i], l, hh, m);
+      }
+    }
+  }
+  rcq_levels<true, GEN>(T, I, r, XL, XH);
+  __syncthreads();  // every wave has read its row tables
+  rcq_write<kSK>(tile, fresh_v(r.cqb), XL, XH);
+  __syncthreads();
+  rh_read<kHA>(tile, fresh_v(r.hab), XL, XH);
+  ha_levels<true, GEN>(T, I, r, XL, XH);
+  __syncthreads();
+  rh_write<kHA>(tile, fresh_v(r.hab), XL, XH);
+  __syncthreads();
+  rh_read<kHDS>(tile, fresh_v(r.hdb), XL, XH);
+  hd_levels<kSK, true>(T, I, XL, XH);
+  slot_store(slot_at(h, pb, tl, h.q * h.M + h.m), r.tid, XL, XH);
+  if (h.q == 0) {  // z = D_1024 of segment 0's sub-transform (the lifted low part of D_k)
+    uint32_t AL[16], AH[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) AL[j] = AH[j] = 0;
+    add_derivative_hd<kSK>(AL, XL, r.l);
+    add_derivative_hd<kSK>(AH, XH, r.l);
+    slot_store(slot_at(h, pb, tl, h.NQ * h.M + h.m), r.tid, AL, AH);
+  }
+}
+
+// Fold coefficients kappa_q (Cantor coordinates, kernels_fast.hip):
+// NQ = 2: (1, 1); NQ = 4: (0, 1, 1 + beta, beta), beta = Cantor(2); NQ = 8:
+// rec8_kappa.
+template <int NQ>
+__host__ __device__ constexpr uint32_t huge_kappa(int q) {
+  return NQ == 2 ? 1u : NQ == 4 ? (q == 0 ? 0u : q == 1 ? 1u : q == 2 ? 3u : 2u) : rec8_kappa_res(q);
+}
+
+template <int M, int NQ>
+__global__ __launch_bounds__(256) void k_huge_rec_top(DevTables T, HugeArgs h, size_t units) {
+  const size_t gid = static_cast<size_t>(blockIdx.x) * 256u + threadIdx.x;
+  if (gid >= units) return;
+  const size_t pt = gid >> 14;  // tile of the slice
+  if (uniform(h.mode[pt / h.tiles]) != kHugeDecode) return;
+  uint8_t* base = h.scr + pt * h.slots * kSlotBytes + (gid & 16383u) * 8u;
+  auto at = [&](uint32_t slot) __attribute__((always_inline)) { return base + static_cast<size_t>(slot) * kSlotBytes; };
+  uint2 d[M], x[M];
+  // x_0 and the lifted D_1024(y_0)
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    x[m] = *reinterpret_cast<const uint2*>(at(m));
+    d[m] = *reinterpret_cast<const uint2*>(at(NQ * M + m));
+  }
+  top_inverse_h<M>(T, x, 0u);
+  top_inverse_h<M>(T, d, 0u);
+  // D_k's high single-bit terms: position 1024 m + p' takes x_0 at 1024 (m | 2^L) + p'
+#pragma unroll
+  for (int m = 0; m < M; ++m)
+#pragma unroll
+    for (int L = 0; (1 << L) < M; ++L)
+      if (!(m & (1 << L))) {
+        d[m].x ^= x[m | (1 << L)].x;
+        d[m].y ^= x[m | (1 << L)].y;
+      }
+  if constexpr (huge_kappa<NQ>(0) == 1u) {
+#pragma unroll
+    for (int m = 0; m < M; ++m) d[m].x ^= x[m].x, d[m].y ^= x[m].y;
+  }
+#pragma unroll
+  for (int q = 1; q < NQ; ++q) {
+#pragma unroll
+    for (int m = 0; m < M; ++m) x[m] = *reinterpret_cast<const uint2*>(at(q * M + m));
+    top_inverse_h<M>(T, x, uniform(q * h.K));
+    const uint32_t kq = huge_kappa<NQ>(q);
+    if (kq == 1u) {
+#pragma unroll
+      for (int m = 0; m < M; ++m) d[m].x ^= x[m].x, d[m].y ^= x[m].y;
+    } else {
+#pragma unroll
+      for (int m = 0; m < M; ++m) top_mul(T, kq, d[m], x[m]);
+    }
+  }
+  top_forward_h<M>(T, d, 0u);
+#pragma unroll
+  for (int m = 0; m < M; ++m) *reinterpret_cast<uint2*>(at(m)) = d[m];
+}
+
+template <int GEN>
+__global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k_huge_rec_fwd(
+    DevTables T, ReconstructArgs a, HugeArgs h, uint32_t nsyms) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* tile = smem;
+  const TileRef tr = tile_of(blockIdx.x, h.tiles, (a.batch & 7u) == 0);
+  const uint32_t pb = tr.pb, tl = tr.tl;
+  const uint32_t mode = uniform(h.mode[pb]);
+  if (mode == kHugeSkip) return;
+  const uint32_t col0 = tl * kRC, ncols = min(static_cast<uint32_t>(kRC), nsyms - col0);
+  const uint32_t I = uniform(kSK * h.m);  // output rows I .. I + 1023
+  const uint8_t* pres = a.present + static_cast<size_t>(pb) * a.n;
+  const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);
+  const bool full = ncols == kRC && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
+  const bool out16 = out_vec_ok(a.out, a.out_stride);
+  const Res r = res_coords<kSK>();
+  uint32_t AL[16], AH[16];
+  if (mode == kHugeDecode) {
+    slot_load(slot_at(h, pb, tl, h.m), r.tid, AL, AH);
+    hd_levels<kSK, false>(T, I, AL, AH);
+    rh_write<kHDS>(tile, fresh_v(r.hdb), AL, AH);
+    __syncthreads();
+    rh_read<kHA>(tile, fresh_v(r.hab), AL, AH);
+    ha_levels<false, GEN>(T, I, r, AL, AH);
+    __syncthreads();
+    rh_write<kHA>(tile, fresh_v(r.hab), AL, AH);
+    __syncthreads();
+    rcq_read<kSK>(tile, fresh_v(r.cqb), AL, AH);
+    rcq_levels<false, GEN>(T, I, r, AL, AH);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) AL[j] = AH[j] = 0;
+  }
+  // merge: received systematic rows, postmultiplied recovered ones
+  // (inc_reconstruct.rs:46-50, :82-84; tower in, Cantor out)
+  const uint32_t pm = lane_rows_present(pres, I, r);
+  uint2 raw[16];
+  load_lane_rows(raw, sh, a.shard_len, I, pm, r, ncols, full, T.zeros);
+  __syncthreads();  // every wave has read the tile
+  if (mode == kHugeDecode) stage_row_tables_loc(tile, T, h.loc + static_cast<size_t>(pb) * a.n, pres, I, r.tid, true);
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    uint32_t l, hh;
+    if ((pm >> i) & 1u) {
+      blk_to_quad(raw[i], l, hh);
+    } else {
+      const FullT m = row_table(tile, 64u * r.w + 16u * r.u + i);
+      qmul_set_vv(l, hh, AL[i], AH[i], m);
+    }
+    AL[i] = l;
+    AH[i] = hh;
+  }
+  res_copy_out<kSK>(a.out + static_cast<size_t>(pb) * a.out_stride + static_cast<size_t>(col0) * 2 * h.K + 2 * I, AL, AH,
+                    r, ncols, out16, 2 * static_cast<size_t>(h.K));
+}
+
+// ------------------------------------------------------------ dispatch ----
+// f(Int<GEN>) for GEN = res_gen<1024>(I) of a sub-transform index I < 65536.
+template <typename F>
+hipError_t with_sub_gen(uint32_t I, F&& f) {
+  switch (res_gen<kSK>(I)) {
+    case 2: return f(Int<2>{});
+    case 3: return f(Int<3>{});
+    case 4: return f(Int<4>{});
+    case 5: return f(Int<5>{});
+    case 6: return f(Int<6>{});
+    case 7: return f(Int<7>{});
+    case 8: return f(Int<8>{});
+    default: return hipErrorInvalidValue;
+  }
+}
+template <typename F>
+hipError_t with_m(uint32_t M, F&& f) {
+  switch (M) {
+    case 2: return f(Int<2>{});
+    case 4: return f(Int<4>{});
+    case 8: return f(Int<8>{});
+    case 16: return f(Int<16>{});
+    default: return hipErrorInvalidValue;
+  }
+}
+template <typename F>
+hipError_t with_nq(uint32_t NQ, F&& f) {
+  switch (NQ) {
+    case 2: return f(Int<2>{});
+    case 4: return f(Int<4>{});
+    case 8: return f(Int<8>{});
+    default: return hipErrorInvalidValue;
+  }
+}
+
+HugeArgs huge_args(uint8_t* scr, uint32_t n, uint32_t k, size_t tiles, uint32_t slots) {
+  HugeArgs h{};
+  h.scr = scr;
+  h.tiles = static_cast<uint32_t>(tiles);
+  h.slots = slots;
+  h.K = k;
+  h.M = k / kSK;
+  h.NQ = n / k;
+  return h;
+}
+
+}  // namespace
+
+bool huge_encode_supported(uint32_t n, uint32_t k) { return k >= 2048 && k <= 16384 && n >= 2 * k && n <= 65536; }
+bool huge_reconstruct_supported(uint32_t n, uint32_t k) {
+  return k >= 2048 && k <= 16384 && (n == 2 * k || n == 4 * k || n == 8 * k) && n <= 65536;
+}
+size_t huge_encode_scratch_per_payload(size_t shard_len, uint32_t n, uint32_t k) {
+  (void)k;
+  const size_t tiles = (shard_len / 2 + kRC - 1) / kRC;
+  return tiles * (n / kSK) * static_cast<size_t>(kSlotBytes);
+}
+size_t huge_reconstruct_scratch_per_payload(size_t shard_len, uint32_t n, uint32_t k) {
+  const size_t tiles = (shard_len / 2 + kRC - 1) / kRC;
+  return tiles * ((n + k) / kSK) * static_cast<size_t>(kSlotBytes);
+}
+
+hipError_t launch_encode_huge(const DevTables& T, const EncodeArgs& a, uint8_t* scratch, hipStream_t s) {
+  if (!huge_encode_supported(a.n, a.k)) return hipErrorInvalidValue;
+  const size_t nchunks = (a.payload_len + 2 * a.k - 1) / (2 * a.k);
+  if (nchunks == 0 || a.batch == 0) return hipSuccess;
+  if (nchunks > 0xffffffffu) return hipErrorInvalidValue;
+  const size_t tiles = (nchunks + kRC - 1) / kRC;
+  const size_t blocks = a.batch * tiles;
+  if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
+  const uint32_t nb = static_cast<uint32_t>(blocks), nc = static_cast<uint32_t>(nchunks);
+  HugeArgs h = huge_args(scratch, a.n, a.k, tiles, a.n / kSK);
+  hipError_t e = hipSuccess;
+  for (uint32_t m = 0; m < h.M && e == hipSuccess; ++m) {
+    h.m = m;
+    e = with_sub_gen(kSK * m, [&](auto g) {
+      k_huge_enc_inv<decltype(g)::value><<<nb, kSK, RGeo<kSK>::kTileBytes, s>>>(T, a, h, nc);
+      return hipGetLastError();
+    });
+  }
+  const size_t units = blocks * 16 * kSK;
+  if (e == hipSuccess)
+    e = with_m(h.M, [&](auto mc) {
+      k_huge_enc_top<decltype(mc)::value><<<static_cast<uint32_t>(units / 256), 256, 0, s>>>(T, h, h.NQ, a.wanted_n, units);
+      return hipGetLastError();
+    });
+  for (uint32_t sh = 1; sh < h.NQ && e == hipSuccess; ++sh)
+    for (uint32_t m = 0; m < h.M && e == hipSuccess && sh * a.k + kSK * m < a.wanted_n; ++m) {
+      h.q = sh;
+      h.m = m;
+      e = with_sub_gen(sh * a.k + kSK * m, [&](auto g) {
+        k_huge_enc_fwd<decltype(g)::value><<<nb, kSK, RGeo<kSK>::kTileBytes, s>>>(T, a, h, nc);
+        return hipGetLastError();
+      });
+    }
+  return e;
+}
+
+hipError_t launch_reconstruct_huge(const DevTables& T, const ReconstructArgs& a, uint8_t* scratch, uint8_t* mode,
+                                   uint16_t* locators, hipStream_t s) {
+  if (!huge_reconstruct_supported(a.n, a.k)) return hipErrorInvalidValue;
+  const size_t nsyms = a.shard_len / 2;
+  if (a.batch == 0) return hipSuccess;
+  if (a.batch > 0x7fffffffu || nsyms > 0xffffffffu) return hipErrorInvalidValue;
+  k_huge_records<<<static_cast<uint32_t>(a.batch), 256, 0, s>>>(a, mode);
+  hipError_t e = hipGetLastError();
+  if (nsyms == 0 || e != hipSuccess) return e;
+  const uint16_t* loc = a.locators;
+  if (!loc) {
+    e = launch_error_locator(T, a.n, a.present, a.batch, locators, s);
+    loc = locators;
+  }
+  const size_t tiles = (nsyms + kRC - 1) / kRC;
+  const size_t blocks = a.batch * tiles;
+  if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
+  const uint32_t nb = static_cast<uint32_t>(blocks), ns = static_cast<uint32_t>(nsyms);
+  HugeArgs h = huge_args(scratch, a.n, a.k, tiles, (a.n + a.k) / kSK);
+  h.loc = loc;
+  h.mode = mode;
+  for (uint32_t q = 0; q < h.NQ && e == hipSuccess; ++q)
+    for (uint32_t m = 0; m < h.M && e == hipSuccess; ++m) {
+      h.q = q;
+      h.m = m;
+      e = with_sub_gen(q * a.k + kSK * m, [&](auto g) {
+        k_huge_rec_inv<decltype(g)::value><<<nb, kSK, RGeo<kSK>::kTileBytes, s>>>(T, a, h, ns);
+        return hipGetLastError();
+      });
+    }
+  const size_t units = blocks * 16 * kSK;
+  if (e == hipSuccess)
+    e = with_m(h.M, [&](auto mc) {
+      return with_nq(h.NQ, [&](auto qc) {
+        k_huge_rec_top<decltype(mc)::value, decltype(qc)::value>
+            <<<static_cast<uint32_t>(units / 256), 256, 0, s>>>(T, h, units);
+        return hipGetLastError();
+      });
+    });
+  for (uint32_t m = 0; m < h.M && e == hipSuccess; ++m) {
+    h.m = m;
+    e = with_sub_gen(kSK * m, [&](auto g) {
+      k_huge_rec_fwd<decltype(g)::value><<<nb, kSK, RGeo<kSK>::kTileBytes, s>>>(T, a, h, ns);
+      return hipGetLastError();
+    });
+  }
+  return e;
+}
+
+hipError_t configure_huge_kernels() {
+  hipError_t e = hipSuccess;
+  auto set = [&](const void* f) {
+    const hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(RGeo<kSK>::kTileBytes));
+    if (r != hipSuccess && e == hipSuccess) e = r;
+  };
+  for (uint32_t g = 2; g <= 8; ++g)
+    (void)with_sub_gen((256u << g) - 1024u, [&](auto gc) {
+      constexpr int G = decltype(gc)::value;
+      set(reinterpret_cast<const void*>(&k_huge_enc_inv<G>));
+      set(reinterpret_cast<const void*>(&k_huge_enc_fwd<G>));
+      set(reinterpret_cast<const void*>(&k_huge_rec_inv<G>));
+      set(reinterpret_cast<const void*>(&k_huge_rec_fwd<G>));
+      return hipSuccess;
+    });
+  return e;
+}
+
+}  // namespace np

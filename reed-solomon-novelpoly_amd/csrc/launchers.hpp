@@ -134,4 +134,17 @@ bool res_reconstruct_supported(uint32_t n, uint32_t k);
 hipError_t launch_encode_res(const DevTables& T, const EncodeArgs& a, hipStream_t s);
 hipError_t launch_reconstruct_res(const DevTables& T, const ReconstructArgs& a, hipStream_t s);
 hipError_t configure_res_kernels();
+
+// ---- k = 2048 .. 16384 (kernels_huge.hip): M = k / 1024 resident size-1024
+// sub-transforms plus the top levels, through per-tile scratch slots of
+// 128 KiB (scratch_per_payload bytes per payload of the slice). ----
+bool huge_encode_supported(uint32_t n, uint32_t k);       // n >= 2k, n <= 65536
+bool huge_reconstruct_supported(uint32_t n, uint32_t k);  // n / k in {2, 4, 8}
+size_t huge_encode_scratch_per_payload(size_t shard_len, uint32_t n, uint32_t k);
+size_t huge_reconstruct_scratch_per_payload(size_t shard_len, uint32_t n, uint32_t k);
+hipError_t launch_encode_huge(const DevTables& T, const EncodeArgs& a, uint8_t* scratch, hipStream_t s);
+// mode: batch bytes; locators: batch x n u16 (unused when a.locators is set)
+hipError_t launch_reconstruct_huge(const DevTables& T, const ReconstructArgs& a, uint8_t* scratch, uint8_t* mode,
+                                   uint16_t* locators, hipStream_t s);
+hipError_t configure_huge_kernels();
 }  // namespace np

@@ -1,0 +1,58 @@
+"""k = 2048 .. 16384 as size-1024 sub-transforms plus top levels
+(kernels_huge.hip; more than 12,288 validators: n = 16384 .. 65536): encode
+and reconstruct bit-exact against the oracle over every n / k the crate
+derives there, full and partial 64-column tiles, odd payload tails, wanted_n
+< n, random / worst-case / no erasures.  Reference: inc_encode.rs:15-48,
+inc_reconstruct.rs:1-113, mod.rs:43-61 / :117-239."""
+import numpy as np
+import pytest
+
+import novelpoly_amd as npa
+from novelpoly_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+# (n_wanted, k_wanted, payload bytes): n16384 k4096 (NQ 4), n32768 k4096 (8),
+# n32768 k8192 (4), n65536 k8192 (8), n65536 k16384 (4); tiles of 64 columns
+ENC = [(16384, 5462, 2 * 4096 * 64), (16384, 5462, 2 * 4096 * 70 + 3), (12289, 4097, 2 * 4096 * 3 + 1),
+       (20000, 6667, 2 * 4096 * 65), (24000, 8000, 999), (30000, 10000, 2 * 8192 * 64 + 5),
+       (32768, 10923, 2 * 8192 * 2), (40000, 13334, 2 * 8192 * 66), (65536, 21846, 2 * 16384 * 65 + 7),
+       (50000, 16667, 2 * 16384 * 3)]
+
+
+@pytest.mark.parametrize("nw,kw,plen", ENC)
+def test_huge_encode(gpu, oracle, nw, kw, plen):
+    p = npa.CodeParams.derive_parameters(nw, kw)
+    assert p.k() >= 4096
+    pl = synth.payload(nw + plen, plen)
+    got = p.make_encoder(gpu).encode(pl)
+    st, want = oracle.encode(pl, p.n(), p.k(), nw)
+    assert st == 0
+    bad = [v for v in range(nw) if got[v] != want[v]]
+    assert not bad, f"{len(bad)} shards differ, first {bad[:5]}"
+
+
+# erase: number of random erasures; -1: every systematic shard lost; 0: none (copy)
+REC = [(16384, 5462, 2 * 4096 * 64, 8000), (16384, 5462, 2 * 4096 * 70 + 3, -1), (20000, 6667, 2 * 4096 * 65, 13333),
+       (20000, 6667, 2 * 4096 * 2, 0), (30000, 10000, 2 * 8192 * 64 + 5, 20000), (30000, 10000, 2 * 8192 * 3, -1),
+       (40000, 13334, 2 * 8192 * 66, 26666), (65536, 21846, 2 * 16384 * 65 + 7, 43690),
+       (65536, 21846, 2 * 16384 * 2, -1)]
+
+
+@pytest.mark.parametrize("nw,kw,plen,erase", REC)
+def test_huge_reconstruct(gpu, oracle, nw, kw, plen, erase):
+    p = npa.CodeParams.derive_parameters(nw, kw)
+    n, k = p.n(), p.k()
+    assert k >= 4096 and n in (2 * k, 4 * k, 8 * k)
+    pl = synth.payload(3 * nw + plen, plen)
+    shards = p.make_encoder(gpu).encode(pl)
+    if erase == -1:
+        gone = set(range(k))
+    else:
+        gone = set(synth.erasure_indices(plen + erase, nw, min(erase, nw - k)).tolist())
+    recv = [None if i in gone else s for i, s in enumerate(shards[:nw])]
+    assert sum(r is not None for r in recv) >= k
+    got = p.make_encoder(gpu).reconstruct(recv)
+    st, want = oracle.reconstruct(recv, n, k)
+    assert st == 0 and got == want
+    assert got[:plen] == pl

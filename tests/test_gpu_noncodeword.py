@@ -30,7 +30,11 @@ SHAPES = [(256, 86, 2 * 300), (1024, 342, 2 * 300), (4096, 1366, 2 * 260), (300,
           (700, 234, 2 * 300), (1200, 400, 2 * 290), (600, 256, 2 * 280), (2048, 1024, 2 * 270),
           (1024, 512, 2 * 270), (2000, 667, 2 * 260), (2500, 834, 2 * 270), (5000, 1667, 2 * 260),
           (100, 34, 2 * 300), (150, 50, 2 * 270), (60, 20, 2 * 260), (40, 14, 2 * 280), (16, 8, 2 * 300),
-          (64, 32, 2 * 257), (7000, 2334, 2 * 260), (4096, 2048, 2 * 257), (10000, 3334, 2 * 260)]
+          (64, 32, 2 * 257), (7000, 2334, 2 * 260), (4096, 2048, 2 * 257), (10000, 3334, 2 * 260),
+          # k = 4096 .. 16384 (kernels_huge.hip): n16384 k4096, n32768 k4096 / k8192,
+          # n65536 k8192 / k16384; one full 64-column tile plus a partial one
+          (16384, 5462, 2 * 70), (20000, 6667, 2 * 66), (30000, 10000, 2 * 65), (40000, 13334, 2 * 64 + 2),
+          (65536, 21846, 2 * 67)]
 
 
 def _dev(a):
