@@ -54,8 +54,19 @@ struct HugeArgs {
   const uint16_t* loc;  // reconstruct: locators, batch x n (log form)
   const uint8_t* mode;  // reconstruct: per payload kHugeSkip / kHugeCopy / kHugeDecode
   uint32_t tiles, slots, M, K, NQ;
-  uint32_t m, q;        // this launch's sub-segment and segment (reconstruct) / shift (encode)
+  // this launch's sub-transforms: u0 .. u0 + (grid / per) - 1 (index 1024 u,
+  // slot u; all of one res_gen), per = batch x tiles workgroups each
+  uint32_t u0, per;
 };
+// Workgroup b of a launch: sub-transform u, batch entry and tile.
+struct SubRef {
+  uint32_t u, pb, tl;
+};
+__device__ __forceinline__ SubRef sub_of(const HugeArgs& h, uint32_t b, size_t batch) {
+  const uint32_t u = uniform(h.u0 + b / h.per);
+  const TileRef tr = tile_of(b % h.per, h.tiles, (batch & 7u) == 0);
+  return SubRef{u, tr.pb, tr.tl};
+}
 constexpr uint8_t kHugeSkip = 0, kHugeCopy = 1, kHugeDecode = 2;
 
 __device__ __forceinline__ uint8_t* slot_at(const HugeArgs& h, uint32_t pb, uint32_t tl, uint32_t slot) {
@@ -127,10 +138,10 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
     DevTables T, EncodeArgs a, HugeArgs h, uint32_t nchunks) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
-  const TileRef tr = tile_of(blockIdx.x, h.tiles, (a.batch & 7u) == 0);
-  const uint32_t pb = tr.pb, tl = tr.tl, ch0 = tl * kRC;
+  const SubRef sr = sub_of(h, blockIdx.x, a.batch);
+  const uint32_t pb = sr.pb, tl = sr.tl, ch0 = tl * kRC;
   const uint32_t ncols = min(static_cast<uint32_t>(kRC), nchunks - ch0);
-  const uint32_t I = uniform(kSK * h.m);
+  const uint32_t I = kSK * sr.u;  // sub-segment u of IFFT(k, 0)
   const Res r = res_coords<kSK>();
   const bool full = ncols == kRC && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
   const bool nt = rows_nt(a.shards, a.batch_stride, a.shard_len);
@@ -153,7 +164,7 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
   __syncthreads();
   rh_read<kHDS>(tile, fresh_v(r.hdb), L, H);
   hd_levels<kSK, true>(T, I, L, H);
-  slot_store(slot_at(h, pb, tl, h.m), r.tid, L, H);
+  slot_store(slot_at(h, pb, tl, sr.u), r.tid, L, H);
 }
 
 // Thread (tile, j, t): the coefficients of its quads, then every shift's
@@ -186,15 +197,15 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
     DevTables T, EncodeArgs a, HugeArgs h, uint32_t nchunks) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
-  const TileRef tr = tile_of(blockIdx.x, h.tiles, (a.batch & 7u) == 0);
-  const uint32_t pb = tr.pb, tl = tr.tl, ch0 = tl * kRC;
+  const SubRef sr = sub_of(h, blockIdx.x, a.batch);
+  const uint32_t pb = sr.pb, tl = sr.tl, ch0 = tl * kRC;
   const uint32_t ncols = min(static_cast<uint32_t>(kRC), nchunks - ch0);
-  const uint32_t I = uniform(h.q * h.K + kSK * h.m);
+  const uint32_t I = kSK * sr.u;  // shift u / M, sub-segment u % M
   const Res r = res_coords<kSK>();
   const bool full = ncols == kRC && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
   const bool nt = rows_nt(a.shards, a.batch_stride, a.shard_len);
   uint32_t L[16], H[16];
-  slot_load(slot_at(h, pb, tl, h.q * h.M + h.m), r.tid, L, H);
+  slot_load(slot_at(h, pb, tl, sr.u), r.tid, L, H);
   hd_levels<kSK, false>(T, I, L, H);
   rh_write<kHDS>(tile, fresh_v(r.hdb), L, H);
   __syncthreads();
@@ -214,16 +225,28 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
 // Status (mod.rs:178-180) and mode of each payload: fewer than k present rows:
 // skip; all k systematic rows present: their copy (inc_reconstruct.rs:46-50);
 // else the full decode from every present row.
+// Thread t counts the present flags of rows 4 (t + 256 i) .. + 3 (one dword
+// each; n is a multiple of 1024), then one block sum.
 __global__ __launch_bounds__(256) void k_huge_records(ReconstructArgs a, uint8_t* mode) {
+  __shared__ int part[2][4];
   const uint32_t pb = blockIdx.x;
   const uint8_t* pres = a.present + static_cast<size_t>(pb) * a.n;
-  int have1 = 0, have = 0;
-  for (uint32_t r = 0; r < a.n; r += 256) {
-    const uint32_t v = r + threadIdx.x;
-    const bool p = pres[v] != 0;  // n is a multiple of 256
-    if (r < a.k) have1 += __syncthreads_count(p);
-    have += __syncthreads_count(p);
+  int c1 = 0, c = 0;
+  for (uint32_t v = 4u * threadIdx.x; v < a.n; v += 1024u) {
+    const uint32_t w = *reinterpret_cast<const uint32_t*>(pres + v);  // the flags are 0 / 1 bytes
+    const int cnt = ((w & 0xffu) != 0) + ((w & 0xff00u) != 0) + ((w & 0xff0000u) != 0) + ((w >> 24) != 0);
+    c += cnt;
+    if (v < a.k) c1 += cnt;
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    c += __shfl_xor(c, o);
+    c1 += __shfl_xor(c1, o);
+  }
+  if ((threadIdx.x & 63u) == 0) part[0][threadIdx.x >> 6] = c1, part[1][threadIdx.x >> 6] = c;
+  __syncthreads();
+  const int have1 = part[0][0] + part[0][1] + part[0][2] + part[0][3];
+  const int have = part[1][0] + part[1][1] + part[1][2] + part[1][3];
   const bool ok = have >= static_cast<int>(a.k);
   if (threadIdx.x == 0) {
     if (a.status) {
@@ -239,11 +262,11 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
     DevTables T, ReconstructArgs a, HugeArgs h, uint32_t nsyms) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
-  const TileRef tr = tile_of(blockIdx.x, h.tiles, (a.batch & 7u) == 0);
-  const uint32_t pb = tr.pb, tl = tr.tl;
+  const SubRef sr = sub_of(h, blockIdx.x, a.batch);
+  const uint32_t pb = sr.pb, tl = sr.tl;
   if (uniform(h.mode[pb]) != kHugeDecode) return;
   const uint32_t col0 = tl * kRC, ncols = min(static_cast<uint32_t>(kRC), nsyms - col0);
-  const uint32_t I = uniform(h.q * h.K + kSK * h.m);  // the segment's rows I .. I + 1023
+  const uint32_t I = kSK * sr.u;  // rows I .. I + 1023: segment u / M, sub-segment u % M
   const uint8_t* pres = a.present + static_cast<size_t>(pb) * a.n;
   const uint16_t* loc = h.loc + static_cast<size_t>(pb) * a.n;
   const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);
@@ -280,14 +303,14 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
   __syncthreads();
   rh_read<kHDS>(tile, fresh_v(r.hdb), XL, XH);
   hd_levels<kSK, true>(T, I, XL, XH);
-  slot_store(slot_at(h, pb, tl, h.q * h.M + h.m), r.tid, XL, XH);
-  if (h.q == 0) {  // z = D_1024 of segment 0's sub-transform (the lifted low part of D_k)
+  slot_store(slot_at(h, pb, tl, sr.u), r.tid, XL, XH);
+  if (sr.u < h.M) {  // z = D_1024 of segment 0's sub-transform (the lifted low part of D_k)
     uint32_t AL[16], AH[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) AL[j] = AH[j] = 0;
     add_derivative_hd<kSK>(AL, XL, r.l);
     add_derivative_hd<kSK>(AH, XH, r.l);
-    slot_store(slot_at(h, pb, tl, h.NQ * h.M + h.m), r.tid, AL, AH);
+    slot_store(slot_at(h, pb, tl, h.NQ * h.M + sr.u), r.tid, AL, AH);
   }
 }
 
@@ -353,12 +376,12 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
     DevTables T, ReconstructArgs a, HugeArgs h, uint32_t nsyms) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
-  const TileRef tr = tile_of(blockIdx.x, h.tiles, (a.batch & 7u) == 0);
-  const uint32_t pb = tr.pb, tl = tr.tl;
+  const SubRef sr = sub_of(h, blockIdx.x, a.batch);
+  const uint32_t pb = sr.pb, tl = sr.tl;
   const uint32_t mode = uniform(h.mode[pb]);
   if (mode == kHugeSkip) return;
   const uint32_t col0 = tl * kRC, ncols = min(static_cast<uint32_t>(kRC), nsyms - col0);
-  const uint32_t I = uniform(kSK * h.m);  // output rows I .. I + 1023
+  const uint32_t I = kSK * sr.u;  // output rows I .. I + 1023
   const uint8_t* pres = a.present + static_cast<size_t>(pb) * a.n;
   const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);
   const bool full = ncols == kRC && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
@@ -366,7 +389,7 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
   const Res r = res_coords<kSK>();
   uint32_t AL[16], AH[16];
   if (mode == kHugeDecode) {
-    slot_load(slot_at(h, pb, tl, h.m), r.tid, AL, AH);
+    slot_load(slot_at(h, pb, tl, sr.u), r.tid, AL, AH);
     hd_levels<kSK, false>(T, I, AL, AH);
     rh_write<kHDS>(tile, fresh_v(r.hdb), AL, AH);
     __syncthreads();
@@ -467,39 +490,50 @@ size_t huge_reconstruct_scratch_per_payload(size_t shard_len, uint32_t n, uint32
   return tiles * ((n + k) / kSK) * static_cast<size_t>(kSlotBytes);
 }
 
+// Sub-transforms u in [u0, u1) in launches of one res_gen each: res_gen(1024 u)
+// is 2 for u = 0 and g for u in [2^(g-3), 2^(g-2)).
+template <typename F>
+hipError_t for_gen_ranges(uint32_t u0, uint32_t u1, F&& f) {
+  hipError_t e = hipSuccess;
+  while (u0 < u1 && e == hipSuccess) {
+    const uint32_t end = u0 == 0 ? 1u : std::min(u1, 2u * (1u << (31 - __builtin_clz(u0))));
+    e = with_sub_gen(kSK * u0, [&](auto g) { return f(g, u0, std::min(end, u1)); });
+    u0 = std::min(end, u1);
+  }
+  return e;
+}
+
 hipError_t launch_encode_huge(const DevTables& T, const EncodeArgs& a, uint8_t* scratch, hipStream_t s) {
   if (!huge_encode_supported(a.n, a.k)) return hipErrorInvalidValue;
   const size_t nchunks = (a.payload_len + 2 * a.k - 1) / (2 * a.k);
   if (nchunks == 0 || a.batch == 0) return hipSuccess;
   if (nchunks > 0xffffffffu) return hipErrorInvalidValue;
   const size_t tiles = (nchunks + kRC - 1) / kRC;
-  const size_t blocks = a.batch * tiles;
-  if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
-  const uint32_t nb = static_cast<uint32_t>(blocks), nc = static_cast<uint32_t>(nchunks);
+  const size_t per = a.batch * tiles;
+  if (per * (a.n / kSK) > 0x7fffffffu) return hipErrorInvalidValue;
+  const uint32_t nc = static_cast<uint32_t>(nchunks);
   HugeArgs h = huge_args(scratch, a.n, a.k, tiles, a.n / kSK);
-  hipError_t e = hipSuccess;
-  for (uint32_t m = 0; m < h.M && e == hipSuccess; ++m) {
-    h.m = m;
-    e = with_sub_gen(kSK * m, [&](auto g) {
-      k_huge_enc_inv<decltype(g)::value><<<nb, kSK, RGeo<kSK>::kTileBytes, s>>>(T, a, h, nc);
-      return hipGetLastError();
-    });
-  }
-  const size_t units = blocks * 16 * kSK;
+  h.per = static_cast<uint32_t>(per);
+  auto grid = [&](uint32_t u0, uint32_t u1) { return static_cast<uint32_t>(per * (u1 - u0)); };
+  hipError_t e = for_gen_ranges(0, h.M, [&](auto g, uint32_t u0, uint32_t u1) {
+    h.u0 = u0;
+    k_huge_enc_inv<decltype(g)::value><<<grid(u0, u1), kSK, RGeo<kSK>::kTileBytes, s>>>(T, a, h, nc);
+    return hipGetLastError();
+  });
+  const size_t units = per * 16 * kSK;
   if (e == hipSuccess)
     e = with_m(h.M, [&](auto mc) {
       k_huge_enc_top<decltype(mc)::value><<<static_cast<uint32_t>(units / 256), 256, 0, s>>>(T, h, h.NQ, a.wanted_n, units);
       return hipGetLastError();
     });
-  for (uint32_t sh = 1; sh < h.NQ && e == hipSuccess; ++sh)
-    for (uint32_t m = 0; m < h.M && e == hipSuccess && sh * a.k + kSK * m < a.wanted_n; ++m) {
-      h.q = sh;
-      h.m = m;
-      e = with_sub_gen(sh * a.k + kSK * m, [&](auto g) {
-        k_huge_enc_fwd<decltype(g)::value><<<nb, kSK, RGeo<kSK>::kTileBytes, s>>>(T, a, h, nc);
-        return hipGetLastError();
-      });
-    }
+  // parity sub-segments holding wanted rows: u in [M, ceil(wanted_n / 1024))
+  const uint32_t u_end = std::min(a.n, a.wanted_n + kSK - 1) / kSK;
+  if (e == hipSuccess)
+    e = for_gen_ranges(h.M, u_end, [&](auto g, uint32_t u0, uint32_t u1) {
+      h.u0 = u0;
+      k_huge_enc_fwd<decltype(g)::value><<<grid(u0, u1), kSK, RGeo<kSK>::kTileBytes, s>>>(T, a, h, nc);
+      return hipGetLastError();
+    });
   return e;
 }
 
@@ -518,22 +552,21 @@ hipError_t launch_reconstruct_huge(const DevTables& T, const ReconstructArgs& a,
     loc = locators;
   }
   const size_t tiles = (nsyms + kRC - 1) / kRC;
-  const size_t blocks = a.batch * tiles;
-  if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
-  const uint32_t nb = static_cast<uint32_t>(blocks), ns = static_cast<uint32_t>(nsyms);
+  const size_t per = a.batch * tiles;
+  if (per * (a.n / kSK) > 0x7fffffffu) return hipErrorInvalidValue;
+  const uint32_t ns = static_cast<uint32_t>(nsyms);
   HugeArgs h = huge_args(scratch, a.n, a.k, tiles, (a.n + a.k) / kSK);
   h.loc = loc;
   h.mode = mode;
-  for (uint32_t q = 0; q < h.NQ && e == hipSuccess; ++q)
-    for (uint32_t m = 0; m < h.M && e == hipSuccess; ++m) {
-      h.q = q;
-      h.m = m;
-      e = with_sub_gen(q * a.k + kSK * m, [&](auto g) {
-        k_huge_rec_inv<decltype(g)::value><<<nb, kSK, RGeo<kSK>::kTileBytes, s>>>(T, a, h, ns);
-        return hipGetLastError();
-      });
-    }
-  const size_t units = blocks * 16 * kSK;
+  h.per = static_cast<uint32_t>(per);
+  auto grid = [&](uint32_t u0, uint32_t u1) { return static_cast<uint32_t>(per * (u1 - u0)); };
+  if (e == hipSuccess)
+    e = for_gen_ranges(0, a.n / kSK, [&](auto g, uint32_t u0, uint32_t u1) {
+      h.u0 = u0;
+      k_huge_rec_inv<decltype(g)::value><<<grid(u0, u1), kSK, RGeo<kSK>::kTileBytes, s>>>(T, a, h, ns);
+      return hipGetLastError();
+    });
+  const size_t units = per * 16 * kSK;
   if (e == hipSuccess)
     e = with_m(h.M, [&](auto mc) {
       return with_nq(h.NQ, [&](auto qc) {
@@ -542,13 +575,12 @@ hipError_t launch_reconstruct_huge(const DevTables& T, const ReconstructArgs& a,
         return hipGetLastError();
       });
     });
-  for (uint32_t m = 0; m < h.M && e == hipSuccess; ++m) {
-    h.m = m;
-    e = with_sub_gen(kSK * m, [&](auto g) {
-      k_huge_rec_fwd<decltype(g)::value><<<nb, kSK, RGeo<kSK>::kTileBytes, s>>>(T, a, h, ns);
+  if (e == hipSuccess)
+    e = for_gen_ranges(0, h.M, [&](auto g, uint32_t u0, uint32_t u1) {
+      h.u0 = u0;
+      k_huge_rec_fwd<decltype(g)::value><<<grid(u0, u1), kSK, RGeo<kSK>::kTileBytes, s>>>(T, a, h, ns);
       return hipGetLastError();
     });
-  }
   return e;
 }
 
