@@ -5,7 +5,7 @@
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/huge
 run() { tag=$1; shift
-  timeout -k 10 300 env "$@" > gpurun_out/huge/$tag.log 2>&1 || { tail -5 gpurun_out/huge/$tag.log; exit 1; }
+  timeout -k 10 300 env "$@" --out gpurun_out/huge/$tag.json > gpurun_out/huge/$tag.log 2>&1 || { tail -5 gpurun_out/huge/$tag.log; exit 1; }
   python3 -c "
 import json; d=json.loads(open('gpurun_out/huge/$tag.log').read().strip().split('\n')[-1])
 c=d['config']; print('$tag', 'n', c['n'], 'k', c['k'], 'GiB/s', d['value'], {k:(v['ms'], v['frac']) for k,v in d['kernels'].items()}, 'ok', d['roundtrip_ok'])"
