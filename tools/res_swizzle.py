@@ -54,7 +54,7 @@ def conflicts(K, f):
     return bad
 
 
-PRODUCT = {1024: [24, 4, 1, 2, 20, 8], 512: None}
+PRODUCT = {1024: [24, 4, 1, 2, 20, 8], 512: [28, 14, 1, 25, 20, 27]}  # kernels_res rsw<K>
 
 
 def search(K, tries=200000, seed=1):
