@@ -30,6 +30,9 @@ __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4))) void k_e
   const uint32_t wanted_store = ((kExp & 2) && a.k != 12345u) ? 0u : a.wanted_n;  // experiment: no stores
 
   load_pay_tile<K>(tile, pay, a.payload_len, ch0, 2 * K, 0, r.tid);
+  const uint32_t nshift = a.n / K;
+  uint32_t* VS = reinterpret_cast<uint32_t*>(smem + RGeo<K>::kTileBytes);  // HA / HD tables, RStage
+  stage_rh_tables<K>(T, VS, nshift);
   __syncthreads();
   // ---- CQ: systematic rows, inverse levels 0-3 (index 0: every multiplier in GF(2^8))
   {
@@ -46,17 +49,16 @@ __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4))) void k_e
   {
     uint32_t L[16], H[16];
     rh_read<kHA>(tile, fresh_v(r.hab), L, H);
-    ha_levels<true>(T, 0, r, L, H);
+    ha_levels_st<K, true>(T, 0, r, L, H, VS);
     __syncthreads();
     rh_write<kHA>(tile, fresh_v(r.hab), L, H);
     __syncthreads();
     rh_read<kHD>(tile, fresh_v(r.hdb), ML, MH);
   }
-  hd_levels<K, true>(T, 0, ML, MH);
+  hd_levels_st<K, true>(T, 0, ML, MH, VS);
 #pragma unroll
   for (int q = 0; q < 16; ++q) asm volatile("" : "+v"(ML[q]), "+v"(MH[q]));  // materialise M once
 
-  const uint32_t nshift = a.n / K;
   auto shift = [&](auto gc, uint32_t sh) __attribute__((always_inline)) {
     constexpr int GEN = decltype(gc)::value;
     const uint32_t I = sh * K;
@@ -66,12 +68,13 @@ __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4))) void k_e
       L[q] = ML[q];
       H[q] = MH[q];
     }
-    hd_levels<K, false>(T, I, L, H);
+    const uint32_t* vs = VS + sh * RStage<K>::kWords;
+    hd_levels_st<K, false>(T, I, L, H, vs);
     __syncthreads();  // the previous CQ pass is done with the tile
     rh_write<kHD>(tile, fresh_v(r.hdb), L, H);
     __syncthreads();
     rh_read<kHA>(tile, fresh_v(r.hab), L, H);
-    ha_levels<false, GEN>(T, I, r, L, H);
+    ha_levels_st<K, false, GEN>(T, I, r, L, H, vs);
     __syncthreads();
     rh_write<kHA>(tile, fresh_v(r.hab), L, H);
     __syncthreads();
@@ -141,12 +144,13 @@ __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructAr
   rcq_write<K>(tile, fresh_v(rr.cqb), XL, XH);
   __syncthreads();
   rh_read<kHA>(tile, fresh_v(rr.hab), XL, XH);
-  ha_levels<true, res_gen<K>(I)>(T, I, rr, XL, XH);
+  const uint32_t* vs = reinterpret_cast<const uint32_t*>(tile + RGeo<K>::kTileBytes) + q * RStage<K>::kWords;
+  ha_levels_st<K, true, res_gen<K>(I)>(T, I, rr, XL, XH, vs);
   __syncthreads();
   rh_write<kHA>(tile, fresh_v(rr.hab), XL, XH);
   __syncthreads();
   rh_read<kHD>(tile, fresh_v(rr.hdb), XL, XH);
-  hd_levels<K, true>(T, I, XL, XH);
+  hd_levels_st<K, true>(T, I, XL, XH, vs);
   // fold x_q into d (kernels_fast.hip rec_segments)
   if constexpr (NQ == 8 && q != 0 && rec8_kappa_res(q) != 1u) {  // d ^= kappa_q x_q, kappa_q in GF(16)
     uint32_t kp[20];
@@ -201,6 +205,8 @@ __device__ __forceinline__ void res_decode_tile(const DevTables& T, const Recons
                                                 const uint8_t* pools, const uint8_t* pres, const uint8_t* sh,
                                                 uint8_t* out_tile, uint32_t ncols, bool full, bool out16) {
   uint32_t AL[16], AH[16];
+  const uint32_t* VS = reinterpret_cast<const uint32_t*>(tile + RGeo<K>::kTileBytes);  // RStage blocks 0..NQ-1
+  stage_rh_tables<K>(T, reinterpret_cast<uint32_t*>(tile + RGeo<K>::kTileBytes), NQ);  // the first step's barriers order it
   if (!res_sweep<K, NQ>(T, a, tile, pools, pres, sh, out_tile, ncols, full, out16, AL, AH,
                      std::make_integer_sequence<int, NQ>{}))
     return;
@@ -216,12 +222,12 @@ __device__ __forceinline__ void res_decode_tile(const DevTables& T, const Recons
     return;
   }
   // ---- out = FFT(K, 0)(d), first k rows (inc_reconstruct.rs:80)
-  hd_levels<K, false>(T, 0, AL, AH);
+  hd_levels_st<K, false>(T, 0, AL, AH, VS);
   __syncthreads();  // the last step's HD read is done
   rh_write<kHD>(tile, fresh_v(r.hdb), AL, AH);
   __syncthreads();
   rh_read<kHA>(tile, fresh_v(r.hab), AL, AH);
-  ha_levels<false>(T, 0, r, AL, AH);
+  ha_levels_st<K, false>(T, 0, r, AL, AH, VS);
   __syncthreads();
   rh_write<kHA>(tile, fresh_v(r.hab), AL, AH);
   __syncthreads();
@@ -307,6 +313,14 @@ bool res_encode_supported(uint32_t n, uint32_t k) { return (k == 512 || k == 102
 bool res_reconstruct_supported(uint32_t n, uint32_t k) { return res_encode_supported(n, k); }
 
 namespace {
+// Dynamic LDS of a kernel over nblk transform indices: the tile plus the RStage blocks.
+template <int K>
+constexpr uint32_t res_lds(uint32_t nblk) {
+  return RGeo<K>::kTileBytes + 4u * RStage<K>::kWords * nblk;
+}
+static_assert(res_lds<1024>(8) <= 160u * 1024u, "k = 1024: one workgroup per CU");
+static_assert(res_lds<512>(8) <= 80u * 1024u, "k = 512: two workgroups per CU");
+
 template <int K>
 hipError_t launch_reconstruct_res_k(const DevTables& T, const ReconstructArgs& a, hipStream_t s) {
   using G = RGeo<K>;
@@ -318,9 +332,9 @@ hipError_t launch_reconstruct_res_k(const DevTables& T, const ReconstructArgs& a
   if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
   const uint32_t nb = static_cast<uint32_t>(blocks), ns = static_cast<uint32_t>(nsyms);
   k_reconstruct_res<K, 1><<<nb, G::kThreads, 0, s>>>(T, a, ns, tiles);
-  if (a.n == 2u * K || a.trusted) k_reconstruct_res<K, 2><<<nb, G::kThreads, G::kTileBytes, s>>>(T, a, ns, tiles);
-  if (a.n == 4u * K) k_reconstruct_res<K, 4><<<nb, G::kThreads, G::kTileBytes, s>>>(T, a, ns, tiles);
-  if (a.n == 8u * K) k_reconstruct_res<K, 8><<<nb, G::kThreads, G::kTileBytes, s>>>(T, a, ns, tiles);
+  if (a.n == 2u * K || a.trusted) k_reconstruct_res<K, 2><<<nb, G::kThreads, res_lds<K>(2), s>>>(T, a, ns, tiles);
+  if (a.n == 4u * K) k_reconstruct_res<K, 4><<<nb, G::kThreads, res_lds<K>(4), s>>>(T, a, ns, tiles);
+  if (a.n == 8u * K) k_reconstruct_res<K, 8><<<nb, G::kThreads, res_lds<K>(8), s>>>(T, a, ns, tiles);
   return hipGetLastError();
 }
 
@@ -333,7 +347,7 @@ hipError_t launch_encode_res_k(const DevTables& T, const EncodeArgs& a, hipStrea
   const uint32_t tiles = static_cast<uint32_t>((nchunks + kRC - 1) / kRC);
   const size_t blocks = a.batch * tiles;
   if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
-  k_encode_res<K><<<static_cast<uint32_t>(blocks), G::kThreads, G::kTileBytes, s>>>(T, a, static_cast<uint32_t>(nchunks), tiles);
+  k_encode_res<K><<<static_cast<uint32_t>(blocks), G::kThreads, res_lds<K>(a.n / K), s>>>(T, a, static_cast<uint32_t>(nchunks), tiles);
   return hipGetLastError();
 }
 
@@ -343,7 +357,7 @@ hipError_t configure_res_k() {
   for (const void* f : {reinterpret_cast<const void*>(&k_encode_res<K>), reinterpret_cast<const void*>(&k_reconstruct_res<K, 2>),
                         reinterpret_cast<const void*>(&k_reconstruct_res<K, 4>),
                         reinterpret_cast<const void*>(&k_reconstruct_res<K, 8>)}) {
-    const hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(RGeo<K>::kTileBytes));
+    const hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(res_lds<K>(8)));
     if (r != hipSuccess && e == hipSuccess) e = r;
   }
   return e;

@@ -416,14 +416,55 @@ __host__ __device__ constexpr int rh_groups() {
   return n;
 }
 
+// Staged VGPR halves of the HA / HD multipliers (kernels_res.hip), per
+// transform of index I = blk K: kNH + 1 blocks of 15 slots of 8 dwords
+// (pool dwords 0-7); block h < kNH holds the HA groups of hi = h (position
+// bits 8-9 = w >> 2), block kNH the HD groups (hi = 0).  Level r (relative to
+// the layout's first position bit), group t: slot rslot(r, t) of its block.
+template <int K>
+struct RStage {
+  static constexpr uint32_t kNH = K / 256;
+  static constexpr uint32_t kSlots = 15u * (kNH + 1);
+  static constexpr uint32_t kWords = 8u * kSlots;  // per transform
+};
+__host__ __device__ constexpr uint32_t rslot(int r, int t) {
+  return 16u - (16u >> r) + static_cast<uint32_t>(t);
+}
+
+// Copies the staged halves of the transforms at I = 0, K, .., (nblk - 1) K
+// into VS (nblk * RStage<K>::kWords dwords).  Caller synchronises.
+template <int K>
+__device__ __forceinline__ void stage_rh_tables(const DevTables& T, uint32_t* VS, uint32_t nblk) {
+  using S = RStage<K>;
+  constexpr int pbd = RGeo<K>::kLogK - 4;  // HD's first position bit
+  const uint32_t* pools = fresh(T.tower_pools);
+  const uint32_t total = 2u * S::kSlots * nblk;
+  for (uint32_t i = fresh_v(threadIdx.x); i < total; i += K) {
+    const uint32_t half = i & 1u, s = i >> 1;
+    const uint32_t blk = s / S::kSlots, sl = s % S::kSlots;
+    const uint32_t hb = sl / 15u, loc = sl % 15u;
+    uint32_t r = 0;
+    while (loc >= 16u - (8u >> r)) ++r;
+    const uint32_t t = loc - (16u - (16u >> r)), I = blk * K;
+    const uint32_t c = hb < S::kNH ? 2u * ((hb << (3 - r)) + t) + (I >> (4 + r)) : 2u * t + (I >> (pbd + r));
+    *reinterpret_cast<uint4*>(VS + 8u * s + 4u * half) =
+        *reinterpret_cast<const uint4*>(pools + static_cast<size_t>(c) * kPoolWords + 4u * half);
+  }
+}
+
 // Levels PB0 + r, R0 <= r < R1, in a register layout whose register index j
 // holds position bits PB0..PB0+3 and whose wave holds the bits above as `hi`:
 // group T = (j >> (r + 1)) + (hi << (3 - r)).  Every multiplier is
 // wave-uniform; levels below GEN (res_gen(I)) hold full ones (level 4 for
 // I >= 4096, the shifts and segments of n = 8192), the others lie in GF(2^8).
-template <int PB0, int R0, int R1, bool INVERSE, int GEN = 0>
+//
+// With vsb (the kernels_res.hip kernels) the VGPR halves of the multipliers
+// come from the LDS block of the transform (RStage, stage_rh_tables) by
+// ds_read instead of as v_mov copies of the s_loaded pool: 4 v_mov_b64 per
+// group, i.e. up to a fifth of a level-4 butterfly.
+template <int PB0, int R0, int R1, bool INVERSE, int GEN = 0, bool ST = false>
 __device__ __forceinline__ void rh_levels(const DevTables& T, uint32_t I, uint32_t hi, uint32_t (&L)[16],
-                                          uint32_t (&H)[16]) {
+                                          uint32_t (&H)[16], const uint32_t* vsb = nullptr) {
   if constexpr (kExp & 1) return;
   const uint32_t h = fresh(hi);
   auto cval = [&](auto fc) __attribute__((always_inline)) {
@@ -448,7 +489,18 @@ __device__ __forceinline__ void rh_levels(const DevTables& T, uint32_t I, uint32
       }
     }
   };
-  tpipelined<rh_groups<R0, R1>()>(T, cval, group);
+  if constexpr (ST) {
+    auto vaddr = [&](auto fc) __attribute__((always_inline)) {
+      constexpr GroupRef g = rh_group<R0, R1, INVERSE>(decltype(fc)::value);
+      return vsb + 8u * rslot(g.b, g.t);
+    };
+    auto subf = [&](auto fc) __attribute__((always_inline)) {
+      return std::integral_constant<bool, (PB0 + rh_group<R0, R1, INVERSE>(decltype(fc)::value).b >= GEN)>{};
+    };
+    pipelined_staged<rh_groups<R0, R1>(), true>(T, cval, vaddr, subf, group);
+  } else {
+    tpipelined<rh_groups<R0, R1>()>(T, cval, group);
+  }
 }
 
 // HA: levels 4-7 (hi = position bits 8-9 = w >> 2; K = 512: bit 8).  HD:
@@ -465,6 +517,21 @@ __device__ __forceinline__ void hd_levels(const DevTables& T, uint32_t I, uint32
   if constexpr (kExp & 1024) return;
   constexpr int pb0 = RGeo<K>::kLogK - 4;
   rh_levels<pb0, 8 - pb0, 4, INVERSE>(T, I, 0u, L, H);
+}
+// The same with the staged VGPR halves: vs = the transform's RStage block.
+template <int K, bool INVERSE, int GEN = 0>
+__device__ __forceinline__ void ha_levels_st(const DevTables& T, uint32_t I, const Res& r, uint32_t (&L)[16],
+                                             uint32_t (&H)[16], const uint32_t* vs) {
+  if constexpr (kExp & 512) return;
+  const uint32_t h = fresh(r.w >> 2);
+  rh_levels<4, 0, 4, INVERSE, GEN, true>(T, I, h, L, H, vs + 120u * h);
+}
+template <int K, bool INVERSE>
+__device__ __forceinline__ void hd_levels_st(const DevTables& T, uint32_t I, uint32_t (&L)[16], uint32_t (&H)[16],
+                                             const uint32_t* vs) {
+  if constexpr (kExp & 1024) return;
+  constexpr int pb0 = RGeo<K>::kLogK - 4;
+  rh_levels<pb0, 8 - pb0, 4, INVERSE, 0, true>(T, I, 0u, L, H, vs + 120u * RStage<K>::kNH);
 }
 
 // A ^= D_K(X) in the HD layout for one byte plane (inc_afft.rs:17-31,
