@@ -31,7 +31,9 @@ __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4))) void k_e
 
   load_pay_tile<K>(tile, pay, a.payload_len, ch0, 2 * K, 0, r.tid);
   const uint32_t nshift = a.n / K;
-  uint32_t* VS = reinterpret_cast<uint32_t*>(smem + RGeo<K>::kTileBytes);  // HA / HD tables, RStage
+  uint32_t* DL = reinterpret_cast<uint32_t*>(smem + RGeo<K>::kTileBytes);  // CQ delta tables
+  uint32_t* VS = DL + kDeltaWords;                                           // HA / HD tables, RStage
+  stage_delta_tables(T, DL);
   stage_rh_tables<K>(T, VS, nshift);
   __syncthreads();
   // ---- CQ: systematic rows, inverse levels 0-3 (index 0: every multiplier in GF(2^8))
@@ -40,7 +42,7 @@ __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4))) void k_e
     rcq_read_nat<K>(tile, r.cqb, L, H);
     rres_store_rows(out, a.shard_len, 0, wanted_store, L, H, r, ncols, full, nt);
     tower_convert(T, L, H);  // the transforms run in tower coordinates
-    rcq_levels<true, res_gen<K>(0)>(T, 0, r, L, H);
+    rcq_levels<true, res_gen<K>(0), true>(T, 0, r, L, H, DL);
     __syncthreads();  // every wave has read its payload blocks
     rcq_write<K>(tile, fresh_v(r.cqb), L, H);
   }
@@ -79,7 +81,7 @@ __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4))) void k_e
     rh_write<kHA>(tile, fresh_v(r.hab), L, H);
     __syncthreads();
     rcq_read<K>(tile, fresh_v(r.cqb), L, H);
-    rcq_levels<false, GEN>(T, I, r, L, H);
+    rcq_levels<false, GEN, true>(T, I, r, L, H, DL);
     tower_convert(T, L, H);  // back to Cantor coordinates for the shard rows
     rres_store_rows(out, a.shard_len, I, wanted_store, L, H, r, ncols, full, nt);
   };
@@ -89,6 +91,12 @@ __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4))) void k_e
 #pragma unroll 1
   for (uint32_t sh = 4; sh < nshift && sh * K < a.wanted_n; ++sh) shift(Int<res_gen<K>(4 * K)>{}, sh);  // n = 8K
 }
+
+// The decode's full CQ levels through per-lane full tables (rcq_group ST),
+// except in the k = 1024, 8-segment instance, where the tables' 20 VGPRs
+// made the allocator spill 60 dwords instead of 15.
+template <int K, int NQ>
+constexpr bool kRecDeltaST = !(K == 1024 && NQ == 8);
 
 template <int NQ>
 __host__ __device__ constexpr int res_seg(int step) {  // segments 2, 3, 1, 0 (NQ = 4); 1, 0 (NQ = 2); 7..0 (NQ = 8)
@@ -135,7 +143,8 @@ __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructAr
     res_copy_out<K>(out_tile, XL, XH, rr, ncols, out16);
     return false;
   }
-  rcq_levels<true, res_gen<K>(I)>(T, I, rr, XL, XH);
+  const uint32_t* DL = reinterpret_cast<const uint32_t*>(tile + RGeo<K>::kTileBytes);
+  rcq_levels<true, res_gen<K>(I), kRecDeltaST<K, NQ>>(T, I, rr, XL, XH, DL);
   if constexpr ((kExp & 32768) != 0 && STEP == 0) {  // experiment: the first step after its CQ levels
     res_copy_out<K>(out_tile, XL, XH, rr, ncols, out16);
     return false;
@@ -144,7 +153,7 @@ __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructAr
   rcq_write<K>(tile, fresh_v(rr.cqb), XL, XH);
   __syncthreads();
   rh_read<kHA>(tile, fresh_v(rr.hab), XL, XH);
-  const uint32_t* vs = reinterpret_cast<const uint32_t*>(tile + RGeo<K>::kTileBytes) + q * RStage<K>::kWords;
+  const uint32_t* vs = DL + kDeltaWords + q * RStage<K>::kWords;
   ha_levels_st<K, true, res_gen<K>(I)>(T, I, rr, XL, XH, vs);
   __syncthreads();
   rh_write<kHA>(tile, fresh_v(rr.hab), XL, XH);
@@ -205,8 +214,10 @@ __device__ __forceinline__ void res_decode_tile(const DevTables& T, const Recons
                                                 const uint8_t* pools, const uint8_t* pres, const uint8_t* sh,
                                                 uint8_t* out_tile, uint32_t ncols, bool full, bool out16) {
   uint32_t AL[16], AH[16];
-  const uint32_t* VS = reinterpret_cast<const uint32_t*>(tile + RGeo<K>::kTileBytes);  // RStage blocks 0..NQ-1
-  stage_rh_tables<K>(T, reinterpret_cast<uint32_t*>(tile + RGeo<K>::kTileBytes), NQ);  // the first step's barriers order it
+  uint32_t* DL = reinterpret_cast<uint32_t*>(tile + RGeo<K>::kTileBytes);  // CQ delta tables
+  uint32_t* VS = DL + kDeltaWords;                                      // RStage blocks 0..NQ-1
+  stage_delta_tables(T, DL);  // the first step's barriers order both
+  stage_rh_tables<K>(T, VS, NQ);
   if (!res_sweep<K, NQ>(T, a, tile, pools, pres, sh, out_tile, ncols, full, out16, AL, AH,
                      std::make_integer_sequence<int, NQ>{}))
     return;
@@ -232,7 +243,7 @@ __device__ __forceinline__ void res_decode_tile(const DevTables& T, const Recons
   rh_write<kHA>(tile, fresh_v(r.hab), AL, AH);
   __syncthreads();
   rcq_read<K>(tile, fresh_v(r.cqb), AL, AH);
-  rcq_levels<false, res_gen<K>(0)>(T, 0, r, AL, AH);
+  rcq_levels<false, res_gen<K>(0), kRecDeltaST<K, NQ>>(T, 0, r, AL, AH, DL);
   // ---- merge: received systematic rows, postmultiplied recovered ones
   // (inc_reconstruct.rs:46-50, :82-84; tower in, Cantor out)
   const uint32_t pm = lane_rows_present(pres, 0, r);
@@ -313,10 +324,11 @@ bool res_encode_supported(uint32_t n, uint32_t k) { return (k == 512 || k == 102
 bool res_reconstruct_supported(uint32_t n, uint32_t k) { return res_encode_supported(n, k); }
 
 namespace {
-// Dynamic LDS of a kernel over nblk transform indices: the tile plus the RStage blocks.
+// Dynamic LDS of a kernel over nblk transform indices: the tile, the CQ delta
+// tables and the RStage blocks.
 template <int K>
 constexpr uint32_t res_lds(uint32_t nblk) {
-  return RGeo<K>::kTileBytes + 4u * RStage<K>::kWords * nblk;
+  return RGeo<K>::kTileBytes + 4u * (kDeltaWords + RStage<K>::kWords * nblk);
 }
 static_assert(res_lds<1024>(8) <= 160u * 1024u, "k = 1024: one workgroup per CU");
 static_assert(res_lds<512>(8) <= 80u * 1024u, "k = 512: two workgroups per CU");

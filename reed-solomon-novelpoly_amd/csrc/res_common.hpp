@@ -256,6 +256,46 @@ __device__ __forceinline__ void qmul_set_vv(uint32_t& ol, uint32_t& oh, uint32_t
   qplane_set_vv(oh, s, m.p[4], m.p[5], m.p[6], m.p[7], m.p[14], m.p[15], m.p[16], m.p[17], m.p[18], m.p[19]);
 }
 
+// x ^= c*y with a per-lane full table (qmul_set_vv's accumulating form).
+__device__ __forceinline__ void qplane_vv(uint32_t& acc, const uint32_t (&s)[6], uint32_t va, uint32_t vb,
+                                          uint32_t vc, uint32_t vd, uint32_t sa, uint32_t sb, uint32_t sc,
+                                          uint32_t sd, uint32_t se, uint32_t sf) {
+  uint32_t t0, t1, t2;
+  asm volatile(
+      "v_perm_b32 %[t0], %[sa], %[va], %[s0]\n\t"
+      "v_perm_b32 %[t1], %[sb], %[vb], %[s1]\n\t"
+      "v_perm_b32 %[t2], %[sc], %[sc], %[s2]\n\t"
+      "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t"
+      "v_perm_b32 %[t1], %[sd], %[vc], %[s3]\n\t"
+      "v_perm_b32 %[t2], %[se], %[vd], %[s4]\n\t"
+      "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t"
+      "v_perm_b32 %[t1], %[sf], %[sf], %[s5]\n\t"
+      "v_bitop3_b32 %[acc], %[acc], %[t0], %[t1] bitop3:0x96"
+      : [acc] "+v"(acc), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2)
+      : [s0] "v"(s[0]), [s1] "v"(s[1]), [s2] "v"(s[2]), [s3] "v"(s[3]), [s4] "v"(s[4]), [s5] "v"(s[5]),
+        [va] "v"(va), [vb] "v"(vb), [vc] "v"(vc), [vd] "v"(vd), [sa] "v"(sa), [sb] "v"(sb), [sc] "v"(sc),
+        [sd] "v"(sd), [se] "v"(se), [sf] "v"(sf));
+}
+__device__ __forceinline__ void qmul_vv(uint32_t& xl, uint32_t& xh, uint32_t yl, uint32_t yh, const FullT& m) {
+  uint32_t s[6];
+  selectors(yl, yh, s);
+  qplane_vv(xl, s, m.p[0], m.p[1], m.p[2], m.p[3], m.p[8], m.p[9], m.p[10], m.p[11], m.p[12], m.p[13]);
+  qplane_vv(xh, s, m.p[4], m.p[5], m.p[6], m.p[7], m.p[14], m.p[15], m.p[16], m.p[17], m.p[18], m.p[19]);
+}
+
+// Full-layout tables of the per-lane deltas Cantor(u << (4 - b)), b, u < 4
+// (tower_full_sub), staged once per kernel for the full CQ levels b >= 1:
+// table (b, u) at DL + 20 (4 b + u).  Caller synchronises.
+constexpr uint32_t kDeltaWords = 16u * kPoolWords;
+__device__ __forceinline__ void stage_delta_tables(const DevTables& T, uint32_t* DL) {
+  const uint32_t i = threadIdx.x;
+  if (i < kDeltaWords / 4u) {
+    const uint32_t slot = i / 5u, part = i % 5u, b = slot >> 2, u = slot & 3u;
+    *reinterpret_cast<uint4*>(DL + kPoolWords * slot + 4u * part) = *reinterpret_cast<const uint4*>(
+        T.tower_full_sub + static_cast<size_t>(u << (4 - b)) * kPoolWords + 4u * part);
+  }
+}
+
 // The per-lane part delta = Cantor(u << (4 - b)) of the CQ skews at level b:
 // its subfield tables (tower_pools, sub layout).
 __device__ __forceinline__ SubT delta_tables(const DevTables& T, uint32_t u, int b) {
@@ -292,9 +332,13 @@ static_assert(res_gen<512>(0) == 1 && res_gen<512>(512) == 2 && res_gen<512>(153
 // CQ levels 0-3 of a size-1024 transform at index I.  GEN: levels b < GEN
 // have full multipliers (gen_of(I), fast_common.hpp kSubLevel).  Group t of
 // level b in this thread is registers t 2^(b+1) .. + 2^(b+1).
-template <bool INVERSE, int GEN, int B, int TG>
+// ST (kernels_res.hip): full levels b >= 1 multiply by c_w + delta through a
+// per-lane full table, the XOR of c_w's (s_load) and delta's (staged in LDS at
+// dl, stage_delta_tables): 20 XORs per group instead of a delta multiply (10
+// instructions) per butterfly and the 4 v_mov copies of c_w's VGPR half.
+template <bool INVERSE, int GEN, int B, int TG, bool ST = false>
 __device__ __forceinline__ void rcq_group(const DevTables& T, uint32_t I, uint32_t w, const SubT& dt,
-                                          uint32_t (&L)[16], uint32_t (&H)[16]) {
+                                          uint32_t (&L)[16], uint32_t (&H)[16], const uint32_t* dl = nullptr) {
   constexpr int d = 1 << B;
   // uniform element of group TG: Cantor(w << (6 - B) | 2 TG | I >> B)
   const uint32_t cw = (w << (6 - B)) + 2u * TG + (I >> B);
@@ -318,6 +362,31 @@ __device__ __forceinline__ void rcq_group(const DevTables& T, uint32_t I, uint32
         qmul_sub_vv(L[x], H[x], L[y], H[y], m);
       } else {
         qmul_sub_vv(L[x], H[x], L[y], H[y], m);
+        L[y] ^= L[x];
+        H[y] ^= H[x];
+      }
+    }
+  } else if constexpr (ST && B >= 1) {  // per-lane full table of c_w + delta
+    const uint32_t c = fresh(cw);
+    const cpool_t q = (cpool_t)(c < 256u ? T.tower_full_sub : T.tower_pools) + c * kPoolWords;
+    FullT m;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const uint4 d = *reinterpret_cast<const uint4*>(dl + 4 * i);
+      m.p[4 * i] = q[4 * i] ^ d.x;
+      m.p[4 * i + 1] = q[4 * i + 1] ^ d.y;
+      m.p[4 * i + 2] = q[4 * i + 2] ^ d.z;
+      m.p[4 * i + 3] = q[4 * i + 3] ^ d.w;
+    }
+#pragma unroll
+    for (int v = 0; v < d; ++v) {
+      const int x = TG * 2 * d + v, y = x + d;
+      if constexpr (INVERSE) {
+        L[y] ^= L[x];
+        H[y] ^= H[x];
+        qmul_vv(L[x], H[x], L[y], H[y], m);
+      } else {
+        qmul_vv(L[x], H[x], L[y], H[y], m);
         L[y] ^= L[x];
         H[y] ^= H[x];
       }
@@ -348,31 +417,37 @@ __device__ __forceinline__ void rcq_group(const DevTables& T, uint32_t I, uint32
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <bool INVERSE, int GEN, int B, int... TG>
+template <bool INVERSE, int GEN, int B, bool ST, int... TG>
 __device__ __forceinline__ void rcq_level(const DevTables& T, uint32_t I, uint32_t w, uint32_t u, uint32_t (&L)[16],
-                                          uint32_t (&H)[16], std::integer_sequence<int, TG...>) {
-  const SubT dt = delta_tables(T, u, B);
-  (rcq_group<INVERSE, GEN, B, TG>(T, I, w, dt, L, H), ...);
+                                          uint32_t (&H)[16], const uint32_t* DL, std::integer_sequence<int, TG...>) {
+  if constexpr (ST && B >= 1 && B < GEN) {
+    const uint32_t* dl = DL + kPoolWords * (4u * B + u);
+    const SubT dt{};
+    (rcq_group<INVERSE, GEN, B, TG, true>(T, I, w, dt, L, H, dl), ...);
+  } else {
+    const SubT dt = delta_tables(T, u, B);
+    (rcq_group<INVERSE, GEN, B, TG>(T, I, w, dt, L, H), ...);
+  }
 }
 
 // Experiment builds (NP_EXP, never the product): bit 8 skips the CQ levels,
 // bit 9 the HA levels, bit 10 the HD levels (tools/res_debug.py).
-template <bool INVERSE, int GEN>
+template <bool INVERSE, int GEN, bool ST = false>
 __device__ __forceinline__ void rcq_levels(const DevTables& T, uint32_t I, const Res& r, uint32_t (&L)[16],
-                                           uint32_t (&H)[16]) {
+                                           uint32_t (&H)[16], const uint32_t* DL = nullptr) {
   if constexpr (kExp & (1 | 256)) return;
   if constexpr (INVERSE ? (kExp & 4096) != 0 : (kExp & 2048) != 0) return;  // experiment: one direction only
   const uint32_t w = fresh(r.w), u = fresh_v(r.u);
   if constexpr (INVERSE) {
-    rcq_level<true, GEN, 0>(T, I, w, u, L, H, std::make_integer_sequence<int, 8>{});
-    rcq_level<true, GEN, 1>(T, I, w, u, L, H, std::make_integer_sequence<int, 4>{});
-    rcq_level<true, GEN, 2>(T, I, w, u, L, H, std::make_integer_sequence<int, 2>{});
-    rcq_level<true, GEN, 3>(T, I, w, u, L, H, std::make_integer_sequence<int, 1>{});
+    rcq_level<true, GEN, 0, ST>(T, I, w, u, L, H, DL, std::make_integer_sequence<int, 8>{});
+    rcq_level<true, GEN, 1, ST>(T, I, w, u, L, H, DL, std::make_integer_sequence<int, 4>{});
+    rcq_level<true, GEN, 2, ST>(T, I, w, u, L, H, DL, std::make_integer_sequence<int, 2>{});
+    rcq_level<true, GEN, 3, ST>(T, I, w, u, L, H, DL, std::make_integer_sequence<int, 1>{});
   } else {
-    rcq_level<false, GEN, 3>(T, I, w, u, L, H, std::make_integer_sequence<int, 1>{});
-    rcq_level<false, GEN, 2>(T, I, w, u, L, H, std::make_integer_sequence<int, 2>{});
-    rcq_level<false, GEN, 1>(T, I, w, u, L, H, std::make_integer_sequence<int, 4>{});
-    rcq_level<false, GEN, 0>(T, I, w, u, L, H, std::make_integer_sequence<int, 8>{});
+    rcq_level<false, GEN, 3, ST>(T, I, w, u, L, H, DL, std::make_integer_sequence<int, 1>{});
+    rcq_level<false, GEN, 2, ST>(T, I, w, u, L, H, DL, std::make_integer_sequence<int, 2>{});
+    rcq_level<false, GEN, 1, ST>(T, I, w, u, L, H, DL, std::make_integer_sequence<int, 4>{});
+    rcq_level<false, GEN, 0, ST>(T, I, w, u, L, H, DL, std::make_integer_sequence<int, 8>{});
   }
 }
 

@@ -4,5 +4,5 @@ cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
 tail -2 gpurun_out/pytest_gpu.log
 [ $rc -ne 0 ] && { grep -E "FAILED|Error" gpurun_out/pytest_gpu.log | head; exit $rc; }
-CONFIG=4 ROUNDS=3 bash tools/ab_libs.sh ab_libs/libA.so ab_libs/libB.so || exit 1
-BENCH_ARGS="--n-wanted 2000 --k-wanted 667 --payload 1048576 --batch 1024 --erase 1333" ROUNDS=3 bash tools/ab_libs.sh ab_libs/libA.so ab_libs/libB.so
+CONFIG=4 ROUNDS=3 bash tools/ab_libs.sh ab_libs/libB.so ab_libs/libC.so || exit 1
+BENCH_ARGS="--n-wanted 2000 --k-wanted 667 --payload 1048576 --batch 1024 --erase 1333" ROUNDS=3 bash tools/ab_libs.sh ab_libs/libB.so ab_libs/libC.so
