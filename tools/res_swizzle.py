@@ -57,6 +57,38 @@ def conflicts(K, f):
 PRODUCT = {1024: [24, 4, 1, 2, 20, 8], 512: [28, 14, 1, 25, 20, 27]}  # kernels_res rsw<K>
 
 
+# The encode's quad items (kernels_res.hip Qi): column quad cq at position p,
+# item index 16 pi(p) + cq with pi(p) = p ^ ((p >> 4) & 1) (pi_bit = 4), or
+# the identity (pi_bit = None).  Sweeps: CQ (lane 16 u + cq, p = 64 w + 16 u
+# + i), HA' (p = (w >> 2) << 8 | j << 4 | (w & 3) << 2 | a), HD' (p = j <<
+# (logK - 4) | w << 2 | a), a = lane >> 4.
+def qi_sweeps(K):
+    W, logk = K // 64, K.bit_length() - 1
+    out = []
+    for w in range(W):
+        for i in range(16):
+            out.append([(l & 15, 64 * w + 16 * (l >> 4) + i) for l in range(64)])
+            out.append([(l & 15, ((w >> 2) << 8) | (i << 4) | ((w & 3) << 2) | (l >> 4)) for l in range(64)])
+            out.append([(l & 15, (i << (logk - 4)) | (w << 2) | (l >> 4)) for l in range(64)])
+    return out
+
+
+def qi_conflicts(K, pi_bit=4):
+    def pi(p):
+        return p if pi_bit is None else p ^ ((p >> pi_bit) & 1)
+    bad = 0
+    for lanes in qi_sweeps(K):
+        items = [16 * pi(p) + cq for cq, p in lanes]
+        assert len(set(items)) == 64 and max(items) < 16 * K
+        for h in range(2):
+            if len({x % 32 for x in items[32 * h:32 * h + 32]}) != 32:
+                bad += 1
+        for g in range(4):
+            if len({x % 16 for x in items[16 * g:16 * g + 16]}) != 16:
+                bad += 1
+    return bad
+
+
 def search(K, tries=200000, seed=1):
     rng = random.Random(seed)
     top = K // 4
@@ -74,3 +106,4 @@ if __name__ == "__main__":
             print(K, rows, "conflicting wave-instruction groups:", conflicts(K, rsw_of(rows)))
         else:
             print(K, "search:", search(K))
+        print(K, "encode quad items, conflicting wave-instruction groups:", qi_conflicts(K))
