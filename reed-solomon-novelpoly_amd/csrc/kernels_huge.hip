@@ -48,6 +48,9 @@ namespace {
 constexpr int kSK = 1024;                             // sub-transform size
 constexpr uint32_t kSlotBytes = 16u * 1024u * 8u;     // one sub-segment of a tile in thread order
 constexpr uint32_t kHDS = RGeo<kSK>::kHD;
+// Dynamic LDS of the sub-transform kernels: the tile, the CQ delta tables and
+// the RStage block of the workgroup's transform index.
+constexpr uint32_t kHugeLds = RGeo<kSK>::kTileBytes + 4u * (kDeltaWords + RStage<kSK>::kWords);
 
 struct HugeArgs {
   uint8_t* scr;         // tile slots of the slice: tile (pb, tl) at (pb tiles + tl) slots kSlotBytes
@@ -147,24 +150,29 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
   const bool nt = rows_nt(a.shards, a.batch_stride, a.shard_len);
   load_pay_tile<kSK>(tile, a.payloads + static_cast<size_t>(pb) * a.payload_stride, a.payload_len, ch0,
                      2 * static_cast<size_t>(h.K), 2 * static_cast<size_t>(I), r.tid);
+  uint32_t* DL = reinterpret_cast<uint32_t*>(smem + RGeo<kSK>::kTileBytes);
+  uint32_t* VS = DL + kDeltaWords;
+  stage_delta_tables(T, DL);
+  stage_rh_tables<kSK>(T, VS, 1, I);
+  const Qi qc = qi_coords<kSK>(r);
   __syncthreads();
   uint32_t L[16], H[16];
   rcq_read_nat<kSK>(tile, r.cqb, L, H);
   rres_store_rows(a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(ch0), a.shard_len, I,
                   a.wanted_n, L, H, r, ncols, full, nt);
   tower_convert(T, L, H);
-  rcq_levels<true, GEN>(T, I, r, L, H);
+  rcq_levels<true, GEN, true>(T, I, r, L, H, DL);
   __syncthreads();  // every wave has read its payload blocks
-  rcq_write<kSK>(tile, fresh_v(r.cqb), L, H);
+  qi_cq<true>(tile, qc, L, H);
   __syncthreads();
-  rh_read<kHA>(tile, fresh_v(r.hab), L, H);
-  ha_levels<true, GEN>(T, I, r, L, H);
+  qi_ha<false>(tile, qc, L, H);
+  ha_levels_st<kSK, true, GEN>(T, I, r, L, H, VS);
   __syncthreads();
-  rh_write<kHA>(tile, fresh_v(r.hab), L, H);
+  qi_ha<true>(tile, qc, L, H);
   __syncthreads();
-  rh_read<kHDS>(tile, fresh_v(r.hdb), L, H);
-  hd_levels<kSK, true>(T, I, L, H);
-  slot_store(slot_at(h, pb, tl, sr.u), r.tid, L, H);
+  qi_hd<kSK, false>(tile, qc, L, H);
+  hd_levels_st<kSK, true>(T, I, L, H, VS);
+  slot_store(slot_at(h, pb, tl, sr.u), r.tid, L, H);  // HD' registers in thread order
 }
 
 // Thread (tile, j, t): the coefficients of its quads, then every shift's
@@ -204,18 +212,24 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
   const Res r = res_coords<kSK>();
   const bool full = ncols == kRC && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
   const bool nt = rows_nt(a.shards, a.batch_stride, a.shard_len);
+  uint32_t* DL = reinterpret_cast<uint32_t*>(smem + RGeo<kSK>::kTileBytes);
+  uint32_t* VS = DL + kDeltaWords;
+  stage_delta_tables(T, DL);
+  stage_rh_tables<kSK>(T, VS, 1, I);
+  const Qi qc = qi_coords<kSK>(r);
   uint32_t L[16], H[16];
   slot_load(slot_at(h, pb, tl, sr.u), r.tid, L, H);
-  hd_levels<kSK, false>(T, I, L, H);
-  rh_write<kHDS>(tile, fresh_v(r.hdb), L, H);
+  __syncthreads();  // the staged tables
+  hd_levels_st<kSK, false>(T, I, L, H, VS);
+  qi_hd<kSK, true>(tile, qc, L, H);
   __syncthreads();
-  rh_read<kHA>(tile, fresh_v(r.hab), L, H);
-  ha_levels<false, GEN>(T, I, r, L, H);
+  qi_ha<false>(tile, qc, L, H);
+  ha_levels_st<kSK, false, GEN>(T, I, r, L, H, VS);
   __syncthreads();
-  rh_write<kHA>(tile, fresh_v(r.hab), L, H);
+  qi_ha<true>(tile, qc, L, H);
   __syncthreads();
-  rcq_read<kSK>(tile, fresh_v(r.cqb), L, H);
-  rcq_levels<false, GEN>(T, I, r, L, H);
+  qi_cq<false>(tile, qc, L, H);
+  rcq_levels<false, GEN, true>(T, I, r, L, H, DL);
   tower_convert(T, L, H);  // back to Cantor coordinates for the shard rows
   rres_store_rows(a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(ch0), a.shard_len, I,
                   a.wanted_n, L, H, r, ncols, full, nt);
@@ -272,12 +286,16 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
   const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);
   const bool full = ncols == kRC && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
   const Res r = res_coords<kSK>();
+  uint32_t* DL = reinterpret_cast<uint32_t*>(smem + RGeo<kSK>::kTileBytes);
+  uint32_t* VS = DL + kDeltaWords;
   uint32_t XL[16], XH[16];
   {
     const uint32_t pm = lane_rows_present(pres, I, r);
     uint2 raw[8];
     load_lane_rows<8>(raw, sh, a.shard_len, I, pm, r, ncols, full, T.zeros, 0);
     stage_row_tables_loc(tile, T, loc, pres, I, r.tid, false);
+    stage_delta_tables(T, DL);
+    stage_rh_tables<kSK>(T, VS, 1, I);
     __syncthreads();
     // premultiply (inc_reconstruct.rs:72-74; Cantor in, tower out), two halves
 #pragma unroll
@@ -292,17 +310,17 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
       }
     }
   }
-  rcq_levels<true, GEN>(T, I, r, XL, XH);
+  rcq_levels<true, GEN, true>(T, I, r, XL, XH, DL);
   __syncthreads();  // every wave has read its row tables
   rcq_write<kSK>(tile, fresh_v(r.cqb), XL, XH);
   __syncthreads();
   rh_read<kHA>(tile, fresh_v(r.hab), XL, XH);
-  ha_levels<true, GEN>(T, I, r, XL, XH);
+  ha_levels_st<kSK, true, GEN>(T, I, r, XL, XH, VS);
   __syncthreads();
   rh_write<kHA>(tile, fresh_v(r.hab), XL, XH);
   __syncthreads();
   rh_read<kHDS>(tile, fresh_v(r.hdb), XL, XH);
-  hd_levels<kSK, true>(T, I, XL, XH);
+  hd_levels_st<kSK, true>(T, I, XL, XH, VS);
   slot_store(slot_at(h, pb, tl, sr.u), r.tid, XL, XH);
   if (sr.u < h.M) {  // z = D_1024 of segment 0's sub-transform (the lifted low part of D_k)
     uint32_t AL[16], AH[16];
@@ -389,17 +407,22 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
   const Res r = res_coords<kSK>();
   uint32_t AL[16], AH[16];
   if (mode == kHugeDecode) {
+    uint32_t* DL = reinterpret_cast<uint32_t*>(smem + RGeo<kSK>::kTileBytes);
+    uint32_t* VS = DL + kDeltaWords;
+    stage_delta_tables(T, DL);
+    stage_rh_tables<kSK>(T, VS, 1, I);
     slot_load(slot_at(h, pb, tl, sr.u), r.tid, AL, AH);
-    hd_levels<kSK, false>(T, I, AL, AH);
+    __syncthreads();  // the staged tables
+    hd_levels_st<kSK, false>(T, I, AL, AH, VS);
     rh_write<kHDS>(tile, fresh_v(r.hdb), AL, AH);
     __syncthreads();
     rh_read<kHA>(tile, fresh_v(r.hab), AL, AH);
-    ha_levels<false, GEN>(T, I, r, AL, AH);
+    ha_levels_st<kSK, false, GEN>(T, I, r, AL, AH, VS);
     __syncthreads();
     rh_write<kHA>(tile, fresh_v(r.hab), AL, AH);
     __syncthreads();
     rcq_read<kSK>(tile, fresh_v(r.cqb), AL, AH);
-    rcq_levels<false, GEN>(T, I, r, AL, AH);
+    rcq_levels<false, GEN, true>(T, I, r, AL, AH, DL);
   } else {
 #pragma unroll
     for (int j = 0; j < 16; ++j) AL[j] = AH[j] = 0;
@@ -517,7 +540,7 @@ hipError_t launch_encode_huge(const DevTables& T, const EncodeArgs& a, uint8_t* 
   auto grid = [&](uint32_t u0, uint32_t u1) { return static_cast<uint32_t>(per * (u1 - u0)); };
   hipError_t e = for_gen_ranges(0, h.M, [&](auto g, uint32_t u0, uint32_t u1) {
     h.u0 = u0;
-    k_huge_enc_inv<decltype(g)::value><<<grid(u0, u1), kSK, RGeo<kSK>::kTileBytes, s>>>(T, a, h, nc);
+    k_huge_enc_inv<decltype(g)::value><<<grid(u0, u1), kSK, kHugeLds, s>>>(T, a, h, nc);
     return hipGetLastError();
   });
   const size_t units = per * 16 * kSK;
@@ -531,7 +554,7 @@ hipError_t launch_encode_huge(const DevTables& T, const EncodeArgs& a, uint8_t* 
   if (e == hipSuccess)
     e = for_gen_ranges(h.M, u_end, [&](auto g, uint32_t u0, uint32_t u1) {
       h.u0 = u0;
-      k_huge_enc_fwd<decltype(g)::value><<<grid(u0, u1), kSK, RGeo<kSK>::kTileBytes, s>>>(T, a, h, nc);
+      k_huge_enc_fwd<decltype(g)::value><<<grid(u0, u1), kSK, kHugeLds, s>>>(T, a, h, nc);
       return hipGetLastError();
     });
   return e;
@@ -563,7 +586,7 @@ hipError_t launch_reconstruct_huge(const DevTables& T, const ReconstructArgs& a,
   if (e == hipSuccess)
     e = for_gen_ranges(0, a.n / kSK, [&](auto g, uint32_t u0, uint32_t u1) {
       h.u0 = u0;
-      k_huge_rec_inv<decltype(g)::value><<<grid(u0, u1), kSK, RGeo<kSK>::kTileBytes, s>>>(T, a, h, ns);
+      k_huge_rec_inv<decltype(g)::value><<<grid(u0, u1), kSK, kHugeLds, s>>>(T, a, h, ns);
       return hipGetLastError();
     });
   const size_t units = per * 16 * kSK;
@@ -578,7 +601,7 @@ hipError_t launch_reconstruct_huge(const DevTables& T, const ReconstructArgs& a,
   if (e == hipSuccess)
     e = for_gen_ranges(0, h.M, [&](auto g, uint32_t u0, uint32_t u1) {
       h.u0 = u0;
-      k_huge_rec_fwd<decltype(g)::value><<<grid(u0, u1), kSK, RGeo<kSK>::kTileBytes, s>>>(T, a, h, ns);
+      k_huge_rec_fwd<decltype(g)::value><<<grid(u0, u1), kSK, kHugeLds, s>>>(T, a, h, ns);
       return hipGetLastError();
     });
   return e;
@@ -587,7 +610,7 @@ hipError_t launch_reconstruct_huge(const DevTables& T, const ReconstructArgs& a,
 hipError_t configure_huge_kernels() {
   hipError_t e = hipSuccess;
   auto set = [&](const void* f) {
-    const hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(RGeo<kSK>::kTileBytes));
+    const hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kHugeLds));
     if (r != hipSuccess && e == hipSuccess) e = r;
   };
   for (uint32_t g = 2; g <= 8; ++g)

@@ -6,68 +6,6 @@
 namespace np {
 namespace {
 
-// ------------------------------------------------- encode: quad items ----
-// After its payload read, the encode's tile holds quad items: column quad cq
-// (4 columns, byte-planar: exactly a CQ register pair) at position p, at byte
-// 128 pi(p) + 8 cq with pi(p) = p ^ ((p >> 4) & 1).  So the exchanges between
-// its layouts move register pairs as they are: no tr4x4 (the decode keeps the
-// planar items of res_common.hpp, whose HD layout its derivative needs).
-// Layouts besides CQ (lane 16 a + cq, a = lane bits 4-5):
-//  * HA': register j = position bits 4-7, a = bits 0-1, w & 3 = bits 2-3,
-//    w >> 2 = bits 8-9 (the HA levels' hi, as in res_common's HA);
-//  * HD': register j = position bits logK-4 .. logK-1, a = bits 0-1, w = the
-//    bits between.
-// Banks: a ds_write_b64 of 16 lanes covers one position's 128-byte row; the
-// 32-lane halves of a ds_read_b64 cover two positions that differ in bit 4
-// (CQ: u) or bit 0 (HA', HD': a), and pi puts those in opposite halves of a
-// 256-byte bank row.
-struct Qi {
-  uint32_t cqe, cqo;  // CQ: item i at (i odd ? cqo : cqe) + 128 i
-  uint32_t ha;        // HA': item j at (j odd ? ha ^ 128 : ha) + 2048 j
-  uint32_t hd;        // HD': item j at hd + (128 << (logK - 4)) j
-};
-template <int K>
-__device__ __forceinline__ Qi qi_coords(const Res& r) {
-  Qi q;
-  const uint32_t e = r.u & 1u;  // position bit 4 in CQ
-  const uint32_t cqb = 128u * (64u * r.w + 16u * r.u) + 8u * r.cq;
-  q.cqe = cqb + 128u * e;  // even i: i ^ e = i + e
-  q.cqo = cqb - 128u * e;  // odd i: i ^ e = i - e
-  q.ha = 128u * (((r.w >> 2) << 8) | ((r.w & 3u) << 2) | r.u) + 8u * r.cq;
-  const uint32_t ph = (r.w << 2) | r.u;
-  q.hd = 128u * (ph ^ ((ph >> 4) & 1u)) + 8u * r.cq;
-  return q;
-}
-template <bool WRITE>
-__device__ __forceinline__ void qi_item(uint8_t* tile, uint32_t addr, uint32_t& l, uint32_t& h) {
-  if constexpr (WRITE) {
-    *reinterpret_cast<uint2*>(tile + addr) = make_uint2(l, h);
-  } else {
-    const uint2 d = *reinterpret_cast<const uint2*>(tile + addr);
-    l = d.x;
-    h = d.y;
-  }
-}
-template <bool WRITE>
-__device__ __forceinline__ void qi_cq(uint8_t* tile, const Qi& q, uint32_t (&L)[16], uint32_t (&H)[16]) {
-  const uint32_t be = fresh_v(q.cqe), bo = fresh_v(q.cqo);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) qi_item<WRITE>(tile, ((i & 1) ? bo : be) + 128u * i, L[i], H[i]);
-}
-template <bool WRITE>
-__device__ __forceinline__ void qi_ha(uint8_t* tile, const Qi& q, uint32_t (&L)[16], uint32_t (&H)[16]) {
-  const uint32_t be = fresh_v(q.ha), bo = fresh_v(q.ha ^ 128u);
-#pragma unroll
-  for (int j = 0; j < 16; ++j) qi_item<WRITE>(tile, ((j & 1) ? bo : be) + 2048u * j, L[j], H[j]);
-}
-template <int K, bool WRITE>
-__device__ __forceinline__ void qi_hd(uint8_t* tile, const Qi& q, uint32_t (&L)[16], uint32_t (&H)[16]) {
-  constexpr uint32_t step = 128u << (RGeo<K>::kLogK - 4);
-  const uint32_t b0 = fresh_v(q.hd), b1 = fresh_v(q.hd + 8u * step);  // two bases: ds offsets < 64 KiB
-#pragma unroll
-  for (int j = 0; j < 16; ++j) qi_item<WRITE>(tile, (j < 8 ? b0 : b1) + step * (j & 7), L[j], H[j]);
-}
-
 // ---------------------------------------------------------------- encode ----
 // One workgroup: 64 chunks of one payload.  mod.rs:144-154 /
 // inc_encode.rs:15-48: IFFT(K, 0) of each chunk -> coefficients M (HD
