@@ -2,7 +2,7 @@
 for every sweep the kernels make (tools/res_swizzle.py models the CQ, HA and
 HD reads and writes and the payload tile's writes under the guide's bank
 rules), and rsw<K> in the source is the swizzle the model checks; the
-encode's quad items (kernels_res.hip Qi, pi(p) = p ^ bit 4 of p) are
+encode's quad items (res_common.hpp Qi, pi(p) = p ^ bit 4 of p) are
 conflict-free for its CQ, HA' and HD' sweeps."""
 import os
 import re
@@ -39,7 +39,7 @@ def test_model_sees_conflicts():
 
 @pytest.mark.parametrize("K", [1024, 512])
 def test_encode_quad_items_conflict_free(K):
-    src = open(os.path.join(ROOT, "reed-solomon-novelpoly_amd", "csrc", "kernels_res.hip")).read()
+    src = open(os.path.join(ROOT, "reed-solomon-novelpoly_amd", "csrc", "res_common.hpp")).read()
     assert "q.hd = 128u * (ph ^ ((ph >> 4) & 1u))" in src  # the pi of the model
     assert res_swizzle.qi_conflicts(K) == 0
     assert res_swizzle.qi_conflicts(K, pi_bit=None) > 0  # without pi the CQ reads conflict

@@ -57,7 +57,7 @@ def conflicts(K, f):
 PRODUCT = {1024: [24, 4, 1, 2, 20, 8], 512: [28, 14, 1, 25, 20, 27]}  # kernels_res rsw<K>
 
 
-# The encode's quad items (kernels_res.hip Qi): column quad cq at position p,
+# The encode's quad items (res_common.hpp Qi): column quad cq at position p,
 # item index 16 pi(p) + cq with pi(p) = p ^ ((p >> 4) & 1) (pi_bit = 4), or
 # the identity (pi_bit = None).  Sweeps: CQ (lane 16 u + cq, p = 64 w + 16 u
 # + i), HA' (p = (w >> 2) << 8 | j << 4 | (w & 3) << 2 | a), HD' (p = j <<
