@@ -145,6 +145,11 @@ def cpu_baseline(cfg, params, seconds):
         raise RuntimeError("CPU baseline harness missing: run __graft_entry__.build()")
     hc = host_cores()
     threads = hc["used"]
+    # OMP_NUM_THREADS caps it (16 on the GPU boxes, equal to their cgroup quota;
+    # rounds 1-2 used min(affinity, OMP_NUM_THREADS, 16), round 3 the quota alone)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        threads = min(threads, int(omp))
     n, k, plen, erase = params.n(), params.k(), cfg["payload"], cfg["erase"]
 
     def run(t, secs):
@@ -160,6 +165,7 @@ def cpu_baseline(cfg, params, seconds):
         "value": round(multi["gib_s"], 6),
         "unit": "GiB/s",
         "cores": threads,
+        "omp_num_threads": omp or None,
         "cores_available": hc["affinity"],
         "cpu_quota": hc["quota"],
         "kind": multi["kind"],

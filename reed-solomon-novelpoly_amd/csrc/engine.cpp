@@ -115,6 +115,10 @@ struct np_ctx {
   hipStream_t pipe_s[kPipe] = {};
   DevBuf pipe_in[kPipe], pipe_out[kPipe];
   DevBuf pipe_pres;  // the present mask of a whole host reconstruct call
+  // Pageable host reconstruct: pinned staging per slot for the present rows
+  // (gathered by host threads) and for the outputs, and the slot's last event.
+  HostBuf pipe_hin[kPipe], pipe_hout[kPipe];
+  hipEvent_t pipe_ev[kPipe] = {};
 };
 
 namespace {
@@ -200,6 +204,22 @@ bool huge_on(uint32_t k) {
   return mode == 2 || (mode == 1 && k >= 4096);
 }
 
+// The kernel family a reconstruct of (n, k, shard_len) runs on, chosen once for
+// launch_reconstruct and for rows_needed (which rows the host pipeline ships):
+// every family but the generic one has a copy mode that reads only the k
+// systematic rows when all of them are present.
+enum class RecPath { FastRes, Huge, Big, Generic };
+
+RecPath rec_path(uint32_t n, uint32_t k, size_t shard_len) {
+  if (np::fast_reconstruct_supported(n, k) || (np::res_reconstruct_supported(n, k) && np::res_enabled()))
+    return RecPath::FastRes;
+  if (np::huge_reconstruct_supported(n, k) && huge_on(k) &&
+      np::huge_reconstruct_scratch_per_payload(shard_len, n, k) <= kBigScratchCap / 2)
+    return RecPath::Huge;
+  if (np::big_reconstruct_supported(n, k)) return RecPath::Big;
+  return RecPath::Generic;
+}
+
 // Caller holds the context lock.
 hipError_t launch_encode(np_ctx* c, const np::EncodeArgs& a, hipStream_t s) {
   if (np::fast_encode_supported(a.n, a.k)) return np::launch_encode_fast(c->T, a, s);
@@ -255,8 +275,9 @@ constexpr size_t kStatusBytes = 2 * sizeof(uint32_t);  // per payload (launchers
 // go in slices.  Caller holds the context lock.
 hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream_t s) {
   const size_t own_status = a.status ? 0 : kStatusBytes;  // scratch bytes per payload for the status
-  const bool res = np::res_reconstruct_supported(a.n, a.k) && np::res_enabled();
-  if (np::fast_reconstruct_supported(a.n, a.k) || res) {
+  const RecPath path = rec_path(a.n, a.k, a.shard_len);
+  const bool res = !np::fast_reconstruct_supported(a.n, a.k);
+  if (path == RecPath::FastRes) {
     // per-payload decode rows + row multipliers and their tables (from the
     // caller's locators when given) and the status, then the decode
     const size_t stride = np::prefix_stride(a.n, a.k);
@@ -276,7 +297,7 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
     return hipSuccess;
   }
   const size_t huge_per = np::huge_reconstruct_scratch_per_payload(a.shard_len, a.n, a.k);
-  if (np::huge_reconstruct_supported(a.n, a.k) && huge_on(a.k) && huge_per <= kBigScratchCap / 2) {
+  if (path == RecPath::Huge) {
     // per payload: tile slots, mode byte, locators (unless the caller's), status
     const size_t side = 16 + (a.locators ? 0 : 2 * static_cast<size_t>(a.n)) + own_status;
     const size_t per = std::max<size_t>(1, kBigScratchCap / (huge_per + side));
@@ -295,7 +316,7 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
     }
     return hipSuccess;
   }
-  if (np::big_reconstruct_supported(a.n, a.k)) {
+  if (path == RecPath::Big) {
     // per-payload records (status, locator as row multipliers) for a slice of
     // the batch, then the decode over the resident workgroups' tile scratch
     const size_t tiles = (a.shard_len / 2 + 255) / 256;
@@ -341,6 +362,29 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
 }
 
 hipStream_t pick(np_ctx* c, void* s) { return s ? static_cast<hipStream_t>(s) : c->stream; }
+
+// f(i) for i in [0, count) on up to kHostThreads host threads (the calling
+// thread is one of them): the host side of the pageable reconstruct's gather
+// and copy-out, which move memcpy-sized row pieces.
+constexpr unsigned kHostThreads = 16;
+
+template <class F>
+void parallel_for(size_t count, F f) {
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const size_t t = std::min<size_t>({count, kHostThreads, hw});
+  if (t <= 1) {
+    for (size_t i = 0; i < count; ++i) f(i);
+    return;
+  }
+  std::vector<std::thread> pool;
+  pool.reserve(t - 1);
+  for (size_t w = 1; w < t; ++w)
+    pool.emplace_back([&, w] {
+      for (size_t i = w; i < count; i += t) f(i);
+    });
+  for (size_t i = 0; i < count; i += t) f(i);
+  for (auto& th : pool) th.join();
+}
 
 }  // namespace
 
@@ -403,10 +447,17 @@ size_t np_shard_len(const np_code_params* p, size_t payload_size) {
   return ((syms + p->k - 1) / p->k) * 2;
 }
 
+// 1 when both directions of (n, k) run specialised kernels (fast / small,
+// resident, sub-transform or big), 0 when either falls to the generic
+// LOG/EXP-gather kernels.  The sub-transform decode also needs its per-payload
+// scratch to fit (very long shards fall back); this answers for shards of
+// up to 64 KiB.
 int np_is_fast_path(const np_code_params* p) {
   if (!p) return 0;
   const uint32_t n = static_cast<uint32_t>(p->n), k = static_cast<uint32_t>(p->k);
-  return (np::fast_encode_supported(n, k) || np::big_encode_supported(n, k)) ? 1 : 0;
+  const bool enc = np::fast_encode_supported(n, k) || (np::res_encode_supported(n, k) && np::res_enabled()) ||
+                   (np::huge_encode_supported(n, k) && huge_on(k)) || np::big_encode_supported(n, k);
+  return (enc && rec_path(n, k, size_t(64) << 10) != RecPath::Generic) ? 1 : 0;
 }
 
 int np_ctx_create(int device, np_ctx** out) {
@@ -472,6 +523,9 @@ void np_ctx_destroy(np_ctx* c) {
     if (c->pipe_s[i]) (void)hipStreamSynchronize(c->pipe_s[i]);
     c->pipe_in[i].release();
     c->pipe_out[i].release();
+    c->pipe_hin[i].release();
+    c->pipe_hout[i].release();
+    if (c->pipe_ev[i]) (void)hipEventDestroy(c->pipe_ev[i]);
     if (c->pipe_s[i]) (void)hipStreamDestroy(c->pipe_s[i]);
   }
   c->pipe_pres.release();
@@ -568,16 +622,16 @@ hipError_t pipe_sync(np_ctx* c, hipError_t e) {
   return e;
 }
 
-// Rows of each payload the reconstruct kernels read: on the fast, resident and
-// big paths only the k systematic rows when all of them are present (the
-// output is those rows: kernels_fast.hip k_prefix_locator, kernels_big.hip
-// kBigCopy), otherwise -- and on the generic path -- all n rows: the
-// reference decodes from every present row (inc_reconstruct.rs:61-85).
-size_t rows_needed(const np_code_params* p, const uint8_t* present, size_t batch) {
+// Rows of each payload the reconstruct kernels read: on the fast, resident,
+// huge and big paths only the k systematic rows when all of them are present
+// (the output is those rows: kernels_fast.hip k_prefix_locator, kernels_huge.hip
+// k_huge_records, kernels_big.hip kBigCopy), otherwise -- and on the generic
+// path -- all n rows: the reference decodes from every present row
+// (inc_reconstruct.rs:61-85).  The path is the one launch_reconstruct takes
+// (rec_path), so a generic decode never reads rows that were not shipped.
+size_t rows_needed(const np_code_params* p, size_t shard_len, const uint8_t* present, size_t batch) {
   const uint32_t n = static_cast<uint32_t>(p->n), k = static_cast<uint32_t>(p->k);
-  if (!np::fast_reconstruct_supported(n, k) && !np::res_reconstruct_supported(n, k) &&
-      !np::big_reconstruct_supported(n, k) && !np::huge_reconstruct_supported(n, k))
-    return p->n;
+  if (rec_path(n, k, shard_len) == RecPath::Generic) return p->n;
   for (size_t b = 0; b < batch; ++b) {
     const uint8_t* pr = present + b * p->n;
     for (size_t v = 0; v < p->k; ++v)
@@ -656,7 +710,7 @@ int np_reconstruct_batch_host(np_ctx* c, const np_code_params* p, const uint8_t*
   if (!shards || !out || bstride < p->n * shard_len || out_stride < olen) return fail(NP_ERR_INVALID_ARGUMENT);
   if (batch == 0) return NP_OK;
   // only the rows the kernels read cross PCIe; the device stride stays n rows
-  const size_t rows = rows_needed(p, present, batch), in_bytes = rows * shard_len, dstride = p->n * shard_len;
+  const size_t rows = rows_needed(p, shard_len, present, batch), in_bytes = rows * shard_len, dstride = p->n * shard_len;
   std::lock_guard<std::mutex> g(c->mu);
   (void)hipSetDevice(c->device);
   // Pinned shards: a kernel reads only the present rows over PCIe (the
@@ -664,13 +718,47 @@ int np_reconstruct_batch_host(np_ctx* c, const np_code_params* p, const uint8_t*
   // ones go by one 2-D DMA of the first `rows` rows of every payload.  The
   // outputs go by DMA either way (the link shares badly between
   // kernel reads of host memory and any D2H, but a DMA D2H is the best of it).
-  const uint8_t* mapped = mapped_host_range(shards, (batch - 1) * bstride + in_bytes);
+  // (4-byte aligned rows only: k_copy_rows moves 16- or 4-byte pieces there;
+  // other layouts keep the DMA, which any alignment runs at full rate)
+  const bool gather_ok = ((reinterpret_cast<uintptr_t>(shards) | bstride | shard_len) & 3) == 0;
+  const uint8_t* mapped = gather_ok ? mapped_host_range(shards, (batch - 1) * bstride + in_bytes) : nullptr;
+  // Pageable shards of a decode (rows == n): host threads copy the present
+  // rows into pinned staging, from where k_copy_rows gathers them as from
+  // pinned shards; outputs come back through pinned staging as well.  Only
+  // the present rows are read from the caller's memory and cross PCIe.
+  const bool host_gather = !mapped && rows == p->n && !std::getenv("NP_NO_GATHER");
   hipError_t e = pipe_init(c);
   const size_t sb = std::min(batch, std::max<size_t>(1, kPipeSlotBytes / (in_bytes + olen)));
+  const size_t slot_in = (sb - 1) * dstride + in_bytes;
   for (int i = 0; e == hipSuccess && i < np_ctx::kPipe; ++i) {
-    e = c->pipe_in[i].ensure((sb - 1) * dstride + in_bytes);
+    e = c->pipe_in[i].ensure(slot_in);
     if (e == hipSuccess) e = c->pipe_out[i].ensure(sb * olen);
+    if (host_gather) {
+      if (e == hipSuccess) e = c->pipe_hin[i].ensure(slot_in);
+      if (e == hipSuccess) e = c->pipe_hout[i].ensure(sb * olen);
+      if (e == hipSuccess && !c->pipe_ev[i]) e = hipEventCreateWithFlags(&c->pipe_ev[i], hipEventDisableTiming);
+    }
   }
+  const uint8_t* hin_dev[np_ctx::kPipe] = {};
+  for (int i = 0; host_gather && e == hipSuccess && i < np_ctx::kPipe; ++i) {
+    hin_dev[i] = mapped_host_range(c->pipe_hin[i].as<uint8_t>(), slot_in);
+    if (!hin_dev[i]) e = hipErrorInvalidValue;  // hipHostMalloc memory is mapped
+  }
+  size_t pend_b0[np_ctx::kPipe] = {}, pend_cnt[np_ctx::kPipe] = {};  // outputs still in a slot's pinned staging
+  auto drain = [&](int sl) {  // slot sl's outputs -> the caller's buffer
+    if (!pend_cnt[sl]) return;
+    const hipError_t r = hipEventSynchronize(c->pipe_ev[sl]);
+    if (e == hipSuccess) e = r;
+    if (r == hipSuccess) {
+      const uint8_t* src = c->pipe_hout[sl].as<uint8_t>();
+      const size_t b0 = pend_b0[sl], pieces = (olen + (1u << 20) - 1) >> 20;
+      parallel_for(pend_cnt[sl] * pieces, [&](size_t i) {
+        const size_t b = i / pieces, off = (i % pieces) << 20, len = std::min<size_t>(olen - off, size_t(1) << 20);
+        std::memcpy(out + (b0 + b) * out_stride + off, src + b * olen + off, len);
+      });
+    }
+    pend_cnt[sl] = 0;
+  };
   // the whole present mask up front, synchronously: from pageable memory an
   // asynchronous copy per sub-batch would wait for its stream, and with it the
   // enqueueing of the next sub-batches
@@ -683,10 +771,26 @@ int np_reconstruct_batch_host(np_ctx* c, const np_code_params* p, const uint8_t*
     uint8_t* din = c->pipe_in[slot].as<uint8_t>();
     uint8_t* dout = c->pipe_out[slot].as<uint8_t>();
     const uint8_t* dpres = c->pipe_pres.as<uint8_t>() + b0 * p->n;
+    if (host_gather) {
+      drain(static_cast<int>(slot));  // the slot's previous sub-batch is done with its staging
+      if (e != hipSuccess) break;
+      uint8_t* hin = c->pipe_hin[slot].as<uint8_t>();
+      const size_t nrows = cnt * p->n;
+      parallel_for((nrows + 63) / 64, [&](size_t i) {  // 64 rows per task
+        for (size_t r = 64 * i; r < std::min(nrows, 64 * i + 64); ++r) {
+          const size_t b = r / p->n, v = r % p->n;
+          if (present[(b0 + b) * p->n + v])
+            std::memcpy(hin + b * dstride + v * shard_len, shards + (b0 + b) * bstride + v * shard_len, shard_len);
+        }
+      });
+      e = np::launch_copy_rows(hin_dev[slot], dstride, din, dstride, shard_len, dpres, static_cast<uint32_t>(p->n),
+                               static_cast<uint32_t>(rows), cnt, kGatherBlocks, s);
+    } else {
     e = mapped ? np::launch_copy_rows(mapped + b0 * bstride, bstride, din, dstride, shard_len, dpres,
                                       static_cast<uint32_t>(p->n), static_cast<uint32_t>(rows), cnt, kGatherBlocks, s)
                : hipMemcpy2DAsync(din, dstride, shards + b0 * bstride, bstride, in_bytes, cnt, hipMemcpyHostToDevice,
                                   s);
+    }
     if (e == hipSuccess) {
       np::ReconstructArgs a{};
       a.shards = din;
@@ -701,9 +805,17 @@ int np_reconstruct_batch_host(np_ctx* c, const np_code_params* p, const uint8_t*
       a.out_stride = olen;
       e = launch_reconstruct(c, a, s);
     }
-    if (e == hipSuccess)
+    if (host_gather) {
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(c->pipe_hout[slot].p, dout, cnt * olen, hipMemcpyDeviceToHost, s);
+      if (e == hipSuccess) e = hipEventRecord(c->pipe_ev[slot], s);
+      if (e == hipSuccess) pend_b0[slot] = b0, pend_cnt[slot] = cnt;
+    } else if (e == hipSuccess) {
       e = hipMemcpy2DAsync(out + b0 * out_stride, out_stride, dout, olen, olen, cnt, hipMemcpyDeviceToHost, s);
+    }
   }
+  // the remaining slots in submission order (a failed call still waits for its streams)
+  for (size_t i = 1; host_gather && i <= np_ctx::kPipe; ++i) drain(static_cast<int>((slot + i) % np_ctx::kPipe));
   return dev_err(pipe_sync(c, e));
 }
 

@@ -68,8 +68,8 @@ __global__ __launch_bounds__(64 * kXferWaves) void k_copy_rows(const uint8_t* __
                                                               uint32_t n, uint32_t rows, size_t chunks, size_t total) {
   const uint32_t lane = threadIdx.x & 63;
   const size_t waves = static_cast<size_t>(gridDim.x) * kXferWaves;
-  const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) | sstride | dstride |
-                     row_bytes) & 15) == 0;
+  const uintptr_t al = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) | sstride | dstride | row_bytes;
+  const bool vec = (al & 15) == 0, vec4 = (al & 3) == 0;
   for (size_t u = static_cast<size_t>(blockIdx.x) * kXferWaves + (threadIdx.x >> 6); u < total; u += waves) {
     const size_t r = u / chunks, ch = u - r * chunks;
     const size_t b = r / rows, v = r - b * rows;
@@ -90,6 +90,19 @@ __global__ __launch_bounds__(64 * kXferWaves) void k_copy_rows(const uint8_t* __
       } else {
         for (size_t i = lane; i < q; i += 64) d4[i] = s4[i];
       }
+    } else if (vec4) {  // e.g. rows of 19,532 bytes (the reference bench's 10 MB at k = 512)
+      const uint32_t* s1 = reinterpret_cast<const uint32_t*>(s);
+      uint32_t* d1 = reinterpret_cast<uint32_t*>(d);
+      const size_t q = len / 4;
+      size_t i = lane;
+      for (; i + 192 < q; i += 256) {  // four 256-byte loads in flight per wave
+        const uint32_t x0 = s1[i], x1 = s1[i + 64], x2 = s1[i + 128], x3 = s1[i + 192];
+        d1[i] = x0;
+        d1[i + 64] = x1;
+        d1[i + 128] = x2;
+        d1[i + 192] = x3;
+      }
+      for (; i < q; i += 64) d1[i] = s1[i];
     } else {
       for (size_t i = lane; i < len; i += 64) d[i] = s[i];
     }

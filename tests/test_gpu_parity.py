@@ -2,6 +2,7 @@
 the golden fixtures generated from the reference's own C build.  Bit-exact
 everywhere (integer arithmetic)."""
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -665,3 +666,39 @@ def test_host_batch_pipeline(gpu, oracle, nw, kw, plen, batch, offset, pinned):
         st, want = oracle.reconstruct(recv, n, k)
         assert st == 0 and out[b, :olen].tobytes() == want, b
         assert want[:plen] == pay[b, :plen].tobytes()
+
+
+# Every systematic row present: the host pipeline ships only the k systematic
+# rows when the kernel family it dispatches to has a copy mode (engine.cpp
+# rec_path / rows_needed).  k = 4096 (n = 16384) and 8192 (n = 32768) on the
+# sub-transform kernels, k = 1024 (n = 4096) and k = 256 (config 3).
+_SYS_CASES = [(12289, 4097, 2 * 4096 * 9, 3), (20000, 6667, 2 * 8192 * 5, 2), (4096, 1366, 2048 * 40, 2),
+              (1024, 342, 512 * 100, 3)]
+
+
+@pytest.mark.parametrize("pinned", [False, True], ids=["pageable", "pinned"])
+@pytest.mark.parametrize("nw,kw,plen,batch", _SYS_CASES)
+def test_host_pipeline_all_systematic(gpu, oracle, nw, kw, plen, batch, pinned):
+    import _pipeline_case
+
+    _pipeline_case.run(gpu, oracle, nw, kw, plen, batch, pinned)
+
+
+@pytest.mark.parametrize("env,nw,kw,plen", [("NP_HUGE=0", 12289, 4097, 2 * 4096 * 9),
+                                            ("NP_RES=0", 4096, 1366, 2048 * 40),
+                                            ("NP_HUGE=1", 6144, 2049, 2 * 2048 * 300)])
+def test_host_pipeline_all_systematic_switched(gpu, env, nw, kw, plen):
+    """The same with a kernel-family switch (read once per process, so in a
+    child process): NP_HUGE=0 sends k = 4096 to the generic kernels, which have
+    no copy mode and read all n rows -- the pipeline must then ship all of them
+    (it shipped k rows and the decode read past the slot)."""
+    import subprocess
+    import sys
+
+    key, val = env.split("=")
+    e = dict(os.environ, **{key: val})
+    script = os.path.join(os.path.dirname(__file__), "_pipeline_case.py")
+    for pinned in (0, 1):
+        r = subprocess.run([sys.executable, script, str(nw), str(kw), str(plen), "2", str(pinned)], env=e,
+                           capture_output=True, text=True, timeout=100)
+        assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (env, pinned, r.stdout[-2000:], r.stderr[-2000:])

@@ -76,6 +76,26 @@ ok = torch.equal(h_out[:, :plen], h_pay) and ok_dma
 # reads (engine.cpp rows_needed: the k systematic rows when every payload of the
 # batch has them all, else all n rows), of those only the present ones on the
 # gather path, (+ flags) in, and 2k*sl/2 out
+# pageable shards and output (numpy): the engine's host threads copy the present
+# rows into pinned staging (engine.cpp host_gather); NP_NO_GATHER=1: the runtime's
+# pageable 2-D DMA of every row (rounds 1-3)
+pg_sh = h_sh.numpy().copy()
+pg_out = np.zeros((B, olen), dtype=np.uint8)
+
+
+def rec_pageable():
+    npa.reconstruct_batch_host(p, pg_sh.ctypes.data, sl, n * sl, pres.ctypes.data, B, pg_out.ctypes.data, olen,
+                               ctx=ctx)
+
+
+t_pg = timed(rec_pageable)
+ok_pg = bool((pg_out[:, :plen] == h_pay.numpy()).all())
+pg_out[:] = 0
+os.environ["NP_NO_GATHER"] = "1"
+t_pg_dma = timed(rec_pageable)
+del os.environ["NP_NO_GATHER"]
+ok_pg = ok_pg and bool((pg_out[:, :plen] == h_pay.numpy()).all())
+ok = ok and ok_pg
 rows_dma = k if all(pres[b, :k].all() for b in range(B)) else n
 rows = float(pres[:, :rows_dma].sum()) / B
 res = {
@@ -90,6 +110,10 @@ res = {
                     "pcie_serial_bound_GiB_s": round(B * plen / (B * rows * sl / (bw_h2d * 1e9) + B * olen / (bw_d2h * 1e9)) / 2**30, 2)},
     "reconstruct_dma": {"GiB_s": round(B * plen / t_dma / 2**30, 2), "ms": round(t_dma * 1e3, 2), "rows_copied": rows_dma,
                         "pcie_bound_GiB_s": round(B * plen / max(B * rows_dma * sl / (bw_h2d * 1e9), B * olen / (bw_d2h * 1e9)) / 2**30, 2)},
+    "reconstruct_pageable": {"GiB_s": round(B * plen / t_pg / 2**30, 2), "ms": round(t_pg * 1e3, 2),
+                             "rows_copied": rows, "host_threads": min(16, os.cpu_count() or 1)},
+    "reconstruct_pageable_all_rows_dma": {"GiB_s": round(B * plen / t_pg_dma / 2**30, 2),
+                                          "ms": round(t_pg_dma * 1e3, 2), "rows_copied": rows_dma},
     "roundtrip_ok": bool(ok),
 }
 print(json.dumps(res))

@@ -90,6 +90,8 @@ if f_read8:  # per dispatch of the calibration kernels
     f_read8 /= len(next(v["FETCH_SIZE"] for i, v in cf.items() if kind(i) == "calib_read8"))
 if w_copy8:
     w_copy8 /= len(next(v["WRITE_SIZE"] for i, v in cw.items() if kind(i) == "calib_copy8"))
+if not f_read8 or not w_copy8:  # every pass measures its own correction (tools/profile_round.sh)
+    sys.exit(f"pmc_summary: no calibration counters under {src}/calib_fetch or calib_write")
 # FETCH_SIZE / WRITE_SIZE are reported in KB (1024 B) by rocprofv3
 fetch_factor = GIB / (f_read8 * 1024) if f_read8 else None
 write_factor = GIB / (w_copy8 * 1024) if w_copy8 else None

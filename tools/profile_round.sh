@@ -11,6 +11,9 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
+# the calibration kernel of the FETCH/WRITE correction: build it here if the
+# tree came without it (it is git-ignored)
+[ -x tools/microbench/calib_traffic ] || make -s -C tools/microbench calib_traffic || exit $?
 B="bench.py --no-cpu --config $CFG --steps 3 --warmup 1"
 BS="bench.py --no-cpu --config $CFG --steps 10 --warmup 3"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/stats --output-format csv -- python3 $BS > $OUT/stats.log 2>&1 &&
