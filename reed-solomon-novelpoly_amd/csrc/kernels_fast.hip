@@ -1316,6 +1316,9 @@ hipError_t launch_encode_fast(const DevTables& T, const EncodeArgs& a, hipStream
     case 64: return launch_encode_k<64>(T, a, s);
     case 128: return launch_encode_k<128>(T, a, s);
     case 256: return launch_encode_k<256>(T, a, s);
+    case 1:
+    case 2:
+    case 4:
     case 8:
     case 16:
     case 32: return launch_encode_small(T, a, s);
@@ -1330,6 +1333,9 @@ hipError_t launch_prefix_locator(const DevTables& T, const ReconstructArgs& a, u
     case 64: return by_nq<64>(a, [&](auto K, auto NQ) { return launch_prefix_k<K.value, NQ.value>(T, a, out, s); });
     case 128: return by_nq<128>(a, [&](auto K, auto NQ) { return launch_prefix_k<K.value, NQ.value>(T, a, out, s); });
     case 256: return by_nq<256>(a, [&](auto K, auto NQ) { return launch_prefix_k<K.value, NQ.value>(T, a, out, s); });
+    case 1: return by_nq<1>(a, [&](auto K, auto NQ) { return launch_prefix_k<K.value, NQ.value>(T, a, out, s); });
+    case 2: return by_nq<2>(a, [&](auto K, auto NQ) { return launch_prefix_k<K.value, NQ.value>(T, a, out, s); });
+    case 4: return by_nq<4>(a, [&](auto K, auto NQ) { return launch_prefix_k<K.value, NQ.value>(T, a, out, s); });
     case 8: return by_nq<8>(a, [&](auto K, auto NQ) { return launch_prefix_k<K.value, NQ.value>(T, a, out, s); });
     case 16: return by_nq<16>(a, [&](auto K, auto NQ) { return launch_prefix_k<K.value, NQ.value>(T, a, out, s); });
     case 32: return by_nq<32>(a, [&](auto K, auto NQ) { return launch_prefix_k<K.value, NQ.value>(T, a, out, s); });
@@ -1344,6 +1350,9 @@ hipError_t launch_reconstruct_fast(const DevTables& T, const ReconstructArgs& a,
     case 64: return by_nq<64>(a, [&](auto K, auto NQ) { return launch_reconstruct_k<K.value, NQ.value>(T, a, s); });
     case 128: return by_nq<128>(a, [&](auto K, auto NQ) { return launch_reconstruct_k<K.value, NQ.value>(T, a, s); });
     case 256: return by_nq<256>(a, [&](auto K, auto NQ) { return launch_reconstruct_k<K.value, NQ.value>(T, a, s); });
+    case 1:
+    case 2:
+    case 4:
     case 8:
     case 16:
     case 32: return launch_reconstruct_small(T, a, s);

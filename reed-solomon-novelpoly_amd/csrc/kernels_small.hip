@@ -1,7 +1,8 @@
-// Specialised gfx950 kernels for small codes: k = K in {8, 16, 32}, encode
-// for 2K <= n <= 8K, reconstruct for n in {2K, 4K, 8K} -- the shapes of 24 to
-// 191 validators (n_wanted / k_wanted ~ 3), which the generic path served at
-// ~13 GiB/s.
+// Specialised gfx950 kernels for small codes: k = K in {1, 2, 4, 8, 16, 32},
+// encode for 2K <= n <= 8K, reconstruct for n in {2K, 4K, 8K} -- the shapes
+// of 2 to 191 validators (n_wanted / k_wanted ~ 3), which the generic path
+// served at ~13 GiB/s.  K < 8: a column is 2K bytes, loaded and stored whole;
+// the 4-position blocks of the register layout are padded.
 //
 // Work mapping.  One wave owns a tile of 256 codeword columns and holds ALL K
 // positions of its lane's four columns in registers: Q[p] = the low / high
@@ -241,7 +242,26 @@ __global__ __launch_bounds__(256) void k_encode_small(DevTables T, EncodeArgs a,
     const size_t c0 = static_cast<size_t>(ch0 + 4u * lane) * 2 * K;
     const bool fast = out_vec_ok(pay, 0) &&  // 16-byte loads at any address (rows_vec_ok)
                       static_cast<size_t>(ch0 + kTile) * 2 * K <= a.payload_len;
-    if (fast) {
+    if (fast && K < 8) {  // k in {1, 2, 4}: the lane's four columns are 8K contiguous bytes
+      uint2 d[4];
+      if constexpr (K == 4) {
+        const u32x4 v0 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pay + c0));
+        const u32x4 v1 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pay + c0 + 16));
+        d[0] = make_uint2(v0.x, v0.y), d[1] = make_uint2(v0.z, v0.w), d[2] = make_uint2(v1.x, v1.y),
+        d[3] = make_uint2(v1.z, v1.w);
+      } else if constexpr (K == 2) {  // a column is one dword: positions 2, 3 of the blocks are padding
+        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pay + c0));
+        d[0] = make_uint2(v.x, 0), d[1] = make_uint2(v.y, 0), d[2] = make_uint2(v.z, 0), d[3] = make_uint2(v.w, 0);
+      } else {  // K == 1: a column is one symbol
+        const uint2 v = *reinterpret_cast<const uint2*>(pay + c0);
+        d[0] = make_uint2(v.x & 0xffffu, 0), d[1] = make_uint2(v.x >> 16, 0), d[2] = make_uint2(v.y & 0xffffu, 0),
+        d[3] = make_uint2(v.y >> 16, 0);
+      }
+      uint64_t Q4[4];
+      blks_to_q(d, Q4);
+#pragma unroll
+      for (int p = 0; p < K; ++p) M[p] = Q4[p];
+    } else if (fast) {
 #pragma unroll
       for (int u2 = 0; u2 < K / 8; ++u2) {  // positions 8u2..8u2+7: 16 bytes per column
         uint2 d0[4], d1[4];
@@ -255,19 +275,27 @@ __global__ __launch_bounds__(256) void k_encode_small(DevTables T, EncodeArgs a,
         blks_to_q(d1, &M[8 * u2 + 4]);
       }
     } else {  // the payload's last tile: bytes past payload_len are zeros (mod.rs:135-141)
+      constexpr int kBlk = K < 4 ? 1 : K / 4, kBytes = K < 4 ? 2 * K : 8;  // 8-byte blocks per column
 #pragma unroll
-      for (int u = 0; u < K / 4; ++u) {  // unrolled: M stays in registers
+      for (int u = 0; u < kBlk; ++u) {  // unrolled: M stays in registers
         uint2 d[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const size_t g0 = c0 + static_cast<size_t>(i) * 2 * K + 8u * u;
           uint32_t w[2] = {0, 0};
 #pragma unroll
-          for (int e = 0; e < 8; ++e)
+          for (int e = 0; e < kBytes; ++e)
             if (g0 + e < a.payload_len) w[e >> 2] |= static_cast<uint32_t>(pay[g0 + e]) << (8 * (e & 3));
           d[i] = make_uint2(w[0], w[1]);
         }
-        blks_to_q(d, &M[4 * u]);
+        if constexpr (K >= 4) {
+          blks_to_q(d, &M[4 * u]);
+        } else {
+          uint64_t Q4[4];
+          blks_to_q(d, Q4);
+#pragma unroll
+          for (int p = 0; p < K; ++p) M[p] = Q4[p];
+        }
       }
     }
   }
@@ -408,6 +436,32 @@ __global__ __launch_bounds__(256) void k_reconstruct_small(DevTables T, Reconstr
   uint8_t* out = a.out + static_cast<size_t>(pb) * a.out_stride + static_cast<size_t>(col0) * 2 * K;
   const bool al16 = full && out_vec_ok(a.out, a.out_stride);
   const bool al8 = NP_UNALIGNED || ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 7u) == 0;
+  if constexpr (K < 8) {  // k in {1, 2, 4}: 2K output bytes per column
+    uint64_t Q4[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int p = 0; p < K; ++p) Q4[p] = X[p];
+    uint2 d[4];
+    q_to_blks(Q4, d);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t c = 4u * lane + i;
+      uint8_t* o = out + static_cast<size_t>(c) * 2 * K;
+      if (c < ncols) {
+        if constexpr (K == 4) {
+          if (al8) {
+            *reinterpret_cast<uint2*>(o) = d[i];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = static_cast<uint8_t>((e < 4 ? d[i].x : d[i].y) >> (8 * (e & 3)));
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 2 * K; ++e) o[e] = static_cast<uint8_t>(d[i].x >> (8 * e));
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int u2 = 0; u2 < K / 8; ++u2) {
     uint2 d0[4], d1[4];
@@ -467,15 +521,18 @@ hipError_t reconstruct_by_nq(const DevTables& T, const ReconstructArgs& a, hipSt
 }  // namespace
 
 bool small_encode_supported(uint32_t n, uint32_t k) {
-  return (k == 8 || k == 16 || k == 32) && n >= 2 * k && n <= kSmallMaxSeg * k;
+  return (k == 1 || k == 2 || k == 4 || k == 8 || k == 16 || k == 32) && n >= 2 * k && n <= kSmallMaxSeg * k;
 }
 
 bool small_reconstruct_supported(uint32_t n, uint32_t k) {
-  return (k == 8 || k == 16 || k == 32) && (n == 2 * k || n == 4 * k || n == 8 * k);
+  return (k == 1 || k == 2 || k == 4 || k == 8 || k == 16 || k == 32) && (n == 2 * k || n == 4 * k || n == 8 * k);
 }
 
 hipError_t launch_encode_small(const DevTables& T, const EncodeArgs& a, hipStream_t s) {
   switch (a.k) {
+    case 1: return launch_encode_k<1>(T, a, s);
+    case 2: return launch_encode_k<2>(T, a, s);
+    case 4: return launch_encode_k<4>(T, a, s);
     case 8: return launch_encode_k<8>(T, a, s);
     case 16: return launch_encode_k<16>(T, a, s);
     case 32: return launch_encode_k<32>(T, a, s);
@@ -485,6 +542,9 @@ hipError_t launch_encode_small(const DevTables& T, const EncodeArgs& a, hipStrea
 
 hipError_t launch_reconstruct_small(const DevTables& T, const ReconstructArgs& a, hipStream_t s) {
   switch (a.k) {
+    case 1: return reconstruct_by_nq<1>(T, a, s);
+    case 2: return reconstruct_by_nq<2>(T, a, s);
+    case 4: return reconstruct_by_nq<4>(T, a, s);
     case 8: return reconstruct_by_nq<8>(T, a, s);
     case 16: return reconstruct_by_nq<16>(T, a, s);
     case 32: return reconstruct_by_nq<32>(T, a, s);

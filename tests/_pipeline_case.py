@@ -21,13 +21,31 @@ import novelpoly_amd as npa  # noqa: E402
 from novelpoly_amd import synth  # noqa: E402
 
 
+_HIP = None
+
+
 def host_array(shape, fill, pinned):
+    """A host array, pageable (numpy) or pinned (hipHostMalloc through the HIP
+    runtime, freed with the array; not torch, whose device discovery does not
+    run in the child processes of a GPU test)."""
     if not pinned:
         return np.full(shape, fill, dtype=np.uint8)
-    import torch
+    import ctypes
+    import weakref
 
-    t = torch.full((int(np.prod(shape)),), fill, dtype=torch.uint8).pin_memory()
-    return t.numpy().reshape(shape)
+    global _HIP
+    if _HIP is None:  # the HIP runtime the product library is linked to (dlsym searches its dependencies)
+        _HIP = ctypes.CDLL(npa.LIB_PATH)
+        _HIP.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+        _HIP.hipHostFree.argtypes = [ctypes.c_void_p]
+    size = int(np.prod(shape))
+    ptr = ctypes.c_void_p()
+    assert _HIP.hipHostMalloc(ctypes.byref(ptr), size, 0) == 0, "hipHostMalloc failed"
+    buf = (ctypes.c_uint8 * size).from_address(ptr.value)
+    a = np.frombuffer(buf, dtype=np.uint8).reshape(shape)
+    a[...] = fill
+    weakref.finalize(buf, _HIP.hipHostFree, ptr.value)
+    return a
 
 
 def run(ctx, oracle, nw, kw, plen, batch, pinned, seed=4100):

@@ -269,10 +269,11 @@ def test_full_size_batch_properties(gpu, oracle, cid):
 
 @pytest.mark.parametrize("batch,plen", [(40, 4 << 20), (33, 2048 * 256 * 9 - 5)])
 def test_big_path_launch_rounds(gpu, oracle, batch, plen):
-    """k = 1024 kernels over more tiles than one launch holds (launches of one
-    resident round each, kernels_big.hip): 320 tiles with an XCD-major batch and
-    297 tiles with a ragged last tile and batch % 8 != 0.  The last payload (in
-    the last, partial launch) against the oracle; every payload round-trips."""
+    """k = 1024 (config 4 shape, the resident kernels of kernels_res.hip; with
+    NP_RES=0 the scratch kernels of kernels_big.hip, test_host_pipeline_all_
+    systematic_switched) over many tiles: 320 tiles with an XCD-major batch and
+    297 tiles with a ragged last tile and batch % 8 != 0.  The last payload
+    against the oracle; every payload round-trips."""
     import torch
 
     p = npa.CodeParams.derive_parameters(4096, 1366)
@@ -366,15 +367,18 @@ def test_fast_reconstruct_shapes(gpu, oracle, nw, kw, plen, erase):
 # {2, 4, 8}, wanted_n < n (last shift partly kept), full / partial / tail tiles
 SMALL_ENC = [(100, 34, 64 * 256), (100, 34, 64 * 300 + 5), (150, 50, 64 * 512), (190, 63, 64 * 257 + 1),
              (64, 32, 64 * 256), (60, 20, 32 * 256), (90, 30, 32 * 257 + 3), (40, 14, 16 * 256),
-             (16, 8, 4096), (30, 10, 999), (24, 8, 16 * 768), (48, 16, 1), (33, 11, 16 * 256 * 5 + 9)]
+             (16, 8, 4096), (30, 10, 999), (24, 8, 16 * 768), (48, 16, 1), (33, 11, 16 * 256 * 5 + 9),
+             # k in {1, 2, 4}: 2 to 21 validators
+             (2, 1, 1000), (3, 1, 999), (4, 2, 4096), (7, 3, 5003), (9, 3, 4 * 256 * 3 + 2), (10, 4, 8 * 256 * 3),
+             (16, 6, 8 * 300 + 5), (20, 7, 65536 + 3), (13, 5, 12345), (21, 7, 1), (5, 2, 2)]
 
 
 @pytest.mark.parametrize("nw,kw,plen", SMALL_ENC)
 def test_small_encode_shapes(gpu, oracle, nw, kw, plen):
-    """Register-only encode kernels for k in {8, 16, 32}, bit-exact against the
-    oracle."""
+    """Register-only encode kernels for k in {1, 2, 4, 8, 16, 32}, bit-exact
+    against the oracle."""
     p = npa.CodeParams.derive_parameters(nw, kw)
-    assert p.k() in (8, 16, 32) and p.is_faster8()
+    assert p.k() in (1, 2, 4, 8, 16, 32) and p.is_faster8()
     pl = synth.payload(nw + plen, plen)
     got = p.make_encoder(gpu).encode(pl)
     st, want = oracle.encode(pl, p.n(), p.k(), nw)
@@ -390,14 +394,19 @@ def test_small_encode_shapes(gpu, oracle, nw, kw, plen):
                                               (60, 20, 32 * 256, 40), (90, 30, 32 * 257 + 3, 60),
                                               (40, 14, 16 * 256, 26), (40, 14, 16 * 300 + 1, -1),
                                               (16, 8, 4096, 8), (16, 8, 4096, -1), (30, 10, 999, 20),
-                                              (24, 8, 16 * 768, 16), (100, 34, 64 * 256, 0)])
+                                              (24, 8, 16 * 768, 16), (100, 34, 64 * 256, 0),
+                                              (2, 1, 1000, 1), (3, 1, 999, 2), (4, 2, 4096, 2), (7, 3, 5003, 5),
+                                              (9, 3, 4 * 256 * 3 + 2, 7), (10, 4, 8 * 256 * 3, 6),
+                                              (10, 4, 8 * 256 * 3, -1), (16, 6, 8 * 300 + 5, 12),
+                                              (20, 7, 65536 + 3, 16), (20, 7, 65536, -1), (13, 5, 12345, 0),
+                                              (4, 2, 77, -1)])
 def test_small_reconstruct_shapes(gpu, oracle, nw, kw, plen, erase):
     """Register-only reconstruct kernels for k in {8, 16, 32}, n in {2k, 4k,
     8k}: random and worst-case erasure sets (-1: every systematic shard lost),
     bit-exact against the oracle."""
     p = npa.CodeParams.derive_parameters(nw, kw)
     n, k = p.n(), p.k()
-    assert k in (8, 16, 32) and n in (2 * k, 4 * k, 8 * k)
+    assert k in (1, 2, 4, 8, 16, 32) and n in (2 * k, 4 * k, 8 * k)
     pl = synth.payload(7 * nw + plen, plen)
     shards = p.make_encoder(gpu).encode(pl)
     if erase == -1:
@@ -702,3 +711,28 @@ def test_host_pipeline_all_systematic_switched(gpu, env, nw, kw, plen):
         r = subprocess.run([sys.executable, script, str(nw), str(kw), str(plen), "2", str(pinned)], env=e,
                            capture_output=True, text=True, timeout=100)
         assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (env, pinned, r.stdout[-2000:], r.stderr[-2000:])
+
+
+# Explicit parameters with n / k >= 16 (CodeParams::derive_parameters accepts
+# any k >= 1, mod.rs:43-61; encode(bytes, n) never derives them): the encode
+# runs the specialised kernels (k = 256: kernels_fast.hip; k = 512 / 1024:
+# kernels_big.hip, their only route there), the reconstruct the generic kernels.
+@pytest.mark.parametrize("nw,kw,plen,erase", [(4096, 256, 512 * 40 + 3, 3000), (8192, 512, 1024 * 9 + 1, 7000),
+                                              (16384, 512, 1024 * 5, 15000), (16384, 1024, 2048 * 5 + 7, 14000),
+                                              (32768, 1024, 2048 * 3, 30000), (8192, 512, 1024 * 4, -1)])
+def test_explicit_wide_codes(gpu, oracle, nw, kw, plen, erase):
+    p = npa.CodeParams.derive_parameters(nw, kw)
+    n, k = p.n(), p.k()
+    assert n // k >= 16 and (n, k) == (nw, kw)
+    pl = synth.payload(nw + kw + plen, plen)
+    shards = p.make_encoder(gpu).encode(pl)
+    st, want = oracle.encode(pl, n, k, nw)
+    assert st == 0
+    bad = [v for v in range(nw) if shards[v] != want[v]]
+    assert not bad, f"{len(bad)} shards differ, first {bad[:5]}"
+    gone = set(range(k)) if erase == -1 else set(synth.erasure_indices(plen + erase, n, erase).tolist())
+    recv = [None if i in gone else s for i, s in enumerate(shards)]
+    got = p.make_encoder(gpu).reconstruct(recv)
+    st, want = oracle.reconstruct(recv, n, k)
+    assert st == 0 and got == want
+    assert got[:plen] == pl

@@ -11,3 +11,6 @@ timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu > gpurun_out/r0
 tail -1 gpurun_out/r04/bench.log | cut -c1-300
 NP_LIB_PATH=$PWD/tools/exp/lib_st64.so timeout -k 10 120 python tools/phase_stamps.py > gpurun_out/r04/stamps.log 2>&1 || exit $?
 cat gpurun_out/r04/stamps.log
+[ -x tools/microbench/bfly_rates ] || make -s -C tools/microbench bfly_rates || exit $?
+timeout -k 10 120 tools/microbench/bfly_rates > gpurun_out/r04/bfly_rates.txt 2>&1 || exit $?
+cat gpurun_out/r04/bfly_rates.txt
