@@ -629,10 +629,76 @@ __device__ __forceinline__ uint32_t seg_mask(const uint32_t (&msk)[NQ], int step
 // systematic rows (for the merge) on exit.  A runtime loop keeps
 // the kernel small; at index 0 the t = 0 multipliers are the zero element,
 // whose table yields 0 (the reference's skipped multiply).
+// NP_REC_DEFER_FOLD: the fold of step s runs at the start of step s + 1,
+// after that step's row loads are issued and before the premultiply waits for
+// them (decodes without kRowPrefetch).
+#ifndef NP_REC_DEFER_FOLD
+#define NP_REC_DEFER_FOLD 0
+#endif
+template <int NQ>
+constexpr bool kRecDeferFold = NP_REC_DEFER_FOLD && !kRowPrefetch<NQ>;
+
 template <int K, int NQ>
 __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&msk)[NQ], uint2 (&raw)[16],
                                              uint32_t (&AL)[16], uint32_t (&AH)[16], bool after_tile) {
   const DevTables& T = c.T;
+  uint32_t XL[16], XH[16];
+  // A (+)= the fold of x_q (XL / XH in the high layout) for segment q at `step`
+  auto fold = [&](int step, int q) __attribute__((always_inline)) {
+    if (NQ == 8 && q != 0) {  // A ^= kappa_q x_q (kRec8Kappa, all in GF(2^8))
+      const uint32_t kq = uniform(rec8_kappa(q));
+      if (kq == 1u) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          AL[j] ^= XL[j];
+          AH[j] ^= XH[j];
+        }
+      } else {
+        uint32_t kp[20];
+        pool_of<true>(T, kq, kp);
+        const Mult pool = make_mult(kp);
+        if (step == 0) {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) qmul_sub_set(AL[j], AH[j], XL[j], XH[j], pool);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) qmul_sub(AL[j], AH[j], XL[j], XH[j], pool);
+        }
+      }
+    } else if (step == 0) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        AL[j] = XL[j];
+        AH[j] = XH[j];
+      }
+    } else if (q == 0) {
+      if (NQ == 2 || NQ == 8) {  // kappa_0 = 1
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          AL[j] ^= XL[j];
+          AH[j] ^= XH[j];
+        }
+      }
+      add_derivative<K>(AL, XL, c.tid % Geo<K>::R);
+      add_derivative<K>(AH, XH, c.tid % Geo<K>::R);
+    } else if (NQ == 4 && q == 3) {
+      uint32_t beta[20];
+      pool_of<true>(T, 2u, beta);  // beta = Cantor(2) in GF(2^8), the t = 1 skew of level logK at index 0
+      const Mult pool = make_mult(beta);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        XL[j] ^= AL[j];
+        XH[j] ^= AH[j];
+        qmul_sub(AL[j], AH[j], XL[j], XH[j], pool);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        AL[j] ^= XL[j];
+        AH[j] ^= XH[j];
+      }
+    }
+  };
 #pragma unroll 1
   for (int step = 0; step < NQ; ++step) {
     const int q = seg_of<NQ>(step);
@@ -647,8 +713,12 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
     if constexpr (!kRowPrefetch<NQ>) {
       issue_rows(raw, (kExp & 32) ? T.zeros : sh, (kExp & 32) ? 0 : shard_len, m, index + 16 * g, T.zeros, c.lane,
                  c.ncols, c.full, q == 0);
+      // the previous step's fold runs while these rows load (kRecDeferFold)
+      if (kRecDeferFold<NQ> && step > 0) {
+        fold(step - 1, seg_of<NQ>(step - 1));
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
-    uint32_t XL[16], XH[16];
     stamp(c.dbg, 2 + 6 * step);
     pipelined_rec<16>(
         [&](auto pc) __attribute__((always_inline)) {
@@ -713,61 +783,10 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
       hi_levels<K, true, false, 0, 0>(T, vp, index, XL, XH);
     stamp(c.dbg, 6 + 6 * step);
     __builtin_amdgcn_sched_barrier(0);
-    if (NQ == 8 && q != 0) {  // A ^= kappa_q x_q (kRec8Kappa, all in GF(2^8))
-      const uint32_t kq = uniform(rec8_kappa(q));
-      if (kq == 1u) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          AL[j] ^= XL[j];
-          AH[j] ^= XH[j];
-        }
-      } else {
-        uint32_t kp[20];
-        pool_of<true>(T, kq, kp);
-        const Mult pool = make_mult(kp);
-        if (step == 0) {
-#pragma unroll
-          for (int j = 0; j < 16; ++j) qmul_sub_set(AL[j], AH[j], XL[j], XH[j], pool);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 16; ++j) qmul_sub(AL[j], AH[j], XL[j], XH[j], pool);
-        }
-      }
-    } else if (step == 0) {
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        AL[j] = XL[j];
-        AH[j] = XH[j];
-      }
-    } else if (q == 0) {
-      if (NQ == 2 || NQ == 8) {  // kappa_0 = 1
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          AL[j] ^= XL[j];
-          AH[j] ^= XH[j];
-        }
-      }
-      add_derivative<K>(AL, XL, c.tid % Geo<K>::R);
-      add_derivative<K>(AH, XH, c.tid % Geo<K>::R);
-    } else if (NQ == 4 && q == 3) {
-      uint32_t beta[20];
-      pool_of<true>(T, 2u, beta);  // beta = Cantor(2) in GF(2^8), the t = 1 skew of level logK at index 0
-      const Mult pool = make_mult(beta);
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        XL[j] ^= AL[j];
-        XH[j] ^= AH[j];
-        qmul_sub(AL[j], AH[j], XL[j], XH[j], pool);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        AL[j] ^= XL[j];
-        AH[j] ^= XH[j];
-      }
-    }
+    if (!kRecDeferFold<NQ>) fold(step, q);
     __builtin_amdgcn_sched_barrier(0);
   }
+  if constexpr (kRecDeferFold<NQ>) fold(NQ - 1, seg_of<NQ>(NQ - 1));
 }
 
 // Decode of one tile (K < 256: see kMultiTile), as rec_tiles with ntl = 1.

@@ -52,3 +52,11 @@ for a, c in zip(used, used[1:]):
     dur = st[:, :, c] - st[:, :, a]
     spread = st[:, :, c].max(axis=1) - st[:, :, c].min(axis=1)
     print(f"{names.get(c, c):>26} {dur.mean():9.0f} {dur.max(axis=1).mean():12.0f} {spread.mean():14.0f}")
+# per-wave mean durations of the phases that end without a barrier (work
+# imbalance between the waves of a workgroup; wave w runs on SIMD w % 4)
+print("per-wave mean duration (ticks), waves 0..15")
+for a, c in zip(used, used[1:]):
+    if "sync" in names.get(c, "") or "write" in names.get(c, ""):
+        continue
+    dur = (st[:, :, c] - st[:, :, a]).mean(axis=0)
+    print(f"{names.get(c, c):>26} " + " ".join(f"{v:6.0f}" for v in dur))
