@@ -285,12 +285,14 @@ __device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArg
                                              uint8_t* out, uint32_t sh, uint32_t g, uint32_t lane, uint32_t ncols,
                                              bool full, uint32_t cqb, uint32_t hb, const uint32_t (&ML)[16],
                                              const uint32_t (&MH)[16], uint32_t (&PL)[8], uint32_t (&PH)[8],
-                                             const uint8_t* dma_pay, uint32_t dma_ch0) {
+                                             const uint8_t* dma_pay, uint32_t dma_ch0, uint64_t* dbg) {
   using G = Geo<K>;
   const uint32_t index = sh * K;
   uint32_t XL[16], XH[16];
   const uint32_t* vp = VP + sh * G::kVPWords;  // the tables of every shift stay staged (kEncBuffers)
+  constexpr int st0 = 7 + 4 * (SH - 1);  // stamp slots of this shift
   shift_hi<K, SH>(T, vp, index, ML, MH, XL, XH, PL, PH);
+  stamp(dbg, st0);
   __syncthreads();  // the previous cq pass is done with the tile
   if constexpr (kEncQx<K>) {
     hi_write_q<K>(tile, g, lane, XL, XH);
@@ -305,9 +307,12 @@ __device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArg
     __syncthreads();  // every wave has its cq registers: the tile is free
     if constexpr (!(kExp & 4)) dma_tile<K>(dma_pay, dma_ch0, tile, g, lane);
   }
+  stamp(dbg, st0 + 1);
   shift_cq<K, SH>(T, vp, index, g, XL, XH);
+  stamp(dbg, st0 + 2);
   store_rows(out, a.shard_len, index + 16 * g, (kExp & 2) ? 0u : a.wanted_n, XL, XH, lane, ncols, full,
              rows_nt(a.shards, a.batch_stride, a.shard_len));
+  stamp(dbg, st0 + 3);
 }
 
 // One tile; returns whether the next tile's payload is on its way by DMA.
@@ -328,6 +333,12 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
   const uint32_t tid = fresh_v(threadIdx.x), lane = tid & 63u, g = uniform(tid >> 6);
   const bool full =
       ncols == kTile && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
+  // experiment builds (NP_EXP bit 6): s_memtime stamps past the payload's shard
+  // rows (tools/enc_stamps.py allocates batch_stride = n shard_len + 4 KiB per tile)
+  uint64_t* dbg = (kExp & 64) ? reinterpret_cast<uint64_t*>(a.shards + static_cast<size_t>(pb) * a.batch_stride +
+                                                             static_cast<size_t>(a.n) * a.shard_len + 4096u * tl)
+                              : nullptr;
+  stamp(dbg, 0);
   // whole tiles load by 8-byte vector loads at any address; the LDS-DMA of the
   // next tile's payload (4-byte pieces) only from 8-byte aligned payloads
   const bool aligned_pay = (reinterpret_cast<uintptr_t>(pay) & 7u) == 0;
@@ -371,6 +382,7 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
     for (uint32_t sh = 0; sh <= last; ++sh) stage_vpools<K, G::kThreads>(T, sh * K, VP + sh * G::kVPWords, true);
   }
   __syncthreads();
+  stamp(dbg, 1);
 
   const uint32_t cqb = col_base<K>(4 * lane) ^ (32u * g);
   {
@@ -378,8 +390,10 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
     cq_read<K>(tile, cqb, CL, CH);
     store_rows(out, a.shard_len, 16 * g, (kExp & 2) ? 0u : a.wanted_n, CL, CH, lane, ncols, full,
                rows_nt(a.shards, a.batch_stride, a.shard_len));
+    stamp(dbg, 2);
     tower_convert(T, CL, CH);  // transforms run in tower coordinates
     cq_levels<K, true, true, 0>(T, VP, 0, g, CL, CH);
+    stamp(dbg, 3);
     if constexpr (kEncQx<K>) {
       // the quad items overlay payload blocks that other waves read: wait for
       // every wave's cq_read (cq_write_p writes back only the blocks it read)
@@ -389,6 +403,7 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
       cq_write_p<K>(tile, cqb, CL, CH);
     }
   }
+  stamp(dbg, 4);
   __syncthreads();
   const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
   uint32_t ML[16], MH[16];
@@ -396,21 +411,23 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
     hi_read_q<K>(tile, g, lane, ML, MH);
   else
     hi_read_p<K>(tile, hb, ML, MH);
+  stamp(dbg, 5);
   hi_levels<K, true, true, 0, 0>(T, VP, 0, ML, MH);
 #pragma unroll
   for (int q = 0; q < 16; ++q) asm volatile("" : "+v"(ML[q]), "+v"(MH[q]));  // materialise M once
+  stamp(dbg, 6);
   uint32_t PL[8], PH[8];
   const bool dma = last >= 1 && next_tl != ~0u && tile_fast(next_tl);
   const uint8_t* dpay = dma ? pay : nullptr;
   const uint32_t dch0 = next_tl * kTile;
   if (last >= 1)
     encode_shift<K, 1>(T, a, tile, VP, out, 1, g, lane, ncols, full, cqb, hb, ML, MH, PL, PH,
-                       last == 1 ? dpay : nullptr, dch0);
+                       last == 1 ? dpay : nullptr, dch0, dbg);
   if (last >= 2)
     encode_shift<K, 2>(T, a, tile, VP, out, 2, g, lane, ncols, full, cqb, hb, ML, MH, PL, PH,
-                       last == 2 ? dpay : nullptr, dch0);
+                       last == 2 ? dpay : nullptr, dch0, dbg);
   if (last >= 3)
-    encode_shift<K, 3>(T, a, tile, VP, out, 3, g, lane, ncols, full, cqb, hb, ML, MH, PL, PH, dpay, dch0);
+    encode_shift<K, 3>(T, a, tile, VP, out, 3, g, lane, ncols, full, cqb, hb, ML, MH, PL, PH, dpay, dch0, dbg);
   return dma;
 }
 
