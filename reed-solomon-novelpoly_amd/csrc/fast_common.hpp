@@ -904,9 +904,15 @@ __device__ __forceinline__ void with_gen(uint32_t index, F&& f) {
 #define NP_CQ_NO_SKIP 0
 #endif
 // GEN: coordinates and subfield levels (kSubLevel).
-template <int K, bool INVERSE, bool INDEX0, int GEN = -1>
+// POST(t), when given, runs after group t of the forward transform's level 0
+// (rows 2t and 2t + 1 are final there).
+struct NoPost {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+template <int K, bool INVERSE, bool INDEX0, int GEN = -1, typename POST = NoPost>
 __device__ __forceinline__ void cq_levels(const DevTables& T, const uint32_t* VP, uint32_t index, uint32_t g,
-                                          uint32_t (&L)[16], uint32_t (&H)[16], uint32_t rows = ~0u) {
+                                          uint32_t (&L)[16], uint32_t (&H)[16], uint32_t rows = ~0u,
+                                          POST post = POST{}) {
   if constexpr (kExp & 1) return;
   auto cval = [&](auto fc) __attribute__((always_inline)) {
     constexpr GroupRef r = cq_group<INVERSE>(decltype(fc)::value);
@@ -939,6 +945,7 @@ __device__ __forceinline__ void cq_levels(const DevTables& T, const uint32_t* VP
       }
     };
     body(std::integral_constant<bool, kSubLevel<GEN>(r.b)>{});
+    if constexpr (!INVERSE && r.b == 0) post(r.t);
   };
   auto subf = [&](auto fc) __attribute__((always_inline)) {
     return std::integral_constant<bool, kSubLevel<GEN>(cq_group<INVERSE>(decltype(fc)::value).b)>{};

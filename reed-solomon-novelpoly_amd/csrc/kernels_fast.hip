@@ -100,6 +100,14 @@ __device__ __forceinline__ void shift_cq(const DevTables& T, const uint32_t* vp,
   }
 }
 
+// NP_ENC_STORE_SPREAD: the multi-tile encode converts and stores each pair
+// of shard rows right after its level-0 butterfly group, so the 16 row stores
+// of a wave are issued among the last level's VALU work instead of in one
+// burst after it (full tiles of 16 wanted rows; otherwise the burst).
+#ifndef NP_ENC_STORE_SPREAD
+#define NP_ENC_STORE_SPREAD 0
+#endif
+
 // The fast encodes exchange layouts through quad items (cq_write_q ..
 // hi_read_q, fast_common.hpp): no byte transposes.
 #ifndef NP_ENC_QX
@@ -308,10 +316,48 @@ __device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArg
     if constexpr (!(kExp & 4)) dma_tile<K>(dma_pay, dma_ch0, tile, g, lane);
   }
   stamp(dbg, st0 + 1);
-  shift_cq<K, SH>(T, vp, index, g, XL, XH);
-  stamp(dbg, st0 + 2);
-  store_rows(out, a.shard_len, index + 16 * g, (kExp & 2) ? 0u : a.wanted_n, XL, XH, lane, ncols, full,
-             rows_nt(a.shards, a.batch_stride, a.shard_len));
+  const uint32_t row0 = index + 16 * g;
+  const uint32_t wanted = (kExp & 2) ? 0u : a.wanted_n;
+  const bool nt = rows_nt(a.shards, a.batch_stride, a.shard_len);
+  if constexpr (NP_ENC_STORE_SPREAD) {
+    // one cq instance: rows are converted in the level-0 hook; stored there
+    // when the whole 16-row piece is wanted and the tile full, else after
+    const bool spread = full && nt && row0 + 16 <= wanted && 16 * a.shard_len < 0x7fffffffu;
+    const __amdgpu_buffer_rsrc_t r = buf_rsrc(out + static_cast<size_t>(row0) * a.shard_len,
+                                              spread ? 16 * static_cast<uint32_t>(a.shard_len) : 0u);
+    const cpool_t q = (cpool_t)(T.tower_pools) + 65536u * kPoolWords;  // tower -> Cantor (tower_convert)
+    const uint32_t sa = q[8 + 3], sb = q[8 + 4], sc = q[8 + 5];
+    const uint64_t vv = tower_conv_vhalf(q);
+    const uint32_t va = static_cast<uint32_t>(vv), vb = static_cast<uint32_t>(vv >> 32);
+    auto post = [&](int t) __attribute__((always_inline)) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int p = 2 * t + e;
+        uint32_t s0, s1, s2;
+        asm volatile(
+            "v_and_b32 %0, 0x07070707, %3\n\t"
+            "v_lshrrev_b32 %1, 3, %3\n\t"
+            "v_lshrrev_b32 %2, 6, %3\n\t"
+            "v_and_b32 %1, 0x07070707, %1\n\t"
+            "v_and_b32 %2, 0x03030303, %2"
+            : "=&v"(s0), "=&v"(s1), "=&v"(s2)
+            : "v"(XH[p]));
+        qplane_sub(XL[p], s0, s1, s2, va, vb, sa, sb, sc);
+        // a zero-size descriptor (not spread) drops the store
+        const uint2 v = cq_row(XL[p], XH[p]);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, r, 8u * lane, static_cast<uint32_t>(p * a.shard_len),
+                                              NP_ROW_STORE_CPOL);
+      }
+    };
+    static_assert(SH >= 1 && SH <= 3, "multi-tile shifts");
+    cq_levels<K, false, false, kShiftGen<K, SH>>(T, vp, index, g, XL, XH, ~0u, post);
+    stamp(dbg, st0 + 2);
+    if (!spread) store_rows(out, a.shard_len, row0, wanted, XL, XH, lane, ncols, full, nt);
+  } else {
+    shift_cq<K, SH>(T, vp, index, g, XL, XH);
+    stamp(dbg, st0 + 2);
+    store_rows(out, a.shard_len, row0, wanted, XL, XH, lane, ncols, full, nt);
+  }
   stamp(dbg, st0 + 3);
 }
 

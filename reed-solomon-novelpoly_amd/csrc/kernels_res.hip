@@ -92,6 +92,15 @@ __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4))) void k_e
   for (uint32_t sh = 4; sh < nshift && sh * K < a.wanted_n; ++sh) shift(Int<res_gen<K>(4 * K)>{}, sh);  // n = 8K
 }
 
+// Experiment builds (NP_EXP bit 6): lane 0 of every wave writes s_memtime to
+// dbg[64 wave + slot] (tools/res_stamps.py; slots: 0 start, 1 tables, 2 + 8
+// step + phase for the segment steps, 40.. the forward transform and merge).
+__device__ __forceinline__ void rstamp(uint64_t* dbg, int slot) {
+  if constexpr ((kExp & 64) != 0) {
+    if ((threadIdx.x & 63u) == 0) dbg[64u * (threadIdx.x >> 6) + slot] = __builtin_amdgcn_s_memtime();
+  }
+}
+
 // The decode's full CQ levels through per-lane full tables (rcq_group ST),
 // except in the k = 1024, 8-segment instance, where the tables' 20 VGPRs
 // made the allocator spill 60 dwords instead of 15.
@@ -112,8 +121,9 @@ template <int K, int NQ, int STEP>
 __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructArgs& a, uint8_t* tile,
                                          const uint8_t* pools, const uint8_t* pres, const uint8_t* sh,
                                          uint8_t* out_tile, uint32_t ncols, bool full, bool out16, uint32_t (&AL)[16],
-                                         uint32_t (&AH)[16]) {
+                                         uint32_t (&AH)[16], uint64_t* dbg) {
   constexpr int q = res_seg<NQ>(STEP);
+  constexpr int s0 = 2 + 8 * STEP;
   constexpr uint32_t I = static_cast<uint32_t>(q) * K;
   constexpr uint32_t kHD = RGeo<K>::kHD;
   const Res rr = res_coords<K>();  // opaque per step: lane-derived values are not hoisted across steps
@@ -125,6 +135,7 @@ __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructAr
     __syncthreads();  // the previous step's HD read is done with the tile
     stage_row_tables(tile, pools, pres, I, rr.tid, false);
     __syncthreads();
+    rstamp(dbg, s0);
     // premultiply by the row multipliers (inc_reconstruct.rs:72-74; Cantor
     // in, tower out), in two halves of 8 rows (register pressure)
 #pragma unroll
@@ -139,6 +150,7 @@ __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructAr
       }
     }
   }
+  rstamp(dbg, s0 + 1);
   if constexpr ((kExp & 16384) != 0 && STEP == 0) {  // experiment: the first step's premultiplied rows
     res_copy_out<K>(out_tile, XL, XH, rr, ncols, out16);
     return false;
@@ -149,17 +161,22 @@ __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructAr
     res_copy_out<K>(out_tile, XL, XH, rr, ncols, out16);
     return false;
   }
+  rstamp(dbg, s0 + 2);
   __syncthreads();  // every wave has read its row tables
   rcq_write<K>(tile, fresh_v(rr.cqb), XL, XH);
   __syncthreads();
   rh_read<kHA>(tile, fresh_v(rr.hab), XL, XH);
+  rstamp(dbg, s0 + 3);
   const uint32_t* vs = DL + kDeltaWords + q * RStage<K>::kWords;
   ha_levels_st<K, true, res_gen<K>(I)>(T, I, rr, XL, XH, vs);
+  rstamp(dbg, s0 + 4);
   __syncthreads();
   rh_write<kHA>(tile, fresh_v(rr.hab), XL, XH);
   __syncthreads();
   rh_read<kHD>(tile, fresh_v(rr.hdb), XL, XH);
+  rstamp(dbg, s0 + 5);
   hd_levels_st<K, true>(T, I, XL, XH, vs);
+  rstamp(dbg, s0 + 6);
   // fold x_q into d (kernels_fast.hip rec_segments)
   if constexpr (NQ == 8 && q != 0 && rec8_kappa_res(q) != 1u) {  // d ^= kappa_q x_q, kappa_q in GF(16)
     uint32_t kp[20];
@@ -196,6 +213,7 @@ __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructAr
 #pragma unroll
     for (int j = 0; j < 16; ++j) AL[j] ^= XL[j], AH[j] ^= XH[j];
   }
+  rstamp(dbg, s0 + 7);
   return true;
 }
 
@@ -203,8 +221,9 @@ template <int K, int NQ, int... STEP>
 __device__ __forceinline__ bool res_sweep(const DevTables& T, const ReconstructArgs& a, uint8_t* tile,
                                           const uint8_t* pools, const uint8_t* pres, const uint8_t* sh,
                                           uint8_t* out_tile, uint32_t ncols, bool full, bool out16,
-                                          uint32_t (&AL)[16], uint32_t (&AH)[16], std::integer_sequence<int, STEP...>) {
-  return (res_step<K, NQ, STEP>(T, a, tile, pools, pres, sh, out_tile, ncols, full, out16, AL, AH) && ...);
+                                          uint32_t (&AL)[16], uint32_t (&AH)[16], uint64_t* dbg,
+                                          std::integer_sequence<int, STEP...>) {
+  return (res_step<K, NQ, STEP>(T, a, tile, pools, pres, sh, out_tile, ncols, full, out16, AL, AH, dbg) && ...);
 }
 
 // One tile; NQ segments of K rows (a.n = NQ * K, or a trusted 2-segment
@@ -212,13 +231,16 @@ __device__ __forceinline__ bool res_sweep(const DevTables& T, const ReconstructA
 template <int K, int NQ>
 __device__ __forceinline__ void res_decode_tile(const DevTables& T, const ReconstructArgs& a, uint8_t* tile,
                                                 const uint8_t* pools, const uint8_t* pres, const uint8_t* sh,
-                                                uint8_t* out_tile, uint32_t ncols, bool full, bool out16) {
+                                                uint8_t* out_tile, uint32_t ncols, bool full, bool out16,
+                                                uint64_t* dbg) {
   uint32_t AL[16], AH[16];
   uint32_t* DL = reinterpret_cast<uint32_t*>(tile + RGeo<K>::kTileBytes);  // CQ delta tables
   uint32_t* VS = DL + kDeltaWords;                                      // RStage blocks 0..NQ-1
+  rstamp(dbg, 0);
   stage_delta_tables(T, DL);  // the first step's barriers order both
   stage_rh_tables<K>(T, VS, NQ);
-  if (!res_sweep<K, NQ>(T, a, tile, pools, pres, sh, out_tile, ncols, full, out16, AL, AH,
+  rstamp(dbg, 1);
+  if (!res_sweep<K, NQ>(T, a, tile, pools, pres, sh, out_tile, ncols, full, out16, AL, AH, dbg,
                      std::make_integer_sequence<int, NQ>{}))
     return;
   constexpr uint32_t kHD = RGeo<K>::kHD, lpc = RGeo<K>::kLPC;
@@ -234,16 +256,21 @@ __device__ __forceinline__ void res_decode_tile(const DevTables& T, const Recons
   }
   // ---- out = FFT(K, 0)(d), first k rows (inc_reconstruct.rs:80)
   hd_levels_st<K, false>(T, 0, AL, AH, VS);
+  rstamp(dbg, 40);
   __syncthreads();  // the last step's HD read is done
   rh_write<kHD>(tile, fresh_v(r.hdb), AL, AH);
   __syncthreads();
   rh_read<kHA>(tile, fresh_v(r.hab), AL, AH);
+  rstamp(dbg, 41);
   ha_levels_st<K, false>(T, 0, r, AL, AH, VS);
+  rstamp(dbg, 42);
   __syncthreads();
   rh_write<kHA>(tile, fresh_v(r.hab), AL, AH);
   __syncthreads();
   rcq_read<K>(tile, fresh_v(r.cqb), AL, AH);
+  rstamp(dbg, 43);
   rcq_levels<false, res_gen<K>(0), kRecDeltaST<K, NQ>>(T, 0, r, AL, AH, DL);
+  rstamp(dbg, 44);
   // ---- merge: received systematic rows, postmultiplied recovered ones
   // (inc_reconstruct.rs:46-50, :82-84; tower in, Cantor out)
   const uint32_t pm = lane_rows_present(pres, 0, r);
@@ -252,6 +279,7 @@ __device__ __forceinline__ void res_decode_tile(const DevTables& T, const Recons
   __syncthreads();  // every wave has read the tile
   stage_row_tables(tile, pools, pres, 0, r.tid, true);
   __syncthreads();
+  rstamp(dbg, 45);
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     uint32_t l, h;
@@ -264,7 +292,9 @@ __device__ __forceinline__ void res_decode_tile(const DevTables& T, const Recons
     AL[i] = l;
     AH[i] = h;
   }
+  rstamp(dbg, 46);
   res_copy_out<K>(out_tile, AL, AH, r, ncols, out16);
+  rstamp(dbg, 47);
 }
 
 // Every systematic row present: the output is those rows (inc_reconstruct.rs:46-50).
@@ -303,10 +333,15 @@ __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4))) void k_r
   const bool full =
       ncols == kRC && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
   const bool out16 = out_vec_ok(a.out, a.out_stride);
+  // experiment builds (NP_EXP bit 6): stamps past the payload's output
+  // (tools/res_stamps.py allocates out_stride = output + 8 KiB per tile)
+  uint64_t* dbg = (kExp & 64) ? reinterpret_cast<uint64_t*>(a.out + static_cast<size_t>(pb) * a.out_stride +
+                                                             static_cast<size_t>(nsyms) * 2 * K + 8192u * tl)
+                              : nullptr;
   if constexpr (SERVE == 1)
     res_copy_tile<K>(a, sh, out_tile, ncols, full, out16, T);
   else
-    res_decode_tile<K, SERVE>(T, a, smem, pools, pres, sh, out_tile, ncols, full, out16);
+    res_decode_tile<K, SERVE>(T, a, smem, pools, pres, sh, out_tile, ncols, full, out16, dbg);
 }
 
 }  // namespace

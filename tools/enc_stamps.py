@@ -51,3 +51,10 @@ for a, c in zip(used, used[1:]):
     print(f"{names.get(c, c):>40} {dur.mean():9.0f} {100 * dur.mean() / tot:5.1f}% {dur.max(axis=1).mean():12.0f} "
           f"{spread.mean():14.0f}")
 # tile-to-tile: start of the next tile of the same workgroup vs this tile's end
+# per-wave mean durations (wave w runs on SIMD w % 4; a SIMD favours its
+# older waves, so waves 12-15 run last on each SIMD: their barrier phases are
+# the SIMD's idle time)
+print("per-wave mean duration (ticks), waves 0..15")
+for a, c in zip(used, used[1:]):
+    dur = (st[:, :, c] - st[:, :, a]).mean(axis=0)
+    print(f"{names.get(c, c):>40} " + " ".join(f"{v:6.0f}" for v in dur))
