@@ -688,6 +688,27 @@ const uint8_t* mapped_host_range(const uint8_t* p, size_t bytes) {
   return d0;
 }
 
+// Pins the pages of [p, p + bytes) in place and maps them for the device
+// (hipHostRegister); returns the registered base for unpin, or nullptr when the
+// runtime refuses (the range overlaps a registered one, ...).
+void* pin_range(const void* p, size_t bytes) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p) & ~uintptr_t(4095);
+  const uintptr_t z = (reinterpret_cast<uintptr_t>(p) + bytes + 4095) & ~uintptr_t(4095);
+  if (hipHostRegister(reinterpret_cast<void*>(a), z - a, hipHostRegisterMapped) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return reinterpret_cast<void*>(a);
+}
+
+// How pageable buffers of the host reconstruct go: "pin" (default) registers
+// them for the call, "gather" copies the present rows into pinned staging on
+// host threads (NP_PAGEABLE).
+bool pageable_pin() {
+  const char* m = std::getenv("NP_PAGEABLE");
+  return !m || std::strcmp(m, "gather") != 0;
+}
+
 }  // namespace
 
 int np_encode_batch_host(np_ctx* c, const np_code_params* p, const uint8_t* payloads, size_t len, size_t pstride,
@@ -701,6 +722,15 @@ int np_encode_batch_host(np_ctx* c, const np_code_params* p, const uint8_t* payl
   if (batch == 0) return NP_OK;
   std::lock_guard<std::mutex> g(c->mu);
   (void)hipSetDevice(c->device);
+  // pageable buffers pinned in place for the call (NP_PAGEABLE=pin): the
+  // copies then run as DMA from / to pinned memory, at the PCIe rate
+  const size_t span_in = (batch - 1) * pstride + len, span_out = (batch - 1) * bstride + row_bytes;
+  void* pinned_in = nullptr;
+  void* pinned_out = nullptr;
+  if (pageable_pin()) {
+    if (!mapped_host_range(payloads, span_in)) pinned_in = pin_range(payloads, span_in);
+    if (!mapped_host_range(shards, span_out)) pinned_out = pin_range(shards, span_out);
+  }
   hipError_t e = pipe_init(c);
   const size_t sb = std::min(batch, std::max<size_t>(1, kPipeSlotBytes / (len + row_bytes)));
   for (int i = 0; e == hipSuccess && i < np_ctx::kPipe; ++i) {
@@ -718,7 +748,10 @@ int np_encode_batch_host(np_ctx* c, const np_code_params* p, const uint8_t* payl
     if (e == hipSuccess)
       e = hipMemcpy2DAsync(shards + b0 * bstride, bstride, dout, row_bytes, row_bytes, cnt, hipMemcpyDeviceToHost, s);
   }
-  return dev_err(pipe_sync(c, e));
+  e = pipe_sync(c, e);
+  if (pinned_in) (void)hipHostUnregister(pinned_in);
+  if (pinned_out) (void)hipHostUnregister(pinned_out);
+  return dev_err(e);
 }
 
 int np_reconstruct_batch_host(np_ctx* c, const np_code_params* p, const uint8_t* shards, size_t shard_len,
@@ -748,12 +781,28 @@ int np_reconstruct_batch_host(np_ctx* c, const np_code_params* p, const uint8_t*
   // (4-byte aligned rows only: k_copy_rows moves 16- or 4-byte pieces there;
   // other layouts keep the DMA, which any alignment runs at full rate)
   const bool gather_ok = ((reinterpret_cast<uintptr_t>(shards) | bstride | shard_len) & 3) == 0;
-  const uint8_t* mapped = gather_ok ? mapped_host_range(shards, (batch - 1) * bstride + in_bytes) : nullptr;
+  const size_t span_in = (batch - 1) * bstride + in_bytes, span_out = (batch - 1) * out_stride + olen;
+  const uint8_t* mapped = gather_ok ? mapped_host_range(shards, span_in) : nullptr;
+  // Pageable buffers pinned in place for the call (NP_PAGEABLE=pin): the
+  // gather kernel then reads the present rows of the caller's own shards, and
+  // the outputs go by DMA straight into the caller's buffer
+  void* pinned_in = nullptr;
+  void* pinned_out = nullptr;
+  if (gather_ok && !mapped && !std::getenv("NP_NO_GATHER") && pageable_pin()) {
+    pinned_in = pin_range(shards, span_in);
+    if (pinned_in) mapped = mapped_host_range(shards, span_in);
+    if (mapped && !mapped_host_range(out, span_out)) pinned_out = pin_range(out, span_out);
+  }
   // Pageable shards of a decode (rows == n): host threads copy the present
   // rows into pinned staging, from where k_copy_rows gathers them as from
   // pinned shards; outputs come back through pinned staging as well.  Only
   // the present rows are read from the caller's memory and cross PCIe.
   const bool host_gather = !mapped && rows == p->n && !std::getenv("NP_NO_GATHER");
+  // Outputs of the staged pageable path: through pinned staging and host
+  // threads, or (NP_PAGEABLE_OUT=direct) by the runtime's pageable D2H, which
+  // measured slower in the pipeline (profiles/r04_e2e_cfg4.json).
+  const char* pout = std::getenv("NP_PAGEABLE_OUT");
+  const bool staged_out = host_gather && !(pout && std::strcmp(pout, "direct") == 0);
   hipError_t e = pipe_init(c);
   const size_t sb = std::min(batch, std::max<size_t>(1, kPipeSlotBytes / (in_bytes + olen)));
   const size_t slot_in = (sb - 1) * dstride + in_bytes;
@@ -762,7 +811,7 @@ int np_reconstruct_batch_host(np_ctx* c, const np_code_params* p, const uint8_t*
     if (e == hipSuccess) e = c->pipe_out[i].ensure(sb * olen);
     if (host_gather) {
       if (e == hipSuccess) e = c->pipe_hin[i].ensure(slot_in);
-      if (e == hipSuccess) e = c->pipe_hout[i].ensure(sb * olen);
+      if (e == hipSuccess && staged_out) e = c->pipe_hout[i].ensure(sb * olen);
       if (e == hipSuccess && !c->pipe_ev[i]) e = hipEventCreateWithFlags(&c->pipe_ev[i], hipEventDisableTiming);
     }
   }
@@ -771,12 +820,14 @@ int np_reconstruct_batch_host(np_ctx* c, const np_code_params* p, const uint8_t*
     hin_dev[i] = mapped_host_range(c->pipe_hin[i].as<uint8_t>(), slot_in);
     if (!hin_dev[i]) e = hipErrorInvalidValue;  // hipHostMalloc memory is mapped
   }
-  size_t pend_b0[np_ctx::kPipe] = {}, pend_cnt[np_ctx::kPipe] = {};  // outputs still in a slot's pinned staging
-  auto drain = [&](int sl) {  // slot sl's outputs -> the caller's buffer
+  // pend_cnt[sl]: payloads of slot sl whose pinned staging is still in use
+  // (the gather kernel, and with staged outputs the D2H into pipe_hout)
+  size_t pend_b0[np_ctx::kPipe] = {}, pend_cnt[np_ctx::kPipe] = {};
+  auto drain = [&](int sl) {  // slot sl's staging is free again (its outputs -> the caller's buffer)
     if (!pend_cnt[sl]) return;
     const hipError_t r = hipEventSynchronize(c->pipe_ev[sl]);
     if (e == hipSuccess) e = r;
-    if (r == hipSuccess) {
+    if (r == hipSuccess && staged_out) {
       const uint8_t* src = c->pipe_hout[sl].as<uint8_t>();
       const size_t b0 = pend_b0[sl], pieces = (olen + (1u << 20) - 1) >> 20;
       parallel_for(pend_cnt[sl] * pieces, [&](size_t i) {
@@ -812,6 +863,10 @@ int np_reconstruct_batch_host(np_ctx* c, const np_code_params* p, const uint8_t*
       });
       e = np::launch_copy_rows(hin_dev[slot], dstride, din, dstride, shard_len, dpres, static_cast<uint32_t>(p->n),
                                static_cast<uint32_t>(rows), cnt, kGatherBlocks, s);
+      if (!staged_out) {  // the input staging is free once the gather kernel is done
+        if (e == hipSuccess) e = hipEventRecord(c->pipe_ev[slot], s);
+        if (e == hipSuccess) pend_b0[slot] = b0, pend_cnt[slot] = cnt;
+      }
     } else {
     e = mapped ? np::launch_copy_rows(mapped + b0 * bstride, bstride, din, dstride, shard_len, dpres,
                                       static_cast<uint32_t>(p->n), static_cast<uint32_t>(rows), cnt, kGatherBlocks, s)
@@ -832,7 +887,7 @@ int np_reconstruct_batch_host(np_ctx* c, const np_code_params* p, const uint8_t*
       a.out_stride = olen;
       e = launch_reconstruct(c, a, s);
     }
-    if (host_gather) {
+    if (staged_out) {
       if (e == hipSuccess)
         e = hipMemcpyAsync(c->pipe_hout[slot].p, dout, cnt * olen, hipMemcpyDeviceToHost, s);
       if (e == hipSuccess) e = hipEventRecord(c->pipe_ev[slot], s);
@@ -843,7 +898,10 @@ int np_reconstruct_batch_host(np_ctx* c, const np_code_params* p, const uint8_t*
   }
   // the remaining slots in submission order (a failed call still waits for its streams)
   for (size_t i = 1; host_gather && i <= np_ctx::kPipe; ++i) drain(static_cast<int>((slot + i) % np_ctx::kPipe));
-  return dev_err(pipe_sync(c, e));
+  e = pipe_sync(c, e);
+  if (pinned_in) (void)hipHostUnregister(pinned_in);
+  if (pinned_out) (void)hipHostUnregister(pinned_out);
+  return dev_err(e);
 }
 
 // ---------------------------------------------------------- reconstruct ----

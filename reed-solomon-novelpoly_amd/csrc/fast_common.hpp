@@ -956,9 +956,16 @@ __device__ __forceinline__ void cq_levels(const DevTables& T, const uint32_t* VP
 // Levels 4..logK-1 in the high layout: quad j pairs with j + 2^(b-2-logR);
 // group t = j >> (b-1-logR).  FIRST > 0 starts at flat group FIRST (the
 // forward transform's top level, one group, done by the caller: fwd_top).
-template <int K, bool INVERSE, bool INDEX0, int FIRST = 0, int GEN = -1>
+// HOOK (forward transforms): hook.pre() runs before the first group of level
+// 4 (the last high level) and hook.post(t) after its group t (quads 2t and
+// 2t + 1 are final there).
+struct NoHiHook {
+  __device__ __forceinline__ void pre() const {}
+  __device__ __forceinline__ void post(int) const {}
+};
+template <int K, bool INVERSE, bool INDEX0, int FIRST = 0, int GEN = -1, typename HOOK = NoHiHook>
 __device__ __forceinline__ void hi_levels(const DevTables& T, const uint32_t* VP, uint32_t index, uint32_t (&L)[16],
-                                          uint32_t (&H)[16]) {
+                                          uint32_t (&H)[16], HOOK hook = HOOK{}) {
   if constexpr (kExp & 1) return;
   constexpr int logR = Geo<K>::kLogR;
   auto cval = [&](auto fc) __attribute__((always_inline)) {
@@ -973,6 +980,7 @@ __device__ __forceinline__ void hi_levels(const DevTables& T, const uint32_t* VP
     constexpr GroupRef r = hi_group<K, INVERSE>(decltype(fc)::value + FIRST);
     constexpr int dj = 1 << (r.b - 2 - logR);
     constexpr bool live = !INDEX0 || r.t != 0;
+    if constexpr (!INVERSE && r.b == 4 && r.t == 0) hook.pre();
     auto body = [&](auto sub_c) __attribute__((always_inline)) {
       constexpr bool SUB = decltype(sub_c)::value;
 #pragma unroll
@@ -990,6 +998,7 @@ __device__ __forceinline__ void hi_levels(const DevTables& T, const uint32_t* VP
       }
     };
     body(std::integral_constant<bool, kSubLevel<GEN>(r.b)>{});
+    if constexpr (!INVERSE && r.b == 4) hook.post(r.t);
   };
   auto subf = [&](auto fc) __attribute__((always_inline)) {
     return std::integral_constant<bool, kSubLevel<GEN>(hi_group<K, INVERSE>(decltype(fc)::value + FIRST).b)>{};

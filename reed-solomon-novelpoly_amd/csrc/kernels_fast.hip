@@ -61,10 +61,10 @@ template <int K, int SH>
 constexpr int kShiftGen = static_cast<int>(gen_of((SH == 23 ? 2 : SH) * K));
 
 // X = M, then the forward high levels of shift sh (top level included).
-template <int K, int SH>
+template <int K, int SH, typename HOOK = NoHiHook>
 __device__ __forceinline__ void shift_hi(const DevTables& T, const uint32_t* vp, uint32_t index,
                                          const uint32_t (&ML)[16], const uint32_t (&MH)[16], uint32_t (&XL)[16],
-                                         uint32_t (&XH)[16], uint32_t (&PL)[8], uint32_t (&PH)[8]) {
+                                         uint32_t (&XH)[16], uint32_t (&PL)[8], uint32_t (&PH)[8], HOOK hook = HOOK{}) {
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     XL[q] = ML[q];
@@ -83,7 +83,7 @@ __device__ __forceinline__ void shift_hi(const DevTables& T, const uint32_t* vp,
     } else {
       fwd_top<K, SH, 0>(T, vp, index, XL, XH, PL, PH);
     }
-    hi_levels<K, false, false, 1, 0>(T, vp, index, XL, XH);  // hi levels: gen_of(index) <= 4
+    hi_levels<K, false, false, 1, 0>(T, vp, index, XL, XH, hook);  // hi levels: gen_of(index) <= 4
   }
 }
 
@@ -100,10 +100,19 @@ __device__ __forceinline__ void shift_cq(const DevTables& T, const uint32_t* vp,
   }
 }
 
+// NP_ENC_HIW_EARLY: the multi-tile encode writes each shift's high-layout quads
+// to LDS right after their last (level-4) butterfly group instead of after
+// the whole high pass.  Measured: encode -1.9 % at config 3 (1.686 -> 1.655
+// ms, two runs each, profiles/r04_ab.txt).
+#ifndef NP_ENC_HIW_EARLY
+#define NP_ENC_HIW_EARLY 1
+#endif
+
 // NP_ENC_STORE_SPREAD: the multi-tile encode converts and stores each pair
 // of shard rows right after its level-0 butterfly group, so the 16 row stores
 // of a wave are issued among the last level's VALU work instead of in one
 // burst after it (full tiles of 16 wanted rows; otherwise the burst).
+// Measured: encode +0.6 to +1.1 % at config 3 (profiles/r04_ab.txt): off.
 #ifndef NP_ENC_STORE_SPREAD
 #define NP_ENC_STORE_SPREAD 0
 #endif
@@ -299,14 +308,36 @@ __device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArg
   uint32_t XL[16], XH[16];
   const uint32_t* vp = VP + sh * G::kVPWords;  // the tables of every shift stay staged (kEncBuffers)
   constexpr int st0 = 7 + 4 * (SH - 1);  // stamp slots of this shift
-  shift_hi<K, SH>(T, vp, index, ML, MH, XL, XH, PL, PH);
-  stamp(dbg, st0);
-  __syncthreads();  // the previous cq pass is done with the tile
-  if constexpr (kEncQx<K>) {
+  if constexpr (NP_ENC_HIW_EARLY && kEncQx<K>) {
+    // the quads of each level-4 group go to LDS as soon as they are final,
+    // among the level's VALU work; the barrier that frees the tile (every
+    // wave's previous cq read) moves before level 4
+    uint8_t* hb0 = tile + 512u * (256u / K) * g + fresh_v(8u * lane);
+    struct Hook {
+      uint8_t* b;
+      uint32_t (&L)[16];
+      uint32_t (&H)[16];
+      __device__ __forceinline__ void pre() const { __syncthreads(); }
+      __device__ __forceinline__ void post(int t) const {
+        *reinterpret_cast<uint2*>(b + hi_q_off<K>(2 * t)) = make_uint2(L[2 * t], H[2 * t]);
+        *reinterpret_cast<uint2*>(b + hi_q_off<K>(2 * t + 1)) = make_uint2(L[2 * t + 1], H[2 * t + 1]);
+      }
+    };
+    shift_hi<K, SH>(T, vp, index, ML, MH, XL, XH, PL, PH, Hook{hb0, XL, XH});
+    stamp(dbg, st0);
+    __syncthreads();
+    cq_read_q(tile, g, lane, XL, XH);
+  } else if constexpr (kEncQx<K>) {
+    shift_hi<K, SH>(T, vp, index, ML, MH, XL, XH, PL, PH);
+    stamp(dbg, st0);
+    __syncthreads();  // the previous cq pass is done with the tile
     hi_write_q<K>(tile, g, lane, XL, XH);
     __syncthreads();
     cq_read_q(tile, g, lane, XL, XH);
   } else {
+    shift_hi<K, SH>(T, vp, index, ML, MH, XL, XH, PL, PH);
+    stamp(dbg, st0);
+    __syncthreads();  // the previous cq pass is done with the tile
     hi_write_p<K>(tile, fresh_v(hb), XL, XH);
     __syncthreads();
     cq_read_p<K>(tile, fresh_v(cqb), XL, XH);
@@ -692,6 +723,58 @@ __device__ __forceinline__ uint32_t seg_mask(const uint32_t (&msk)[NQ], int step
 // systematic rows (for the merge) on exit.  A runtime loop keeps
 // the kernel small; at index 0 the t = 0 multipliers are the zero element,
 // whose table yields 0 (the reference's skipped multiply).
+// NP_REC_ROW_DMA: full tiles of the multi-tile decode (K = 256, 4 or 8
+// segments) bring a step's rows into the LDS tile by LDS-DMA, issued while the
+// previous step's high levels run (the tile is free from its high read until
+// the next cq write); the premultiply reads them from LDS.  A wave moves
+// exactly the rows it premultiplies, so only its own vmcnt is waited for.
+// Measured: decode +3 % at config 3 (2.76 -> 2.85 ms), -0.5 % at config 2
+// (profiles/r04_ab.txt): off.  The premultiply's LDS reads and the barrier it
+// needs before the cq write cost more than the register loads' latency did.
+#ifndef NP_REC_ROW_DMA
+#define NP_REC_ROW_DMA 0
+#endif
+template <int K, int NQ>
+constexpr bool kRecRowDma = NP_REC_ROW_DMA && K == 256 && NQ >= 4;
+
+// Wave g's rows row0 .. row0 + 15 (bytes [8 lane, + 8) of each for every
+// lane: the 512 bytes of the tile's 256 columns) into tile bytes
+// [8 KiB g, + 8 KiB), row i at 512 i: two rows per buffer_load_dwordx4 ... lds
+// (lanes 0-31 row 2i, 32-63 row 2i + 1, 16 bytes each; the LDS image is
+// lane-linear).  One descriptor per row pair, built in SGPRs; a lane whose row
+// is absent gets an offset past the descriptor's range, so it reads zeros and
+// moves no bytes (as issue_rows' 0-size descriptors).  Only one address VGPR
+// is live.  M0 is set in the same statement; the caller waits with vmcnt.
+typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ void dma_rows16(uint8_t* tile, const uint8_t* sh, uint32_t shard_len, uint32_t mask,
+                                           uint32_t row0, uint32_t g, uint32_t lane) {
+  const uint32_t lds0 =
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)(tile))) + 8192u * g;
+  const uint32_t half = lane >> 5;
+  const uint32_t vrow = 16u * (lane & 31u) + half * shard_len;  // the lane's row, relative to row 2i
+  const uint32_t bits = mask >> half;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint64_t base = reinterpret_cast<uint64_t>(sh + static_cast<size_t>(row0 + 2u * i) * shard_len);
+    const u32x4s rs = {uniform(static_cast<uint32_t>(base)), uniform(static_cast<uint32_t>(base >> 32) & 0xffffu),
+                       uniform(shard_len + 512u), 0x00020000u};
+    const uint32_t vo = ((bits >> (2 * i)) & 1u) ? vrow : 0x80000000u;
+    const uint32_t dst = uniform(lds0 + 1024u * i);
+    uint32_t keep;
+    if constexpr (NT)
+      asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen nt lds\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(vo), "s"(rs), "s"(dst)
+                   : "memory");
+    else
+      asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(vo), "s"(rs), "s"(dst)
+                   : "memory");
+  }
+}
+
 // NP_REC_DEFER_FOLD: the fold of step s runs at the start of step s + 1,
 // after that step's row loads are issued and before the premultiply waits for
 // them (decodes without kRowPrefetch).
@@ -773,7 +856,13 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
     const size_t shard_len = fresh(c.shard_len);
     const uint32_t cqb = fresh_v(c.cqb), hb = fresh_v(c.hb);
     uint32_t m = uniform(seg_mask<NQ>(msk, step));
-    if constexpr (!kRowPrefetch<NQ>) {
+    const bool row_dma = kRecRowDma<K, NQ> && c.full;  // this step's rows were DMA'd into the tile
+    if (row_dma) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's own pieces
+      const uint8_t* rp = c.tile + 8192u * g + fresh_v(8u * c.lane);
+#pragma unroll
+      for (int x = 0; x < 16; ++x) raw[x] = *reinterpret_cast<const uint2*>(rp + 512u * x);
+    } else if constexpr (!kRowPrefetch<NQ>) {
       issue_rows(raw, (kExp & 32) ? T.zeros : sh, (kExp & 32) ? 0 : shard_len, m, index + 16 * g, T.zeros, c.lane,
                  c.ncols, c.full, q == 0);
       // the previous step's fold runs while these rows load (kRecDeferFold)
@@ -810,8 +899,10 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
       cq_levels<K, true, false, decltype(gc)::value>(T, vp, index, g, XL, XH, m);
     });
     stamp(c.dbg, 4 + 6 * step);
-    if (step > 0 || after_tile) {
-      __syncthreads();  // the previous high pass (or tile's copy-out) is done with the tile and the other table buffer
+    if (step > 0 || after_tile || row_dma) {
+      // the previous high pass (or tile's copy-out, or the premultiply's reads
+      // of the DMA'd rows) is done with the tile and the other table buffer
+      __syncthreads();
       if (!kRecResident<K, NQ> && step + 1 < NQ) {
         const int qn = seg_of<NQ>(step + 1);
         stage_vpools<K, Geo<K>::kThreads>(T, static_cast<uint32_t>(qn) * K, c.VP + ((step + 1) & 1) * Geo<K>::kVPWords, true);
@@ -837,6 +928,16 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
     __syncthreads();
     stamp(c.dbg, 5 + 6 * step);
     hi_read_p<K>(c.tile, hb, XL, XH);
+    if (row_dma && step + 1 < NQ) {
+      const int qn = seg_of<NQ>(step + 1);
+      __syncthreads();  // every wave has read the tile: the next step's rows may land in it
+      const uint32_t mn = uniform(seg_mask<NQ>(msk, step + 1));
+      if (qn == 0)  // segment 0's rows are read again by the merge: default policy
+        dma_rows16<false>(c.tile, sh, static_cast<uint32_t>(shard_len), mn, 16 * g, g, c.lane);
+      else
+        dma_rows16<true>(c.tile, sh, static_cast<uint32_t>(shard_len), mn, static_cast<uint32_t>(qn) * K + 16 * g, g,
+                         c.lane);
+    }
     // hi levels: gen_of(index) <= 4; segment 0 (index 0) skips the t = 0
     // groups, whose skew is the zero element (15 of the 32 quad multiplies)
     // (the 2-segment decode keeps its rows prefetch live here: no room for two instances)
@@ -1017,6 +1118,20 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
                static_cast<uint32_t>(NQ == 1 ? 0 : seg_of<NQ>(0)) * K + 16 * g0, T.zeros, tid0 & 63u, nc,
                nc == kTile && aligned);
   }
+  // kRecRowDma: tile tn's first-step rows into the LDS tile (full tiles; the
+  // caller has made sure no wave still reads the tile)
+  auto dma_step0 = [&](uint32_t tn) __attribute__((always_inline)) {
+    dma_rows16<seg_of<NQ>(0) != 0>(tile, shp + 2u * static_cast<size_t>(tn) * kTile,
+                                   static_cast<uint32_t>(fresh(a.shard_len)), uniform(fresh(msk0[0])),
+                                   static_cast<uint32_t>(seg_of<NQ>(0)) * K + 16 * fresh(g0), fresh(g0),
+                                   fresh_v(tid0) & 63u);  // (fresh: nothing of it hoisted out of the tile loop)
+  };
+  auto full_at = [&](uint32_t t) __attribute__((always_inline)) {
+    return t < ntl && tile_cols(tile_at(t)) == kTile && aligned;
+  };
+  if constexpr (kRecRowDma<K, NQ>) {
+    if (full_at(0)) dma_step0(tile_at(0));
+  }
   if constexpr (NQ > 1) {
     // multiplier tables of the first two segment transforms (indices 2K, 3K or
     // K, 0), or of all of them (kRecResident): kept for every tile
@@ -1074,6 +1189,14 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
       if constexpr (!kRowPrefetch<NQ> && NP_MERGE_EARLY == 1)  // the merge's rows load during the FFT's cq pass
         issue_rows(raw, sh, shard_len, uniform(msk[NQ - 1]), 16 * g, T.zeros, lane, ncols, full);
       cq_read<K>(tile, fresh_v(cqb), XL, XH);
+      if constexpr (kRecRowDma<K, NQ>) {
+        // the tile is free from here when the copy-out goes from registers:
+        // the next tile's first-step rows land during the merge
+        if (full && out_vec_ok(a.out, a.out_stride) && full_at(t + 1)) {
+          __syncthreads();
+          dma_step0(tile_at(t + 1));
+        }
+      }
       cq_levels<K, false, true, 0>(T, vp0, 0, g, XL, XH, ~uniform(msk[NQ - 1]));  // erased rows only
       stamp(dbg, 29);
     }
@@ -1140,6 +1263,12 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
 #pragma unroll
           for (int e = 0; e < 8; ++e) o[e] = static_cast<uint8_t>((e < 4 ? v.x : v.y) >> (8 * (e & 3)));
         }
+      }
+    }
+    if constexpr (kRecRowDma<K, NQ>) {
+      if (full_at(t + 1)) {  // the tile's LDS copy-out is done
+        __syncthreads();
+        dma_step0(tile_at(t + 1));
       }
     }
     stamp(dbg, 31);

@@ -107,6 +107,15 @@ __device__ __forceinline__ void rstamp(uint64_t* dbg, int slot) {
 template <int K, int NQ>
 constexpr bool kRecDeltaST = !(K == 1024 && NQ == 8);
 
+// NP_RES_TABLE_DMA: a segment step's row tables arrive by LDS-DMA issued
+// during the previous step's HD levels and fold (dma_row_tables), instead of
+// by loads and LDS writes between two barriers at the start of the step.
+// Measured: config-4 decode 4.37 / 4.38 ms on, 4.37 / 4.36 off (noise,
+// profiles/r04_ab.txt); kept on, it leaves the step start to the row loads.
+#ifndef NP_RES_TABLE_DMA
+#define NP_RES_TABLE_DMA 1
+#endif
+
 template <int NQ>
 __host__ __device__ constexpr int res_seg(int step) {  // segments 2, 3, 1, 0 (NQ = 4); 1, 0 (NQ = 2); 7..0 (NQ = 8)
   return NQ == 8 ? 7 - step : NQ == 4 ? (step == 0 ? 2 : step == 1 ? 3 : 3 - step) : 1 - step;
@@ -131,10 +140,19 @@ __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructAr
   {
     const uint32_t pm = lane_rows_present(pres, I, rr);
     uint2 raw[8];
-    load_lane_rows<8>(raw, sh, a.shard_len, I, pm, rr, ncols, full, T.zeros, 0);
-    __syncthreads();  // the previous step's HD read is done with the tile
-    stage_row_tables(tile, pools, pres, I, rr.tid, false);
-    __syncthreads();
+    if constexpr (NP_RES_TABLE_DMA) {
+      // this step's tables were issued by LDS-DMA during the previous step
+      // (res_decode_tile for step 0): wait for this wave's pieces before the
+      // row loads queue behind them, then for every wave's
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      load_lane_rows<8>(raw, sh, a.shard_len, I, pm, rr, ncols, full, T.zeros, 0);
+      __syncthreads();
+    } else {
+      load_lane_rows<8>(raw, sh, a.shard_len, I, pm, rr, ncols, full, T.zeros, 0);
+      __syncthreads();  // the previous step's HD read is done with the tile
+      stage_row_tables(tile, pools, pres, I, rr.tid, false);
+      __syncthreads();
+    }
     rstamp(dbg, s0);
     // premultiply by the row multipliers (inc_reconstruct.rs:72-74; Cantor
     // in, tower out), in two halves of 8 rows (register pressure)
@@ -174,6 +192,10 @@ __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructAr
   rh_write<kHA>(tile, fresh_v(rr.hab), XL, XH);
   __syncthreads();
   rh_read<kHD>(tile, fresh_v(rr.hdb), XL, XH);
+  if constexpr (NP_RES_TABLE_DMA && STEP + 1 < NQ) {
+    __syncthreads();  // every wave has read the tile: the next step's tables may land in it
+    dma_row_tables(tile, pools, static_cast<uint32_t>(res_seg<NQ>(STEP + 1)) * K, K, rr.w, rr.l, K / 64);
+  }
   rstamp(dbg, s0 + 5);
   hd_levels_st<K, true>(T, I, XL, XH, vs);
   rstamp(dbg, s0 + 6);
@@ -237,6 +259,10 @@ __device__ __forceinline__ void res_decode_tile(const DevTables& T, const Recons
   uint32_t* DL = reinterpret_cast<uint32_t*>(tile + RGeo<K>::kTileBytes);  // CQ delta tables
   uint32_t* VS = DL + kDeltaWords;                                      // RStage blocks 0..NQ-1
   rstamp(dbg, 0);
+  if constexpr (NP_RES_TABLE_DMA) {  // the first step's row tables (the tile is free at the start)
+    const Res r0 = res_coords<K>();
+    dma_row_tables(tile, pools, static_cast<uint32_t>(res_seg<NQ>(0)) * K, K, r0.w, r0.l, K / 64);
+  }
   stage_delta_tables(T, DL);  // the first step's barriers order both
   stage_rh_tables<K>(T, VS, NQ);
   rstamp(dbg, 1);
@@ -268,6 +294,10 @@ __device__ __forceinline__ void res_decode_tile(const DevTables& T, const Recons
   rh_write<kHA>(tile, fresh_v(r.hab), AL, AH);
   __syncthreads();
   rcq_read<K>(tile, fresh_v(r.cqb), AL, AH);
+  if constexpr (NP_RES_TABLE_DMA) {  // the merge's tables land during the FFT's CQ levels
+    __syncthreads();  // every wave has read the tile
+    dma_row_tables(tile, pools, 0, K, r.w, r.l, K / 64);
+  }
   rstamp(dbg, 43);
   rcq_levels<false, res_gen<K>(0), kRecDeltaST<K, NQ>>(T, 0, r, AL, AH, DL);
   rstamp(dbg, 44);
@@ -275,10 +305,16 @@ __device__ __forceinline__ void res_decode_tile(const DevTables& T, const Recons
   // (inc_reconstruct.rs:46-50, :82-84; tower in, Cantor out)
   const uint32_t pm = lane_rows_present(pres, 0, r);
   uint2 raw[16];
-  load_lane_rows(raw, sh, a.shard_len, 0, pm, r, ncols, full, T.zeros);
-  __syncthreads();  // every wave has read the tile
-  stage_row_tables(tile, pools, pres, 0, r.tid, true);
-  __syncthreads();
+  if constexpr (NP_RES_TABLE_DMA) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's table pieces
+    load_lane_rows(raw, sh, a.shard_len, 0, pm, r, ncols, full, T.zeros);
+    __syncthreads();  // every wave's
+  } else {
+    load_lane_rows(raw, sh, a.shard_len, 0, pm, r, ncols, full, T.zeros);
+    __syncthreads();  // every wave has read the tile
+    stage_row_tables(tile, pools, pres, 0, r.tid, true);
+    __syncthreads();
+  }
   rstamp(dbg, 45);
 #pragma unroll
   for (int i = 0; i < 16; ++i) {

@@ -748,6 +748,34 @@ __device__ __forceinline__ void stage_row_tables(uint8_t* tile, const uint8_t* p
   for (int i = 0; i < 5; ++i) dst[i] = v[i];
 }
 
+// The same by LDS-DMA, issued without waiting: rows row0 .. row0 + nrows - 1
+// (nrows a multiple of 16) of the payload's record into their slots, every
+// row's record table as it is (an absent row reads zeros, and a table maps
+// zero to zero, so its premultiplied row stays zero).  A 16-row group is 1280
+// contiguous record bytes = 5 pieces of 256 bytes (one global_load_lds_dword
+// per wave: LDS byte M0 + 4 lane); the waves of the workgroup take the pieces
+// in turn.  The caller waits (s_waitcnt vmcnt) and synchronises before the
+// tables are read.  Written as asm (M0 set in the same statement,
+// kernels_fast.hip dma_tile), so the compiler adds no vmcnt(0) of its own.
+__device__ __forceinline__ void dma_row_tables(uint8_t* tile, const uint8_t* pools, uint32_t row0, uint32_t nrows,
+                                               uint32_t w, uint32_t lane, uint32_t nwaves) {
+  static_assert(16 * kRowSlot == 5 * 256, "five 256-byte pieces per 16-row group");
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)(tile)));
+  const uint32_t pieces = (nrows / 16) * 5;
+  const uint8_t* src0 = pools + static_cast<size_t>(row0) * kRowSlot + 4u * lane;
+#pragma unroll 1
+  for (uint32_t pc = w; pc < pieces; pc += nwaves) {
+    const uint32_t g = pc / 5, part = pc - 5 * g;
+    const uint8_t* src = src0 + 1280u * g + 256u * part;
+    const uint32_t dst = uniform(lds0 + kRowGroup * g + 256u * part);
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(dst)
+                 : "memory");
+  }
+}
+
 // The same from the payload's locators (log form, all n rows: mul(x, log m) ==
 // x * EXP[m], inc_log_mul.rs:42-49): the tables of EXP[loc] straight from the
 // context's pools (present rows: in_pools, Cantor -> tower; erased rows:

@@ -629,15 +629,20 @@ def _host_array(shape, fill, pinned, offset=0):
     return t.numpy()[offset:].reshape(shape)  # the view's base keeps the pinned tensor alive
 
 
-@pytest.mark.parametrize("pinned", [False, True], ids=["pageable", "pinned"])
+@pytest.mark.parametrize("pinned,mode", [(False, "pin"), (False, "gather"), (True, "pin")],
+                         ids=["pageable", "pageable-gather", "pinned"])
 @pytest.mark.parametrize("nw,kw,plen,batch,offset", [(1024, 342, 512 * 256, 9, 0), (256, 86, 128 * 99 + 1, 7, 0),
                                                      (300, 100, 5000, 3, 2), (4096, 1366, 2048 * 40, 2, 0),
                                                      (1024, 342, 512 * 256, 3, 6)])
-def test_host_batch_pipeline(gpu, oracle, nw, kw, plen, batch, offset, pinned):
+def test_host_batch_pipeline(gpu, oracle, nw, kw, plen, batch, offset, pinned, mode, monkeypatch):
     """np_encode_batch_host / np_reconstruct_batch_host (host buffers, pipelined
     sub-batches over several streams) give the oracle's shards and payloads;
     strided host layouts, unaligned starts, pinned host memory (present rows
-    gathered over PCIe by a kernel) and garbage in the absent rows included."""
+    gathered over PCIe by a kernel) and garbage in the absent rows included.
+    Pageable buffers go pinned in place for the call (NP_PAGEABLE=pin, the
+    default) or through host-thread staging (NP_PAGEABLE=gather; engine.cpp
+    reads the variable per call)."""
+    monkeypatch.setenv("NP_PAGEABLE", mode)
     p = npa.CodeParams.derive_parameters(nw, kw)
     n, k = p.n(), p.k()
     sl = p.make_encoder(gpu).shard_len(plen)

@@ -76,11 +76,15 @@ ok = torch.equal(h_out[:, :plen], h_pay) and ok_dma
 # reads (engine.cpp rows_needed: the k systematic rows when every payload of the
 # batch has them all, else all n rows), of those only the present ones on the
 # gather path, (+ flags) in, and 2k*sl/2 out
-# pageable shards and output (numpy): the engine's host threads copy the present
-# rows into pinned staging (engine.cpp host_gather); NP_NO_GATHER=1: the runtime's
-# pageable 2-D DMA of every row (rounds 1-3)
+# pageable shards and output (numpy).  Default (NP_PAGEABLE=pin): the engine
+# pins them in place for the call (hipHostRegister) and goes as from pinned
+# memory; NP_PAGEABLE=gather: host threads copy the present rows into pinned
+# staging (engine.cpp host_gather), outputs back through pinned staging;
+# NP_NO_GATHER=1: the runtime's pageable 2-D DMA of every row (rounds 1-3)
 pg_sh = h_sh.numpy().copy()
 pg_out = np.zeros((B, olen), dtype=np.uint8)
+pg_pay = h_pay.numpy().copy()
+pg_enc = np.zeros((B, n * sl), dtype=np.uint8)
 
 
 def rec_pageable():
@@ -88,8 +92,17 @@ def rec_pageable():
                                ctx=ctx)
 
 
+t_enc_pg = timed(lambda: npa.encode_batch_host(p, pg_pay.ctypes.data, plen, plen, B, pg_enc.ctypes.data, n * sl,
+                                               ctx=ctx))
+wb = p.wanted_n * sl  # the rows encode writes
+ok_pg = bool((pg_enc[:, :wb] == h_sh.numpy().reshape(B, -1)[:, :wb]).all())
 t_pg = timed(rec_pageable)
-ok_pg = bool((pg_out[:, :plen] == h_pay.numpy()).all())
+ok_pg = ok_pg and bool((pg_out[:, :plen] == h_pay.numpy()).all())
+pg_out[:] = 0
+os.environ["NP_PAGEABLE"] = "gather"
+t_pg_st = timed(rec_pageable)
+del os.environ["NP_PAGEABLE"]
+ok_pg = ok_pg and bool((pg_out[:, :plen] == h_pay.numpy()).all())
 pg_out[:] = 0
 os.environ["NP_NO_GATHER"] = "1"
 t_pg_dma = timed(rec_pageable)
@@ -110,8 +123,11 @@ res = {
                     "pcie_serial_bound_GiB_s": round(B * plen / (B * rows * sl / (bw_h2d * 1e9) + B * olen / (bw_d2h * 1e9)) / 2**30, 2)},
     "reconstruct_dma": {"GiB_s": round(B * plen / t_dma / 2**30, 2), "ms": round(t_dma * 1e3, 2), "rows_copied": rows_dma,
                         "pcie_bound_GiB_s": round(B * plen / max(B * rows_dma * sl / (bw_h2d * 1e9), B * olen / (bw_d2h * 1e9)) / 2**30, 2)},
-    "reconstruct_pageable": {"GiB_s": round(B * plen / t_pg / 2**30, 2), "ms": round(t_pg * 1e3, 2),
-                             "rows_copied": rows, "host_threads": min(16, os.cpu_count() or 1)},
+    "encode_pageable_pinned_in_place": {"GiB_s": round(B * plen / t_enc_pg / 2**30, 2), "ms": round(t_enc_pg * 1e3, 2)},
+    "reconstruct_pageable_pinned_in_place": {"GiB_s": round(B * plen / t_pg / 2**30, 2), "ms": round(t_pg * 1e3, 2),
+                                             "rows_copied": rows},
+    "reconstruct_pageable_host_gather": {"GiB_s": round(B * plen / t_pg_st / 2**30, 2), "ms": round(t_pg_st * 1e3, 2),
+                                         "rows_copied": rows, "host_threads": min(16, os.cpu_count() or 1)},
     "reconstruct_pageable_all_rows_dma": {"GiB_s": round(B * plen / t_pg_dma / 2**30, 2),
                                           "ms": round(t_pg_dma * 1e3, 2), "rows_copied": rows_dma},
     "roundtrip_ok": bool(ok),
