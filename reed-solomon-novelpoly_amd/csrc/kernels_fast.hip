@@ -784,7 +784,21 @@ __device__ __forceinline__ void dma_rows16(uint8_t* tile, const uint8_t* sh, uin
 template <int NQ>
 constexpr bool kRecDeferFold = NP_REC_DEFER_FOLD && !kRowPrefetch<NQ>;
 
+// NP_REC_TILE_PREFETCH: the multi-tile decodes that load each step's rows
+// where they use them (NQ >= 4) load the next tile's first-step rows during
+// this tile's copy-out (and the first tile's before the tables are staged), as
+// the 2-segment decode does: at the tile boundary only the rows and the output
+// registers are live.  Measured (profiles/r04_ab.txt): config-3 decode
+// 2.78 -> 2.73 ms (-1.6 %); the 8-segment decode (1200 validators) +0.5 %, so
+// 4 segments only.
+#ifndef NP_REC_TILE_PREFETCH
+#define NP_REC_TILE_PREFETCH 1
+#endif
 template <int K, int NQ>
+constexpr bool kTilePrefetch = NP_REC_TILE_PREFETCH && NQ == 4 && kMultiTile<K>;
+
+// PRE0: step 0's rows are in `raw` on entry (kTilePrefetch).
+template <int K, int NQ, bool PRE0 = false>
 __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&msk)[NQ], uint2 (&raw)[16],
                                              uint32_t (&AL)[16], uint32_t (&AH)[16], bool after_tile) {
   const DevTables& T = c.T;
@@ -862,7 +876,7 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
       const uint8_t* rp = c.tile + 8192u * g + fresh_v(8u * c.lane);
 #pragma unroll
       for (int x = 0; x < 16; ++x) raw[x] = *reinterpret_cast<const uint2*>(rp + 512u * x);
-    } else if constexpr (!kRowPrefetch<NQ>) {
+    } else if (!kRowPrefetch<NQ> && !(PRE0 && step == 0)) {
       issue_rows(raw, (kExp & 32) ? T.zeros : sh, (kExp & 32) ? 0 : shard_len, m, index + 16 * g, T.zeros, c.lane,
                  c.ncols, c.full, q == 0);
       // the previous step's fold runs while these rows load (kRecDeferFold)
@@ -949,6 +963,13 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
     __builtin_amdgcn_sched_barrier(0);
     if (!kRecDeferFold<NQ>) fold(step, q);
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PRE0) {
+      // raw is reloaded at every later step: an instruction-free definition
+      // here ends its live range (the loop header's phi would otherwise keep
+      // step 0's rows live through every step)
+#pragma unroll
+      for (int x = 0; x < 16; ++x) asm volatile("" : "=v"(raw[x].x), "=v"(raw[x].y));
+    }
   }
   if constexpr (kRecDeferFold<NQ>) fold(NQ - 1, seg_of<NQ>(NQ - 1));
 }
@@ -1111,7 +1132,7 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
     return tl0 + (i >= ntl ? i - ntl : i);
   };
   uint2 raw[16];
-  if constexpr (kRowPrefetch<NQ>) {
+  if constexpr (kRowPrefetch<NQ> || kTilePrefetch<K, NQ>) {
     const uint32_t nc = tile_cols(tile_at(0));
     issue_rows(raw, (NQ > 1 && (kExp & 32)) ? T.zeros : shp + 2u * static_cast<size_t>(tile_at(0)) * kTile,
                (NQ > 1 && (kExp & 32)) ? 0 : a.shard_len, msk0[0],
@@ -1174,7 +1195,7 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
       RecCtx c{T, shard_len, tile, rows, sh, VP, g, lane, tid, ncols, full, cqb, hb, dbg};
       // t > 0: step 0 waits for the previous tile's last LDS reads (its FFT's
       // cq_read, the copy-out) before writing the tile
-      rec_segments<K, NQ>(c, msk, raw, AL, AH, t > 0 && (NQ == 2 || kRecResident<K, NQ>));
+      rec_segments<K, NQ, kTilePrefetch<K, NQ>>(c, msk, raw, AL, AH, t > 0 && (NQ == 2 || kRecResident<K, NQ>));
       // ---- forward transform of size K at index 0
       const uint32_t* vp0 = VP + vp_slot<K, NQ>(0, NQ - 1) * G::kVPWords;  // segment 0's tables = FFT(K, 0)'s
       stamp(dbg, 26);
@@ -1227,7 +1248,7 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
     }
     stamp(dbg, 30);
     // the next tile's first-step rows load during this tile's copy-out
-    if constexpr (kRowPrefetch<NQ>) {
+    if constexpr (kRowPrefetch<NQ> || kTilePrefetch<K, NQ>) {
       if (t + 1 < ntl) {
         const uint32_t tn = tile_at(t + 1), nc = tile_cols(tn);
         issue_rows(raw, (NQ > 1 && (kExp & 32)) ? T.zeros : shp + 2u * static_cast<size_t>(tn) * kTile,
