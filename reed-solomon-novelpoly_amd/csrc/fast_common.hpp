@@ -410,10 +410,11 @@ __device__ __forceinline__ const uint32_t* skew_pools(const DevTables& T) {
 
 // Only the SGPR half (dwords 8..19) of the tables of c.
 // SUB: only the 6 dwords a subfield pool uses.
-template <bool TW = false, bool SUB = false>
+// OUT: out_pools (the level-0 groups of a kEncConv transform).
+template <bool TW = false, bool SUB = false, bool OUT = false>
 __device__ __forceinline__ void spool_of(const DevTables& T, uint32_t c, uint32_t (&p)[12]) {
   asm volatile("" : "+s"(c));
-  const cpool_t q = (cpool_t)(skew_pools<TW>(T)) + c * kPoolWords + 8;
+  const cpool_t q = (cpool_t)(OUT ? T.out_pools : skew_pools<TW>(T)) + c * kPoolWords + 8;
 #pragma unroll
   for (int i = 0; i < (SUB ? 6 : 12); ++i) p[i] = q[i];
 }
@@ -740,7 +741,16 @@ __device__ __forceinline__ void rpipe_step(RF& rec, NF& need, GF& group, uint32_
       if (need(Int<F + 1>{})) pool_at(rec(Int<F + 1>{}), nxt);
     }
     __builtin_amdgcn_sched_barrier(0);
-    group(Int<F>{}, make_mult(cur));
+    if constexpr (kExp & 8192) {  // experiment: no VGPR copies of the row tables (wrong products)
+      Mult m;
+#pragma unroll
+      for (int i = 0; i < 12; ++i) m.s[i] = cur[8 + i];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) asm volatile("" : "=v"(m.v[i]));
+      group(Int<F>{}, m);
+    } else {
+      group(Int<F>{}, make_mult(cur));
+    }
     __builtin_amdgcn_sched_barrier(0);
     rpipe_step<F + 1, NG>(rec, need, group, nxt, cur);
   }
@@ -757,35 +767,46 @@ __device__ __forceinline__ void pipelined_rec(RF rec, NF need, GF group) {
 // stage_vpools): group f reads them at vaddr(f); only the SGPR half is
 // prefetched with s_load.
 // subf(Int<f>) -> std::integral_constant<bool, group f multiplies in the subfield form>.
-template <int F, int NG, bool TW, typename CF, typename VF, typename SF, typename GF>
-__device__ __forceinline__ void spipe_step(const DevTables& T, CF& cval, VF& vaddr, SF& subf, GF& group,
+// OUTF(f): integral_constant<bool>, group f's SGPR half from out_pools.
+struct NoOut {
+  template <typename FC>
+  __device__ __forceinline__ std::false_type operator()(FC) const {
+    return {};
+  }
+};
+template <int F, int NG, bool TW, typename CF, typename VF, typename SF, typename GF, typename OF>
+__device__ __forceinline__ void spipe_step(const DevTables& T, CF& cval, VF& vaddr, SF& subf, GF& group, OF& outf,
                                            uint32_t (&cur)[12], uint32_t (&nxt)[12], VHalf& curv, VHalf& nxtv) {
   if constexpr (F < NG) {
     if constexpr (NP_PIPE_WAIT) {
       __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
       if constexpr (F + 1 < NG) {
-        spool_of<TW, decltype(subf(Int<F + 1>{}))::value>(T, cval(Int<F + 1>{}), nxt);
+        spool_of<TW, decltype(subf(Int<F + 1>{}))::value, decltype(outf(Int<F + 1>{}))::value>(
+            T, cval(Int<F + 1>{}), nxt);
         vhalf_load<decltype(subf(Int<F + 1>{}))::value>(vaddr(Int<F + 1>{}), nxtv);
       }
       __builtin_amdgcn_sched_barrier(0);
       group(Int<F>{}, mult_from<decltype(subf(Int<F>{}))::value>(cur, curv));
     } else {
-      if constexpr (F + 1 < NG) spool_of<TW, decltype(subf(Int<F + 1>{}))::value>(T, cval(Int<F + 1>{}), nxt);
+      if constexpr (F + 1 < NG)
+        spool_of<TW, decltype(subf(Int<F + 1>{}))::value, decltype(outf(Int<F + 1>{}))::value>(
+            T, cval(Int<F + 1>{}), nxt);
       __builtin_amdgcn_sched_barrier(0);
       group(Int<F>{}, staged_mult<decltype(subf(Int<F>{}))::value>(cur, vaddr(Int<F>{})));
     }
     __builtin_amdgcn_sched_barrier(0);
-    spipe_step<F + 1, NG, TW>(T, cval, vaddr, subf, group, nxt, cur, nxtv, curv);
+    spipe_step<F + 1, NG, TW>(T, cval, vaddr, subf, group, outf, nxt, cur, nxtv, curv);
   }
 }
 
-template <int NG, bool TW = false, typename CF, typename VF, typename SF, typename GF>
-__device__ __forceinline__ void pipelined_staged(const DevTables& T, CF cval, VF vaddr, SF subf, GF group) {
+template <int NG, bool TW = false, typename CF, typename VF, typename SF, typename GF, typename OF = NoOut>
+__device__ __forceinline__ void pipelined_staged(const DevTables& T, CF cval, VF vaddr, SF subf, GF group,
+                                                 OF outf = OF{}) {
   uint32_t pa[12], pb[12];
   VHalf va, vb;
-  spool_of<TW, decltype(subf(Int<0>{}))::value>(T, cval(Int<0>{}), pa);
+  spool_of<TW, decltype(subf(Int<0>{}))::value, decltype(outf(Int<0>{}))::value>(T, cval(Int<0>{}), pa);
   if constexpr (NP_PIPE_WAIT) vhalf_load<decltype(subf(Int<0>{}))::value>(vaddr(Int<0>{}), va);
-  spipe_step<0, NG, TW>(T, cval, vaddr, subf, group, pa, pb, va, vb);
+  spipe_step<0, NG, TW>(T, cval, vaddr, subf, group, outf, pa, pb, va, vb);
 }
 
 // LDS slot of the multiplier of group t at level b of a size-K transform:
@@ -798,11 +819,15 @@ __host__ __device__ constexpr uint32_t vslot(int b, uint32_t t) {
 // Copies the VGPR halves (8 dwords) of every multiplier of a size-K transform
 // at `index` into VP (K - 1 slots).  Caller synchronises.
 // tw: tower_pools (the transform runs in tower coordinates), else perm_pools.
+// l0_out (forward transforms whose outputs leave the tower, kEncConv): the
+// level-0 slots from out_pools (tower in, Cantor out) instead.
 template <int K, int NT>
-__device__ __forceinline__ void stage_vpools(const DevTables& T, uint32_t index, uint32_t* VP, bool tw = false) {
+__device__ __forceinline__ void stage_vpools(const DevTables& T, uint32_t index, uint32_t* VP, bool tw = false,
+                                             bool l0_out = false) {
   // scalar base (a select the compiler may otherwise do per lane, in a VGPR
   // pair that gets spilled across the callers' loops)
   const uint32_t* pools = fresh(tw ? T.tower_pools : T.perm_pools);
+  const uint32_t* pools0 = fresh(l0_out ? T.out_pools : pools);
   for (uint32_t i = fresh_v(threadIdx.x); i < 2u * (K - 1); i += NT) {
     const uint32_t slot = i >> 1, half = i & 1u;
     uint32_t b = 0;
@@ -810,7 +835,7 @@ __device__ __forceinline__ void stage_vpools(const DevTables& T, uint32_t index,
     const uint32_t t = slot - static_cast<uint32_t>(K - (K >> b));
     const uint32_t c = 2u * t + (index >> b);
     *reinterpret_cast<uint4*>(VP + 8 * slot + 4 * half) =
-        *reinterpret_cast<const uint4*>(pools + static_cast<size_t>(c) * kPoolWords + 4 * half);
+        *reinterpret_cast<const uint4*>((b == 0 ? pools0 : pools) + static_cast<size_t>(c) * kPoolWords + 4 * half);
   }
 }
 
@@ -903,17 +928,73 @@ __device__ __forceinline__ void with_gen(uint32_t index, F&& f) {
 #ifndef NP_CQ_NO_SKIP
 #define NP_CQ_NO_SKIP 0
 #endif
+// The VGPR half (dwords 2..3) of the conversion's table, by a scalar load: the
+// compiler otherwise reads it with a vector load (it cannot prove that the row
+// stores do not alias the tables), and that load's vmcnt(0) wait also waits
+// for every row store issued before it.
+__device__ __forceinline__ uint64_t tower_conv_vhalf(cpool_t q) {
+  uint64_t s23, vv;
+  asm volatile("s_load_dwordx2 %0, %1, 0x8\n\ts_waitcnt lgkmcnt(0)" : "=s"(s23) : "s"(q) : "memory");
+  asm volatile("v_mov_b64 %0, %1" : "=v"(vv) : "s"(s23));
+  return vv;
+}
+
+// The conversion's tables (tower_pools[kFieldSize], b slots) for a fused
+// conversion (qbfly_fwd_conv): 3 SGPR and 2 VGPR dwords.
+struct ConvTab {
+  uint32_t sa, sb, sc, va, vb;
+};
+__device__ __forceinline__ ConvTab conv_tab(const DevTables& T) {
+  const cpool_t q = (cpool_t)(T.tower_pools) + 65536u * kPoolWords;
+  const uint64_t vv = tower_conv_vhalf(q);
+  return ConvTab{q[8 + 3], q[8 + 4], q[8 + 5], static_cast<uint32_t>(vv), static_cast<uint32_t>(vv >> 32)};
+}
+
+// The forward butterfly of a transform's last level fused with the tower ->
+// Cantor conversion of both outputs (kEncConv).  With x' = x ^ c y, y' = y ^ x'
+// (tower coordinates) and Tc(v) = (v_L ^ A(v_H), v_H), A the conversion's
+// high -> low plane map (tower_convert):
+//   Tc(x')_L = x_L ^ A(x_H) ^ Tc(c y)_L,   Tc(x')_H = x_H ^ (c y)_H,
+//   Tc(y')   = Tc(x') ^ Tc(y),             Tc(y)_L = y_L ^ A(y_H),
+// where m = out_pools[c] computes exactly (Tc(c y)_L, (c y)_H) from tower y,
+// and A(y_H) reuses the high plane's selectors of the product: 43 VALU
+// instead of a butterfly (28) and two conversions (2 x 10).
+__device__ __forceinline__ void qbfly_fwd_conv(uint32_t& xl, uint32_t& xh, uint32_t& yl, uint32_t& yh, const Mult& m,
+                                               const ConvTab& a) {
+  uint32_t s[6];
+  selectors(yl, yh, s);
+  uint32_t x0, x1, x2;  // selectors of x_H (before x_H changes)
+  asm volatile(
+      "v_and_b32 %0, 0x07070707, %3\n\t"
+      "v_lshrrev_b32 %1, 3, %3\n\t"
+      "v_lshrrev_b32 %2, 6, %3\n\t"
+      "v_and_b32 %1, 0x07070707, %1\n\t"
+      "v_and_b32 %2, 0x03030303, %2"
+      : "=&v"(x0), "=&v"(x1), "=&v"(x2)
+      : "v"(xh));
+  qplane_sub(xl, x0, x1, x2, a.va, a.vb, a.sa, a.sb, a.sc);  // x_L ^ A(x_H)
+  qplane(xl, s, m.v[0], m.v[1], m.v[2], m.v[3], m.s[0], m.s[1], m.s[2], m.s[3], m.s[4], m.s[5]);
+  qplane(xh, s, m.v[4], m.v[5], m.v[6], m.v[7], m.s[6], m.s[7], m.s[8], m.s[9], m.s[10], m.s[11]);
+  qplane_sub(yl, s[3], s[4], s[5], a.va, a.vb, a.sa, a.sb, a.sc);  // y_L ^ A(y_H)
+  yl ^= xl;
+  yh ^= xh;
+}
+
 // GEN: coordinates and subfield levels (kSubLevel).
 // POST(t), when given, runs after group t of the forward transform's level 0
 // (rows 2t and 2t + 1 are final there).
 struct NoPost {
   __device__ __forceinline__ void operator()(int) const {}
 };
-template <int K, bool INVERSE, bool INDEX0, int GEN = -1, typename POST = NoPost>
+// CONV (forward, tower coordinates): the last level leaves the outputs in
+// Cantor coordinates (qbfly_fwd_conv; VP's level-0 slots staged from out_pools,
+// stage_vpools l0_out).
+template <int K, bool INVERSE, bool INDEX0, int GEN = -1, bool CONV = false, typename POST = NoPost>
 __device__ __forceinline__ void cq_levels(const DevTables& T, const uint32_t* VP, uint32_t index, uint32_t g,
                                           uint32_t (&L)[16], uint32_t (&H)[16], uint32_t rows = ~0u,
                                           POST post = POST{}) {
   if constexpr (kExp & 1) return;
+  static_assert(!CONV || (!INVERSE && GEN >= 0 && !kSubLevel<GEN>(0)), "fused conversion: forward, tower, full level 0");
   auto cval = [&](auto fc) __attribute__((always_inline)) {
     constexpr GroupRef r = cq_group<INVERSE>(decltype(fc)::value);
     return 2u * (g * (8u >> r.b) + r.t) + (index >> r.b);
@@ -922,10 +1003,12 @@ __device__ __forceinline__ void cq_levels(const DevTables& T, const uint32_t* VP
     constexpr GroupRef r = cq_group<INVERSE>(decltype(fc)::value);
     return VP + 8u * vslot<K>(r.b, g * (8u >> r.b) + r.t);
   };
+  ConvTab ct{};  // CONV: loaded at level 0's first group, live through that level only
   auto group = [&](auto fc, const Mult& p) __attribute__((always_inline)) {
     constexpr GroupRef r = cq_group<INVERSE>(decltype(fc)::value);
     constexpr int d = 1 << r.b;
     const bool live = NP_CQ_LIVE_ALL || !INDEX0 || r.t != 0 || g != 0;  // c == 0: the skew sentinel, no product
+    if constexpr (CONV && r.b == 0 && r.t == 0) ct = conv_tab(T);
     constexpr uint32_t span = ((1u << (2 * d)) - 1u) << (r.t * 2 * d);  // the group's rows
     if (!NP_CQ_NO_SKIP && (rows & span) == 0) return;
     auto body = [&](auto sub_c) __attribute__((always_inline)) {
@@ -933,7 +1016,9 @@ __device__ __forceinline__ void cq_levels(const DevTables& T, const uint32_t* VP
 #pragma unroll
       for (int u = 0; u < d; ++u) {
         const int x = r.t * 2 * d + u, y = x + d;
-        if (INVERSE) {
+        if constexpr (CONV && r.b == 0) {
+          qbfly_fwd_conv(L[x], H[x], L[y], H[y], p, ct);
+        } else if (INVERSE) {
           L[y] ^= L[x];
           H[y] ^= H[x];
           if (live) qmul_mode<SUB>(L[x], H[x], L[y], H[y], p);
@@ -950,7 +1035,10 @@ __device__ __forceinline__ void cq_levels(const DevTables& T, const uint32_t* VP
   auto subf = [&](auto fc) __attribute__((always_inline)) {
     return std::integral_constant<bool, kSubLevel<GEN>(cq_group<INVERSE>(decltype(fc)::value).b)>{};
   };
-  pipelined_staged<15, (GEN >= 0)>(T, cval, vaddr, subf, group);
+  auto outf = [&](auto fc) __attribute__((always_inline)) {
+    return std::integral_constant<bool, CONV && cq_group<INVERSE>(decltype(fc)::value).b == 0>{};
+  };
+  pipelined_staged<15, (GEN >= 0)>(T, cval, vaddr, subf, group, outf);
 }
 
 // Levels 4..logK-1 in the high layout: quad j pairs with j + 2^(b-2-logR);
@@ -1073,17 +1161,6 @@ __device__ __forceinline__ void add_derivative(uint32_t (&A)[16], uint32_t (&X)[
 // Cantor <-> tower coordinates of NR quads (an involution, field_tables.hpp
 // HostTables::tower_a): the low plane takes A(high plane), 3 byte lookups of
 // the high plane through the b slots of tower_pools[kFieldSize].
-// The VGPR half (dwords 2..3) of the conversion's table, by a scalar load: the
-// compiler otherwise reads it with a vector load (it cannot prove that the row
-// stores do not alias the tables), and that load's vmcnt(0) wait also waits
-// for every row store issued before it.
-__device__ __forceinline__ uint64_t tower_conv_vhalf(cpool_t q) {
-  uint64_t s23, vv;
-  asm volatile("s_load_dwordx2 %0, %1, 0x8\n\ts_waitcnt lgkmcnt(0)" : "=s"(s23) : "s"(q) : "memory");
-  asm volatile("v_mov_b64 %0, %1" : "=v"(vv) : "s"(s23));
-  return vv;
-}
-
 template <int NR>
 __device__ __forceinline__ void tower_convert(const DevTables& T, uint32_t (&L)[NR], const uint32_t (&H)[NR]) {
 #ifdef NP_NO_CONVERT

@@ -87,6 +87,22 @@ __device__ __forceinline__ void shift_hi(const DevTables& T, const uint32_t* vp,
   }
 }
 
+// NP_ENC_CONV: shifts whose level 0 multiplies by full elements (gen_of(sK)
+// >= 1: every shift at k = 256) leave the tower inside that level
+// (cq_levels CONV, qbfly_fwd_conv) instead of converting the 16 rows after it.
+// Measured: config-3 encode 1.656 / 1.663 -> 1.629 / 1.631 ms (-1.8 %,
+// profiles/r04_ab.txt).
+#ifndef NP_ENC_CONV
+#define NP_ENC_CONV 1
+#endif
+// Whether shift sh of a size-K encode fuses its conversion; the staging of its
+// tables must agree (stage_vpools l0_out).  SH = 23 stands for shifts 2 and 3.
+__host__ __device__ constexpr bool enc_conv(int K, uint32_t sh) {
+  return NP_ENC_CONV && sh >= 1 && sh <= 3 && gen_of(sh * static_cast<uint32_t>(K)) >= 1;
+}
+template <int K, int SH>
+constexpr bool kEncConv = SH != 0 && enc_conv(K, SH == 23 ? 2u : static_cast<uint32_t>(SH));
+
 // The forward cq levels of shift sh, ending in Cantor coordinates.
 template <int K, int SH>
 __device__ __forceinline__ void shift_cq(const DevTables& T, const uint32_t* vp, uint32_t index, uint32_t g,
@@ -95,8 +111,9 @@ __device__ __forceinline__ void shift_cq(const DevTables& T, const uint32_t* vp,
     cq_levels<K, false, false, -1>(T, vp, index, g, XL, XH);
   } else {
     static_assert(SH != 23 || kShiftGen<K, 2> == kShiftGen<K, 3>, "shifts 2 and 3 share one instance");
-    cq_levels<K, false, false, kShiftGen<K, SH>>(T, vp, index, g, XL, XH);
-    tower_convert(T, XL, XH);  // back to Cantor coordinates for the shard rows
+    static_assert(SH != 23 || enc_conv(K, 2) == enc_conv(K, 3), "shifts 2 and 3 share one instance");
+    cq_levels<K, false, false, kShiftGen<K, SH>, kEncConv<K, SH>>(T, vp, index, g, XL, XH);
+    if constexpr (!kEncConv<K, SH>) tower_convert(T, XL, XH);  // back to Cantor coordinates for the shard rows
   }
 }
 
@@ -116,6 +133,7 @@ __device__ __forceinline__ void shift_cq(const DevTables& T, const uint32_t* vp,
 #ifndef NP_ENC_STORE_SPREAD
 #define NP_ENC_STORE_SPREAD 0
 #endif
+static_assert(!(NP_ENC_STORE_SPREAD && NP_ENC_CONV), "the spread stores convert in their own hook");
 
 // The fast encodes exchange layouts through quad items (cq_write_q ..
 // hi_read_q, fast_common.hpp): no byte transposes.
@@ -176,10 +194,10 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
   const bool resident = nshift <= 4;
   if (resident) {
     for (uint32_t sh = 0; sh < nshift && sh * K < a.wanted_n; ++sh)
-      stage_vpools<K, G::kThreads>(T, sh * K, VP + sh * G::kVPWords, true);
+      stage_vpools<K, G::kThreads>(T, sh * K, VP + sh * G::kVPWords, true, enc_conv(K, sh));
   } else {
     stage_vpools<K, G::kThreads>(T, 0, VP, true);                                   // inverse transform, index 0
-    if (nshift > 1) stage_vpools<K, G::kThreads>(T, K, VP + G::kVPWords, true);  // first shift
+    if (nshift > 1) stage_vpools<K, G::kThreads>(T, K, VP + G::kVPWords, true, enc_conv(K, 1));  // first shift
   }
   __syncthreads();
 
@@ -221,7 +239,8 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     shift_hi<K, SH>(T, vp, index, ML, MH, XL, XH, PL, PH);
     __syncthreads();  // the previous cq pass is done with the tile and with the other table buffer
     if (!resident && sh + 1 < nshift && (sh + 1) * K < a.wanted_n)
-      stage_vpools<K, G::kThreads>(T, (sh + 1) * K, VP + ((sh + 1) & 1u) * G::kVPWords, sh + 1 < 4);
+      stage_vpools<K, G::kThreads>(T, (sh + 1) * K, VP + ((sh + 1) & 1u) * G::kVPWords, sh + 1 < 4,
+                                   enc_conv(K, sh + 1));
     if constexpr (kEncQx<K>) {
       hi_write_q<K>(tile, g, lane, XL, XH);
       __syncthreads();
@@ -456,7 +475,8 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
   const uint32_t nshift = a.n / K;
   const uint32_t last = min(nshift, (a.wanted_n + K - 1) / K) - 1;  // last shift with wanted rows
   if (first) {  // tables of the inverse transform (index 0) and of every shift, kept for all tiles
-    for (uint32_t sh = 0; sh <= last; ++sh) stage_vpools<K, G::kThreads>(T, sh * K, VP + sh * G::kVPWords, true);
+    for (uint32_t sh = 0; sh <= last; ++sh)
+      stage_vpools<K, G::kThreads>(T, sh * K, VP + sh * G::kVPWords, true, enc_conv(K, sh));
   }
   __syncthreads();
   stamp(dbg, 1);
