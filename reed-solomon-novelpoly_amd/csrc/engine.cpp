@@ -443,7 +443,7 @@ const char* np_status_message(int st) {
   }
 }
 
-const char* np_version(void) { return "novelpoly-mi355x 0.2.0 (gfx950)"; }
+const char* np_version(void) { return "novelpoly-mi355x 0.3.0 (gfx950)"; }
 
 size_t np_recoverability_subset_size(size_t n) { return (n ? (n - 1) / 3 : 0) + 1; }
 

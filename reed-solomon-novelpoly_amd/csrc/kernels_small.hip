@@ -520,12 +520,20 @@ hipError_t reconstruct_by_nq(const DevTables& T, const ReconstructArgs& a, hipSt
 
 }  // namespace
 
+// NP_SMALL_MINK (experiment builds only): the smallest k served here; below
+// it the generic kernels run (tools/records: the generic path's rate at 2-21
+// validators for comparison).
+#ifndef NP_SMALL_MINK
+#define NP_SMALL_MINK 1
+#endif
 bool small_encode_supported(uint32_t n, uint32_t k) {
-  return (k == 1 || k == 2 || k == 4 || k == 8 || k == 16 || k == 32) && n >= 2 * k && n <= kSmallMaxSeg * k;
+  return (k == 1 || k == 2 || k == 4 || k == 8 || k == 16 || k == 32) && k >= NP_SMALL_MINK && n >= 2 * k &&
+         n <= kSmallMaxSeg * k;
 }
 
 bool small_reconstruct_supported(uint32_t n, uint32_t k) {
-  return (k == 1 || k == 2 || k == 4 || k == 8 || k == 16 || k == 32) && (n == 2 * k || n == 4 * k || n == 8 * k);
+  return (k == 1 || k == 2 || k == 4 || k == 8 || k == 16 || k == 32) && k >= NP_SMALL_MINK &&
+         (n == 2 * k || n == 4 * k || n == 8 * k);
 }
 
 hipError_t launch_encode_small(const DevTables& T, const EncodeArgs& a, hipStream_t s) {
