@@ -69,7 +69,8 @@ int np_derive_parameters(size_t n_wanted, size_t k_wanted, np_code_params* out);
 int np_params_new(size_t n, size_t k, size_t wanted_n, np_code_params* out);
 /* mod.rs:102-107 ReedSolomon::shard_len */
 size_t np_shard_len(const np_code_params* params, size_t payload_size);
-/* mod.rs:64-71 CodeParams::is_faster8 analogue: 1 if a specialised GPU kernel serves (n,k) */
+/* mod.rs:64-71 CodeParams::is_faster8 analogue: 1 if specialised GPU kernels serve both
+   directions of (n,k) for 1 MiB payloads (fast, small, resident, huge or big kernels) */
 int np_is_fast_path(const np_code_params* params);
 
 /* ---- context ------------------------------------------------------------- */

@@ -484,7 +484,9 @@ int np_is_fast_path(const np_code_params* p) {
   const uint32_t n = static_cast<uint32_t>(p->n), k = static_cast<uint32_t>(p->k);
   const bool enc = np::fast_encode_supported(n, k) || (np::res_encode_supported(n, k) && np::res_enabled()) ||
                    (np::huge_encode_supported(n, k) && huge_on(k)) || np::big_encode_supported(n, k);
-  return (enc && rec_path(n, k, size_t(64) << 10) != RecPath::Generic) ? 1 : 0;
+  // the reconstruct family for a 1 MiB payload (the huge kernels' tile slots
+  // depend on the shard length: far longer shards fall to the generic decode)
+  return (enc && rec_path(n, k, np_shard_len(p, size_t(1) << 20)) != RecPath::Generic) ? 1 : 0;
 }
 
 int np_ctx_create(int device, np_ctx** out) {

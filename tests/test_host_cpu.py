@@ -104,10 +104,20 @@ def test_synth_is_deterministic():
 
 
 def test_fast_path_table():
-    # the specialised kernels serve the BASELINE shapes; generic covers the rest
+    """np_is_fast_path (the crate's is_faster8 slot, mod.rs:64-71) reports the
+    kernel families the engine dispatches to (engine.cpp rec_path): small
+    (k <= 32), fast (64-256), resident (512, 1024), big (2048) and huge
+    (4096-16384, 1 MiB payloads) serve both directions at n/k in {2, 4, 8};
+    explicit n/k >= 16 reconstructs on the generic kernels."""
     for cfg in synth.CONFIGS.values():
         p = npa.CodeParams.derive_parameters(cfg["n_wanted"], cfg["k_wanted"])
-        assert isinstance(p.is_faster8(), bool)
+        assert p.is_faster8(), cfg
+    served = [(2, 1), (3, 1), (10, 4), (16, 8), (100, 34), (256, 86), (1024, 342), (2000, 667), (4096, 1366),
+              (8192, 2731), (10000, 3334), (16384, 5462), (30000, 10000), (65536, 21846)]
+    for nw, kw in served:
+        assert npa.CodeParams.derive_parameters(nw, kw).is_faster8(), (nw, kw)
+    for nw, kw in [(4096, 256), (8192, 512), (32768, 1024)]:  # n / k >= 16: generic reconstruct
+        assert not npa.CodeParams.derive_parameters(nw, kw).is_faster8(), (nw, kw)
 
 
 def test_ctx_without_gpu_reports_no_device():
