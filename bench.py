@@ -150,7 +150,8 @@ def cpu_baseline(cfg, params, seconds):
     omp = os.environ.get("OMP_NUM_THREADS", "")
     if omp.isdigit() and int(omp) > 0:
         threads = min(threads, int(omp))
-    n, k, plen, erase = params.n(), params.k(), cfg["payload"], cfg["erase"]
+    n, k, plen = params.n(), params.k(), cfg["payload"]
+    erase = cfg["erase"] if cfg["erase"] is not None else n - k  # as the GPU workload (main)
 
     def run(t, secs):
         out = subprocess.run([exe, str(n), str(k), str(plen), str(erase), str(t), str(secs)],
