@@ -1,0 +1,124 @@
+#!/bin/bash
+# Round-4 GPU probes (one gpurun call each: bash tools/r04_probes.sh NAME).
+# Their A/B results are collected in profiles/r04_ab.txt; the libraries they
+# compare are tools/build_variant.sh builds (tools/exp/lib_NAME.so).
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out/r04 gpurun_out/exp
+
+# Round-4 probe on the GPU box: GPU tests, the headline bench, and the
+# per-phase stamps of the config-3 decode (tools/exp/lib_st64.so, NP_EXP=64).
+p1() {
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r04/pytest_gpu.log 2>&1; rc=$?
+  tail -3 gpurun_out/r04/pytest_gpu.log
+  if [ $rc -ne 0 ]; then grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu.log | head -20; exit $rc; fi
+  timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu > gpurun_out/r04/bench.log 2>&1 || exit $?
+  tail -1 gpurun_out/r04/bench.log | cut -c1-300
+  NP_LIB_PATH=$PWD/tools/exp/lib_st64.so timeout -k 10 120 python tools/phase_stamps.py > gpurun_out/r04/stamps.log 2>&1 || exit $?
+  cat gpurun_out/r04/stamps.log
+  [ -x tools/microbench/bfly_rates ] || make -s -C tools/microbench bfly_rates || exit $?
+  timeout -k 10 120 tools/microbench/bfly_rates > gpurun_out/r04/bfly_rates.txt 2>&1 || exit $?
+  cat gpurun_out/r04/bfly_rates.txt
+}
+
+# Round-4 probe 2: per-wave decode stamps, host-memory e2e (pinned and
+# pageable), records.
+p2() {
+  NP_LIB_PATH=$PWD/tools/exp/lib_st192.so timeout -k 10 120 python tools/wave_stamps.py > gpurun_out/r04/wave_stamps.log 2>&1 || exit $?
+  cat gpurun_out/r04/wave_stamps.log
+  for c in 3 4; do timeout -k 10 300 python tools/e2e_bench.py --config $c --batch $([ $c = 3 ] && echo 256 || echo 64) > gpurun_out/r04/e2e_cfg$c.json 2> gpurun_out/r04/e2e_cfg$c.err || { tail -5 gpurun_out/r04/e2e_cfg$c.err; exit 1; }; cat gpurun_out/r04/e2e_cfg$c.json; done
+  bash tools/records.sh r04a
+}
+
+# Round-4 probe 3: per-wave encode stamps, host copy microbenchmark.
+p3() {
+  NP_LIB_PATH=$PWD/tools/exp/lib_st192.so timeout -k 10 120 python tools/enc_stamps.py > gpurun_out/r04/enc_stamps.log 2>&1 || { cat gpurun_out/r04/enc_stamps.log; exit 1; }
+  cat gpurun_out/r04/enc_stamps.log
+  timeout -k 10 120 tools/microbench/host_copy > gpurun_out/r04/host_copy.txt 2>&1 || exit $?
+  cat gpurun_out/r04/host_copy.txt
+  NP_LIB_PATH=$PWD/tools/exp/lib_st192.so timeout -k 10 120 python tools/res_stamps.py > gpurun_out/r04/res_stamps.log 2>&1 || { cat gpurun_out/r04/res_stamps.log; exit 1; }
+  cat gpurun_out/r04/res_stamps.log
+  timeout -k 10 300 python tools/e2e_bench.py --config 4 --batch 64 > gpurun_out/r04/e2e_cfg4_nt.json 2> gpurun_out/r04/e2e_cfg4_nt.err || { tail -5 gpurun_out/r04/e2e_cfg4_nt.err; exit 1; }
+  cat gpurun_out/r04/e2e_cfg4_nt.json
+}
+
+# Round-4 probe 4: GPU tests, encode spread-store A/B, config-4 row-table DMA
+# A/B, per-wave stamps, pageable e2e.
+p4() {
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r04/pytest_gpu4.log 2>&1; rc=$?
+  tail -3 gpurun_out/r04/pytest_gpu4.log
+  if [ $rc -ne 0 ]; then grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu4.log | head -20; exit $rc; fi
+  TAG=p4_ bash tools/exp_one.sh base spread hiw hiwspread base spread hiw hiwspread || exit $?
+  TAG=p4c4_ ARGS="--config 4" bash tools/exp_one.sh base resdma0 base resdma0 || exit $?
+  NP_LIB_PATH=$PWD/tools/exp/lib_st192.so timeout -k 10 120 python tools/enc_stamps.py > gpurun_out/r04/enc_stamps2.log 2>&1 || { cat gpurun_out/r04/enc_stamps2.log; exit 1; }
+  tail -22 gpurun_out/r04/enc_stamps2.log
+  NP_LIB_PATH=$PWD/tools/exp/lib_st192.so timeout -k 10 120 python tools/res_stamps.py > gpurun_out/r04/res_stamps2.log 2>&1 || { cat gpurun_out/r04/res_stamps2.log; exit 1; }
+  tail -20 gpurun_out/r04/res_stamps2.log
+  for c in 3 4; do timeout -k 10 300 python tools/e2e_bench.py --config $c --batch $([ $c = 3 ] && echo 256 || echo 64) > gpurun_out/r04/e2e4_cfg$c.json 2> gpurun_out/r04/e2e4_cfg$c.err || { tail -5 gpurun_out/r04/e2e4_cfg$c.err; exit 1; }; cat gpurun_out/r04/e2e4_cfg$c.json; done
+}
+
+# Round-4 probe 5: GPU tests (product and the decode row-DMA variant), decode
+# row-DMA A/B at configs 3 and 2, encode HIW-early A/B, pageable pin-in-place e2e.
+p5() {
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r04/pytest_gpu5.log 2>&1; rc=$?
+  tail -3 gpurun_out/r04/pytest_gpu5.log
+  if [ $rc -ne 0 ]; then grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu5.log | head -20; exit $rc; fi
+  NP_LIB_PATH=$PWD/tools/exp/lib_rowdma.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r04/pytest_gpu5_rowdma.log 2>&1; rc=$?
+  tail -3 gpurun_out/r04/pytest_gpu5_rowdma.log
+  if [ $rc -ne 0 ]; then grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu5_rowdma.log | head -20; exit $rc; fi
+  TAG=p5_ bash tools/exp_one.sh base rowdma hiw base rowdma hiw || exit $?
+  TAG=p5c2_ ARGS="--config 2" bash tools/exp_one.sh base rowdma base rowdma || exit $?
+  for c in 3 4; do timeout -k 10 300 python tools/e2e_bench.py --config $c --batch $([ $c = 3 ] && echo 256 || echo 64) > gpurun_out/r04/e2e5_cfg$c.json 2> gpurun_out/r04/e2e5_cfg$c.err || { tail -5 gpurun_out/r04/e2e5_cfg$c.err; exit 1; }; cat gpurun_out/r04/e2e5_cfg$c.json; done
+}
+
+# Round-4 probe 6: GPU tests with the next-tile row prefetch (NP_REC_TILE_PREFETCH=1
+# in the product), A/B against tpf0 at config 3 and at 1200 validators (8 segments).
+p6() {
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r04/pytest_gpu6.log 2>&1; rc=$?
+  tail -3 gpurun_out/r04/pytest_gpu6.log
+  if [ $rc -ne 0 ]; then grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu6.log | head -20; exit $rc; fi
+  TAG=p6_ bash tools/exp_one.sh base tpf0 base tpf0 || exit $?
+  TAG=p6v1200_ ARGS="--n-wanted 1200 --batch 1024 --erase 400" bash tools/exp_one.sh base tpf0 base tpf0 || exit $?
+}
+
+# Round-4 probe 8: GPU tests with the encode's fused tower -> Cantor conversion
+# (NP_ENC_CONV=1 in the product), A/B against conv0 at configs 3 and 2.
+p8() {
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r04/pytest_gpu8.log 2>&1; rc=$?
+  tail -3 gpurun_out/r04/pytest_gpu8.log
+  if [ $rc -ne 0 ]; then grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu8.log | head -20; exit $rc; fi
+  TAG=p8_ bash tools/exp_one.sh base conv0 base conv0 || exit $?
+  TAG=p8c2_ ARGS="--config 2" bash tools/exp_one.sh base conv0 || exit $?
+  TAG=p8v700_ ARGS="--n-wanted 700 --batch 1024 --erase 234" bash tools/exp_one.sh base conv0 || exit $?
+}
+
+# Round-4 probe 9: the generic kernels' rate at 2-21 validators (k = 1, 2, 4;
+# smallmin8 = NP_SMALL_MINK=8) against the small kernels of the product.
+p9() {
+  for vc in 2 3 6 10 20; do
+    TAG=p9v${vc}_ ARGS="--n-wanted $vc --batch 1024 --erase $(( (vc - 1) / 3 + 1 ))" bash tools/exp_one.sh base smallmin8 || exit $?
+  done
+}
+
+# Round-4 probe 10: k = 2048 (6,144-12,288 validators) on the big kernels
+# (default) against the size-1024 sub-transform kernels (NP_HUGE=1).
+p10() {
+  for vc in 6144 7000 10000 12000; do
+    for h in def 1; do
+      if [ $h = 1 ]; then export NP_HUGE=1; else unset NP_HUGE; fi
+      timeout -k 10 180 python bench.py --no-cpu --steps 10 --warmup 2 --n-wanted $vc --batch 512 --erase $(( (vc - 1) / 3 + 1 )) > gpurun_out/exp/p10_${vc}_$h.log 2>&1 || { tail -3 gpurun_out/exp/p10_${vc}_$h.log; exit 1; }
+      python3 -c "
+import json; d=json.loads(open('gpurun_out/exp/p10_${vc}_$h.log').read().strip().split('\n')[-1]); c=d['config']; print('p10 vc$vc huge=$h', c['n'], c['k'], d['value'], d['roundtrip_ok'], {k:v['ms'] for k,v in d['kernels'].items()})"
+    done
+  done
+}
+
+# Round-4 profiles: kernel-trace stats and PMC passes for configs 3, 2 and 4.
+profiles() {
+  bash tools/profile_round.sh r04 3 > gpurun_out/prof_r04.log 2>&1 || { tail -20 gpurun_out/prof_r04.log; exit 1; }
+  bash tools/profile_round.sh r04_cfg2 2 > gpurun_out/prof_r04_cfg2.log 2>&1 || { tail -20 gpurun_out/prof_r04_cfg2.log; exit 1; }
+  bash tools/profile_round.sh r04_cfg4 4 > gpurun_out/prof_r04_cfg4.log 2>&1 || { tail -20 gpurun_out/prof_r04_cfg4.log; exit 1; }
+  echo profiles done
+}
+
+"$@"
