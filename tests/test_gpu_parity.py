@@ -554,6 +554,46 @@ def test_encode_multi_tile_workgroups(gpu, oracle, monkeypatch, nw, tpw, batch, 
         assert not bad, (b, len(bad), bad[:5])
 
 
+@pytest.mark.parametrize("nw,kw,tpw,batch", [(256, 86, 2, 5), (256, 86, 4, 3), (300, 100, 3, 4), (512, 128, 2, 6),
+                                              (700, 234, 4, 3)])
+def test_reconstruct_multi_tile_workgroups_small_k(gpu, oracle, monkeypatch, nw, kw, tpw, batch):
+    """k = 64 / 128 (4 and 8 segments): the full-decode instances run several
+    consecutive tiles per workgroup as well (kernels_fast.hip kRecMT), with the
+    next tile's first-step rows loaded during the copy-out at 4 segments.  771
+    columns = 3 full tiles and one of 3 columns; random erasures, some payloads
+    with every systematic row present (the single-tile copy instance)."""
+    import torch
+
+    monkeypatch.setenv("NP_REC_TPW", str(tpw))
+    p = npa.CodeParams.derive_parameters(nw, kw)
+    n, k = p.n(), p.k()
+    assert k in (64, 128)
+    plen = 2 * k * (3 * 256 + 3) - 5
+    sl = p.make_encoder(gpu).shard_len(plen)
+    assert sl // 2 == 771
+    pls = np.stack([np.frombuffer(synth.payload(7100 + b, plen), dtype=np.uint8) for b in range(batch)])
+    dp = dev(pls)
+    ds = torch.empty((batch, n, sl), dtype=torch.uint8, device="cuda")
+    npa.encode_batch_dev(p, dp.data_ptr(), plen, plen, batch, ds.data_ptr(), n * sl, ctx=gpu, stream=stream())
+    rng = np.random.default_rng(nw * 7 + tpw)
+    pres = np.ones((batch, n), dtype=np.uint8)
+    for b in range(batch):
+        lo = k if b == 1 else 0  # payload 1 keeps every systematic row
+        pres[b, lo + rng.choice(n - lo, n - k - (1 if b == 2 else 0) - (n - k) // 3, replace=False)] = 0
+    dpres = dev(pres)
+    olen = (sl // 2) * 2 * k
+    out = torch.empty((batch, olen), dtype=torch.uint8, device="cuda")
+    npa.reconstruct_batch_dev2(p, ds.data_ptr(), sl, n * sl, dpres.data_ptr(), 0, batch, out.data_ptr(), olen,
+                               ctx=gpu, stream=stream())
+    o = host(out)
+    hs = host(ds)
+    for b in range(batch):
+        recv = [hs[b, i].tobytes() if pres[b, i] else None for i in range(n)]
+        st, want = oracle.reconstruct(recv, n, k)
+        assert st == 0 and o[b].tobytes() == want, b
+        assert want[:plen] == pls[b].tobytes()
+
+
 @pytest.mark.parametrize("tpw,batch", [(2, 8), (3, 8), (4, 5), (8, 8)])
 def test_reconstruct_multi_tile_workgroups(gpu, oracle, monkeypatch, tpw, batch):
     """k = 256: one workgroup decodes `tpw` consecutive 256-column tiles of a

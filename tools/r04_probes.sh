@@ -121,4 +121,17 @@ profiles() {
   echo profiles done
 }
 
+# Round-4 probe 11: GPU tests with the multi-tile k = 64 / 128 decodes
+# (NP_REC_MT_SMALL=1 in the product), A/B against mt0 at config 2 and 300 /
+# 700 validators.
+p11() {
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r04/pytest_gpu11.log 2>&1; rc=$?
+  tail -3 gpurun_out/r04/pytest_gpu11.log
+  if [ $rc -ne 0 ]; then grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu11.log | head -20; exit $rc; fi
+  TAG=p11c2_ ARGS="--config 2" bash tools/exp_one.sh base mt0 base mt0 || exit $?
+  TAG=p11v300_ ARGS="--n-wanted 300 --batch 1024 --erase 100" bash tools/exp_one.sh base mt0 || exit $?
+  TAG=p11v700_ ARGS="--n-wanted 700 --batch 1024 --erase 234" bash tools/exp_one.sh base mt0 || exit $?
+  TAG=p11v190_ ARGS="--n-wanted 190 --batch 1024 --erase 64" bash tools/exp_one.sh base mt0 || exit $?
+}
+
 "$@"
