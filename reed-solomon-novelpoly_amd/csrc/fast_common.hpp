@@ -741,16 +741,7 @@ __device__ __forceinline__ void rpipe_step(RF& rec, NF& need, GF& group, uint32_
       if (need(Int<F + 1>{})) pool_at(rec(Int<F + 1>{}), nxt);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (kExp & 8192) {  // experiment: no VGPR copies of the row tables (wrong products)
-      Mult m;
-#pragma unroll
-      for (int i = 0; i < 12; ++i) m.s[i] = cur[8 + i];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) asm volatile("" : "=v"(m.v[i]));
-      group(Int<F>{}, m);
-    } else {
-      group(Int<F>{}, make_mult(cur));
-    }
+    group(Int<F>{}, make_mult(cur));
     __builtin_amdgcn_sched_barrier(0);
     rpipe_step<F + 1, NG>(rec, need, group, nxt, cur);
   }

@@ -125,16 +125,6 @@ __device__ __forceinline__ void shift_cq(const DevTables& T, const uint32_t* vp,
 #define NP_ENC_HIW_EARLY 1
 #endif
 
-// NP_ENC_STORE_SPREAD: the multi-tile encode converts and stores each pair
-// of shard rows right after its level-0 butterfly group, so the 16 row stores
-// of a wave are issued among the last level's VALU work instead of in one
-// burst after it (full tiles of 16 wanted rows; otherwise the burst).
-// Measured: encode +0.6 to +1.1 % at config 3 (profiles/r04_ab.txt): off.
-#ifndef NP_ENC_STORE_SPREAD
-#define NP_ENC_STORE_SPREAD 0
-#endif
-static_assert(!(NP_ENC_STORE_SPREAD && NP_ENC_CONV), "the spread stores convert in their own hook");
-
 // The fast encodes exchange layouts through quad items (cq_write_q ..
 // hi_read_q, fast_common.hpp): no byte transposes.
 #ifndef NP_ENC_QX
@@ -382,45 +372,9 @@ __device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArg
   const uint32_t row0 = index + 16 * g;
   const uint32_t wanted = (kExp & 2) ? 0u : a.wanted_n;
   const bool nt = rows_nt(a.shards, a.batch_stride, a.shard_len);
-  if constexpr (NP_ENC_STORE_SPREAD) {
-    // one cq instance: rows are converted in the level-0 hook; stored there
-    // when the whole 16-row piece is wanted and the tile full, else after
-    const bool spread = full && nt && row0 + 16 <= wanted && 16 * a.shard_len < 0x7fffffffu;
-    const __amdgpu_buffer_rsrc_t r = buf_rsrc(out + static_cast<size_t>(row0) * a.shard_len,
-                                              spread ? 16 * static_cast<uint32_t>(a.shard_len) : 0u);
-    const cpool_t q = (cpool_t)(T.tower_pools) + 65536u * kPoolWords;  // tower -> Cantor (tower_convert)
-    const uint32_t sa = q[8 + 3], sb = q[8 + 4], sc = q[8 + 5];
-    const uint64_t vv = tower_conv_vhalf(q);
-    const uint32_t va = static_cast<uint32_t>(vv), vb = static_cast<uint32_t>(vv >> 32);
-    auto post = [&](int t) __attribute__((always_inline)) {
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int p = 2 * t + e;
-        uint32_t s0, s1, s2;
-        asm volatile(
-            "v_and_b32 %0, 0x07070707, %3\n\t"
-            "v_lshrrev_b32 %1, 3, %3\n\t"
-            "v_lshrrev_b32 %2, 6, %3\n\t"
-            "v_and_b32 %1, 0x07070707, %1\n\t"
-            "v_and_b32 %2, 0x03030303, %2"
-            : "=&v"(s0), "=&v"(s1), "=&v"(s2)
-            : "v"(XH[p]));
-        qplane_sub(XL[p], s0, s1, s2, va, vb, sa, sb, sc);
-        // a zero-size descriptor (not spread) drops the store
-        const uint2 v = cq_row(XL[p], XH[p]);
-        __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, r, 8u * lane, static_cast<uint32_t>(p * a.shard_len),
-                                              NP_ROW_STORE_CPOL);
-      }
-    };
-    static_assert(SH >= 1 && SH <= 3, "multi-tile shifts");
-    cq_levels<K, false, false, kShiftGen<K, SH>>(T, vp, index, g, XL, XH, ~0u, post);
-    stamp(dbg, st0 + 2);
-    if (!spread) store_rows(out, a.shard_len, row0, wanted, XL, XH, lane, ncols, full, nt);
-  } else {
-    shift_cq<K, SH>(T, vp, index, g, XL, XH);
-    stamp(dbg, st0 + 2);
-    store_rows(out, a.shard_len, row0, wanted, XL, XH, lane, ncols, full, nt);
-  }
+  shift_cq<K, SH>(T, vp, index, g, XL, XH);
+  stamp(dbg, st0 + 2);
+  store_rows(out, a.shard_len, row0, wanted, XL, XH, lane, ncols, full, nt);
   stamp(dbg, st0 + 3);
 }
 
@@ -756,67 +710,6 @@ __device__ __forceinline__ uint32_t seg_mask(const uint32_t (&msk)[NQ], int step
 // systematic rows (for the merge) on exit.  A runtime loop keeps
 // the kernel small; at index 0 the t = 0 multipliers are the zero element,
 // whose table yields 0 (the reference's skipped multiply).
-// NP_REC_ROW_DMA: full tiles of the multi-tile decode (K = 256, 4 or 8
-// segments) bring a step's rows into the LDS tile by LDS-DMA, issued while the
-// previous step's high levels run (the tile is free from its high read until
-// the next cq write); the premultiply reads them from LDS.  A wave moves
-// exactly the rows it premultiplies, so only its own vmcnt is waited for.
-// Measured: decode +3 % at config 3 (2.76 -> 2.85 ms), -0.5 % at config 2
-// (profiles/r04_ab.txt): off.  The premultiply's LDS reads and the barrier it
-// needs before the cq write cost more than the register loads' latency did.
-#ifndef NP_REC_ROW_DMA
-#define NP_REC_ROW_DMA 0
-#endif
-template <int K, int NQ>
-constexpr bool kRecRowDma = NP_REC_ROW_DMA && K == 256 && NQ >= 4;
-
-// Wave g's rows row0 .. row0 + 15 (bytes [8 lane, + 8) of each for every
-// lane: the 512 bytes of the tile's 256 columns) into tile bytes
-// [8 KiB g, + 8 KiB), row i at 512 i: two rows per buffer_load_dwordx4 ... lds
-// (lanes 0-31 row 2i, 32-63 row 2i + 1, 16 bytes each; the LDS image is
-// lane-linear).  One descriptor per row pair, built in SGPRs; a lane whose row
-// is absent gets an offset past the descriptor's range, so it reads zeros and
-// moves no bytes (as issue_rows' 0-size descriptors).  Only one address VGPR
-// is live.  M0 is set in the same statement; the caller waits with vmcnt.
-typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
-template <bool NT>
-__device__ __forceinline__ void dma_rows16(uint8_t* tile, const uint8_t* sh, uint32_t shard_len, uint32_t mask,
-                                           uint32_t row0, uint32_t g, uint32_t lane) {
-  const uint32_t lds0 =
-      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)(tile))) + 8192u * g;
-  const uint32_t half = lane >> 5;
-  const uint32_t vrow = 16u * (lane & 31u) + half * shard_len;  // the lane's row, relative to row 2i
-  const uint32_t bits = mask >> half;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const uint64_t base = reinterpret_cast<uint64_t>(sh + static_cast<size_t>(row0 + 2u * i) * shard_len);
-    const u32x4s rs = {uniform(static_cast<uint32_t>(base)), uniform(static_cast<uint32_t>(base >> 32) & 0xffffu),
-                       uniform(shard_len + 512u), 0x00020000u};
-    const uint32_t vo = ((bits >> (2 * i)) & 1u) ? vrow : 0x80000000u;
-    const uint32_t dst = uniform(lds0 + 1024u * i);
-    uint32_t keep;
-    if constexpr (NT)
-      asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen nt lds\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep)
-                   : "v"(vo), "s"(rs), "s"(dst)
-                   : "memory");
-    else
-      asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep)
-                   : "v"(vo), "s"(rs), "s"(dst)
-                   : "memory");
-  }
-}
-
-// NP_REC_DEFER_FOLD: the fold of step s runs at the start of step s + 1,
-// after that step's row loads are issued and before the premultiply waits for
-// them (decodes without kRowPrefetch).
-#ifndef NP_REC_DEFER_FOLD
-#define NP_REC_DEFER_FOLD 0
-#endif
-template <int NQ>
-constexpr bool kRecDeferFold = NP_REC_DEFER_FOLD && !kRowPrefetch<NQ>;
-
 // NP_REC_TILE_PREFETCH: the multi-tile decodes that load each step's rows
 // where they use them (NQ >= 4) load the next tile's first-step rows during
 // this tile's copy-out (and the first tile's before the tables are staged), as
@@ -903,21 +796,9 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
     const size_t shard_len = fresh(c.shard_len);
     const uint32_t cqb = fresh_v(c.cqb), hb = fresh_v(c.hb);
     uint32_t m = uniform(seg_mask<NQ>(msk, step));
-    const bool row_dma = kRecRowDma<K, NQ> && c.full;  // this step's rows were DMA'd into the tile
-    if (row_dma) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's own pieces
-      const uint8_t* rp = c.tile + 8192u * g + fresh_v(8u * c.lane);
-#pragma unroll
-      for (int x = 0; x < 16; ++x) raw[x] = *reinterpret_cast<const uint2*>(rp + 512u * x);
-    } else if (!kRowPrefetch<NQ> && !(PRE0 && step == 0)) {
+    if (!kRowPrefetch<NQ> && !(PRE0 && step == 0))
       issue_rows(raw, (kExp & 32) ? T.zeros : sh, (kExp & 32) ? 0 : shard_len, m, index + 16 * g, T.zeros, c.lane,
                  c.ncols, c.full, q == 0);
-      // the previous step's fold runs while these rows load (kRecDeferFold)
-      if (kRecDeferFold<NQ> && step > 0) {
-        fold(step - 1, seg_of<NQ>(step - 1));
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
     stamp(c.dbg, 2 + 6 * step);
     pipelined_rec<16>(
         [&](auto pc) __attribute__((always_inline)) {
@@ -946,10 +827,8 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
       cq_levels<K, true, false, decltype(gc)::value>(T, vp, index, g, XL, XH, m);
     });
     stamp(c.dbg, 4 + 6 * step);
-    if (step > 0 || after_tile || row_dma) {
-      // the previous high pass (or tile's copy-out, or the premultiply's reads
-      // of the DMA'd rows) is done with the tile and the other table buffer
-      __syncthreads();
+    if (step > 0 || after_tile) {
+      __syncthreads();  // the previous high pass (or tile's copy-out) is done with the tile and the other table buffer
       if (!kRecResident<K, NQ> && step + 1 < NQ) {
         const int qn = seg_of<NQ>(step + 1);
         stage_vpools<K, Geo<K>::kThreads>(T, static_cast<uint32_t>(qn) * K, c.VP + ((step + 1) & 1) * Geo<K>::kVPWords, true);
@@ -975,16 +854,6 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
     __syncthreads();
     stamp(c.dbg, 5 + 6 * step);
     hi_read_p<K>(c.tile, hb, XL, XH);
-    if (row_dma && step + 1 < NQ) {
-      const int qn = seg_of<NQ>(step + 1);
-      __syncthreads();  // every wave has read the tile: the next step's rows may land in it
-      const uint32_t mn = uniform(seg_mask<NQ>(msk, step + 1));
-      if (qn == 0)  // segment 0's rows are read again by the merge: default policy
-        dma_rows16<false>(c.tile, sh, static_cast<uint32_t>(shard_len), mn, 16 * g, g, c.lane);
-      else
-        dma_rows16<true>(c.tile, sh, static_cast<uint32_t>(shard_len), mn, static_cast<uint32_t>(qn) * K + 16 * g, g,
-                         c.lane);
-    }
     // hi levels: gen_of(index) <= 4; segment 0 (index 0) skips the t = 0
     // groups, whose skew is the zero element (15 of the 32 quad multiplies)
     // (the 2-segment decode keeps its rows prefetch live here: no room for two instances)
@@ -994,7 +863,7 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
       hi_levels<K, true, false, 0, 0>(T, vp, index, XL, XH);
     stamp(c.dbg, 6 + 6 * step);
     __builtin_amdgcn_sched_barrier(0);
-    if (!kRecDeferFold<NQ>) fold(step, q);
+    fold(step, q);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (PRE0) {
       // raw is reloaded at every later step: an instruction-free definition
@@ -1004,7 +873,6 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
       for (int x = 0; x < 16; ++x) asm volatile("" : "=v"(raw[x].x), "=v"(raw[x].y));
     }
   }
-  if constexpr (kRecDeferFold<NQ>) fold(NQ - 1, seg_of<NQ>(NQ - 1));
 }
 
 // Decode of one tile (K < 256: see kMultiTile), as rec_tiles with ntl = 1.
@@ -1172,20 +1040,6 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
                static_cast<uint32_t>(NQ == 1 ? 0 : seg_of<NQ>(0)) * K + 16 * g0, T.zeros, tid0 & 63u, nc,
                nc == kTile && aligned);
   }
-  // kRecRowDma: tile tn's first-step rows into the LDS tile (full tiles; the
-  // caller has made sure no wave still reads the tile)
-  auto dma_step0 = [&](uint32_t tn) __attribute__((always_inline)) {
-    dma_rows16<seg_of<NQ>(0) != 0>(tile, shp + 2u * static_cast<size_t>(tn) * kTile,
-                                   static_cast<uint32_t>(fresh(a.shard_len)), uniform(fresh(msk0[0])),
-                                   static_cast<uint32_t>(seg_of<NQ>(0)) * K + 16 * fresh(g0), fresh(g0),
-                                   fresh_v(tid0) & 63u);  // (fresh: nothing of it hoisted out of the tile loop)
-  };
-  auto full_at = [&](uint32_t t) __attribute__((always_inline)) {
-    return t < ntl && tile_cols(tile_at(t)) == kTile && aligned;
-  };
-  if constexpr (kRecRowDma<K, NQ>) {
-    if (full_at(0)) dma_step0(tile_at(0));
-  }
   if constexpr (NQ > 1) {
     // multiplier tables of the first two segment transforms (indices 2K, 3K or
     // K, 0), or of all of them (kRecResident): kept for every tile
@@ -1243,14 +1097,6 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
       if constexpr (!kRowPrefetch<NQ> && NP_MERGE_EARLY == 1)  // the merge's rows load during the FFT's cq pass
         issue_rows(raw, sh, shard_len, uniform(msk[NQ - 1]), 16 * g, T.zeros, lane, ncols, full);
       cq_read<K>(tile, fresh_v(cqb), XL, XH);
-      if constexpr (kRecRowDma<K, NQ>) {
-        // the tile is free from here when the copy-out goes from registers:
-        // the next tile's first-step rows land during the merge
-        if (full && out_vec_ok(a.out, a.out_stride) && full_at(t + 1)) {
-          __syncthreads();
-          dma_step0(tile_at(t + 1));
-        }
-      }
       cq_levels<K, false, true, 0>(T, vp0, 0, g, XL, XH, ~uniform(msk[NQ - 1]));  // erased rows only
       stamp(dbg, 29);
     }
@@ -1317,12 +1163,6 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
 #pragma unroll
           for (int e = 0; e < 8; ++e) o[e] = static_cast<uint8_t>((e < 4 ? v.x : v.y) >> (8 * (e & 3)));
         }
-      }
-    }
-    if constexpr (kRecRowDma<K, NQ>) {
-      if (full_at(t + 1)) {  // the tile's LDS copy-out is done
-        __syncthreads();
-        dma_step0(tile_at(t + 1));
       }
     }
     stamp(dbg, 31);
