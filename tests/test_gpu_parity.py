@@ -576,10 +576,12 @@ def test_reconstruct_multi_tile_workgroups_small_k(gpu, oracle, monkeypatch, nw,
     ds = torch.empty((batch, n, sl), dtype=torch.uint8, device="cuda")
     npa.encode_batch_dev(p, dp.data_ptr(), plen, plen, batch, ds.data_ptr(), n * sl, ctx=gpu, stream=stream())
     rng = np.random.default_rng(nw * 7 + tpw)
-    pres = np.ones((batch, n), dtype=np.uint8)
+    wn = p.wanted_n  # rows >= wanted_n are never produced: absent
+    pres = np.zeros((batch, n), dtype=np.uint8)
+    pres[:, :wn] = 1
     for b in range(batch):
         lo = k if b == 1 else 0  # payload 1 keeps every systematic row
-        pres[b, lo + rng.choice(n - lo, n - k - (1 if b == 2 else 0) - (n - k) // 3, replace=False)] = 0
+        pres[b, lo + rng.choice(wn - lo, wn - k - (1 if b == 2 else 0) - (wn - k) // 3, replace=False)] = 0
     dpres = dev(pres)
     olen = (sl // 2) * 2 * k
     out = torch.empty((batch, olen), dtype=torch.uint8, device="cuda")
