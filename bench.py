@@ -86,7 +86,7 @@ def aggregate_gib_s(world: int, per_rank: int, payload_len: int, elapsed: float,
     return world * per_rank * payload_len / (elapsed / steps) / 2**30
 
 
-ROUND_TAG = "r03"
+ROUND_TAG = "r04"
 
 
 def load_traffic(config: int):
