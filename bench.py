@@ -93,7 +93,7 @@ def load_traffic(config: int):
     """Per-launch HBM bytes (FETCH_SIZE + WRITE_SIZE, calibrated) of each kernel
     from the committed PMC summary of this round for this config
     (tools/profile_round.sh + tools/pmc_summary.py, measured on this same bench
-    command: profiles/r02_pmc_summary.json for config 3, r02_cfg<c>_... else)."""
+    command: profiles/r04_pmc_summary.json for config 3, r04_cfg<c>_... else)."""
     tag = ROUND_TAG if config == 3 else f"{ROUND_TAG}_cfg{config}"
     p = os.path.join(ROOT, "profiles", f"{tag}_pmc_summary.json")
     if not os.path.exists(p):
