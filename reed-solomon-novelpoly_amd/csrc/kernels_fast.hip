@@ -257,21 +257,12 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
 // once every wave has read it back for that last cq pass).  The launch record
 // is re-read from the kernarg segment at every tile, so that none of it stays
 // live in registers across the tile loop.
+// Multi-tile workgroups (k = 256 only).  Tried for the k = 64 / 128 decodes
+// too: 5-11 % slower at 190, 300 and 700 validators, neutral at config 2
+// (profiles/r04_ab.txt probe 11) -- there four workgroups share a CU, and
+// fewer, longer ones hid less.
 template <int K>
 constexpr bool kMultiTile = K == 256;
-// The decode's multi-tile workgroups (rec_tiles) at k = 64 / 128 as well
-// (NP_REC_MT_SMALL): the consecutive tiles of a payload in one workgroup share
-// its table staging, and the next tile's first-step rows load during the
-// copy-out (kRowPrefetch / kTilePrefetch).
-#ifndef NP_REC_MT_SMALL
-#define NP_REC_MT_SMALL 1
-#endif
-template <int K>
-constexpr bool kRecMultiTile = K == 256 || (NP_REC_MT_SMALL && (K == 64 || K == 128));
-// Per kernel instance: the k = 64 / 128 copy-and-2-segment instances (SERVE =
-// 2) keep one tile per workgroup (k = 64's spilled 134 dwords in rec_tiles).
-template <int K, int SERVE>
-constexpr bool kRecMT = K == 256 || (kRecMultiTile<K> && SERVE >= 4);
 
 // Table buffers of the multi-tile encode: the inverse transform's and one per
 // shift, staged once per workgroup (n <= 4K); with the 128 KiB tile they fill
@@ -721,7 +712,7 @@ __device__ __forceinline__ uint32_t seg_mask(const uint32_t (&msk)[NQ], int step
 #define NP_REC_TILE_PREFETCH 1
 #endif
 template <int K, int NQ>
-constexpr bool kTilePrefetch = NP_REC_TILE_PREFETCH && NQ == 4 && kRecMultiTile<K>;
+constexpr bool kTilePrefetch = NP_REC_TILE_PREFETCH && NQ == 4 && kMultiTile<K>;
 
 // PRE0: step 0's rows are in `raw` on entry (kTilePrefetch).
 template <int K, int NQ, bool PRE0 = false>
@@ -1196,7 +1187,7 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
   const uint8_t* rec = a.prefix + static_cast<size_t>(pb) * prefix_stride_c(N, K);
   const int nq = uniform(rec[0]);
   const uint32_t* rows = reinterpret_cast<const uint32_t*>(rec + prefix_pools_offset(N));
-  if constexpr (kRecMT<K, SERVE>) {
+  if constexpr (kMultiTile<K>) {
     if constexpr (SERVE >= 4) {
       if (nq == SERVE) rec_tiles<K, SERVE>(T, a, pres, rows, smem, pb, tl0, ntl, nsyms);
     } else if (nq == 1) {
@@ -1339,9 +1330,9 @@ size_t reconstruct_lds_bytes() {
 // variable that pins the count (tests).
 constexpr size_t kWorkgroups = 1024;
 
-template <int K, bool REC = false>
+template <int K>
 uint32_t tiles_per_workgroup(size_t batch, uint32_t tiles, const char* knob) {
-  if (!(REC ? kRecMultiTile<K> : kMultiTile<K>)) return 1;
+  if (!kMultiTile<K>) return 1;
   size_t want = batch * tiles / kWorkgroups;
   if (const char* e = std::getenv(knob)) want = std::strtoul(e, nullptr, 10);
   return static_cast<uint32_t>(std::max<size_t>(1, std::min<size_t>(tiles, want)));
@@ -1385,13 +1376,11 @@ hipError_t launch_reconstruct_k(const DevTables& T, const ReconstructArgs& a, hi
   if (nsyms == 0 || a.batch == 0) return hipSuccess;
   if (nsyms > 0xffffffffu) return hipErrorInvalidValue;
   const uint32_t tiles = static_cast<uint32_t>((nsyms + kTile - 1) / kTile);
-  const uint32_t tpw = tiles_per_workgroup<K, true>(a.batch, tiles, "NP_REC_TPW");
+  const uint32_t tpw = tiles_per_workgroup<K>(a.batch, tiles, "NP_REC_TPW");
   const size_t blocks = a.batch * ((tiles + tpw - 1) / tpw);
-  if (blocks > 0x7fffffffu || a.batch * tiles > 0x7fffffffu) return hipErrorInvalidValue;
-  const uint32_t tpw2 = kRecMT<K, 2> ? tpw : 1u;  // the copy / 2-segment instance
-  const size_t blocks2 = a.batch * ((tiles + tpw2 - 1) / tpw2);
-  k_reconstruct_fast<K, NQ, 2><<<static_cast<uint32_t>(blocks2), Geo<K>::kThreads, reconstruct_lds_bytes<K, NQ>(), s>>>(
-      T, a, static_cast<uint32_t>(nsyms), tiles, tpw2);
+  if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
+  k_reconstruct_fast<K, NQ, 2><<<static_cast<uint32_t>(blocks), Geo<K>::kThreads, reconstruct_lds_bytes<K, NQ>(), s>>>(
+      T, a, static_cast<uint32_t>(nsyms), tiles, tpw);
   if constexpr (NQ >= 4)
     k_reconstruct_fast<K, NQ, NQ><<<static_cast<uint32_t>(blocks), Geo<K>::kThreads, reconstruct_lds_bytes<K, NQ>(), s>>>(
         T, a, static_cast<uint32_t>(nsyms), tiles, tpw);

@@ -557,11 +557,12 @@ def test_encode_multi_tile_workgroups(gpu, oracle, monkeypatch, nw, tpw, batch, 
 @pytest.mark.parametrize("nw,kw,tpw,batch", [(256, 86, 2, 5), (256, 86, 4, 3), (300, 100, 3, 4), (512, 128, 2, 6),
                                               (700, 234, 4, 3)])
 def test_reconstruct_multi_tile_workgroups_small_k(gpu, oracle, monkeypatch, nw, kw, tpw, batch):
-    """k = 64 / 128 (4 and 8 segments): the full-decode instances run several
-    consecutive tiles per workgroup as well (kernels_fast.hip kRecMT), with the
-    next tile's first-step rows loaded during the copy-out at 4 segments.  771
-    columns = 3 full tiles and one of 3 columns; random erasures, some payloads
-    with every systematic row present (the single-tile copy instance)."""
+    """k = 64 / 128 (4 and 8 segments) over several tiles per payload with a
+    tile-count pin in the environment (one tile per workgroup there: kernels_fast.hip
+    kMultiTile; round 4 measured multi-tile workgroups slower at these k).
+    771 columns = 3 full tiles and one of 3 columns; random erasures, one
+    payload with every systematic row present (copy mode), one with a single
+    extra row."""
     import torch
 
     monkeypatch.setenv("NP_REC_TPW", str(tpw))
