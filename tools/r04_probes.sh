@@ -134,13 +134,4 @@ p11() {
   TAG=p11v190_ ARGS="--n-wanted 190 --batch 1024 --erase 64" bash tools/exp_one.sh base mt0 || exit $?
 }
 
-# Round-4 probe 12: GPU tests with no barrier before the encode's next-tile
-# payload DMA (the product), A/B against dmabar (NP_ENC_DMA_BARRIER=1) at config 3.
-p12() {
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r04/pytest_gpu12.log 2>&1; rc=$?
-  tail -3 gpurun_out/r04/pytest_gpu12.log
-  if [ $rc -ne 0 ]; then grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu12.log | head -20; exit $rc; fi
-  TAG=p12_ bash tools/exp_one.sh base dmabar base dmabar base dmabar || exit $?
-}
-
 "$@"
