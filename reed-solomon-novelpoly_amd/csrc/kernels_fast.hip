@@ -307,6 +307,12 @@ __device__ __forceinline__ void dma_tile(const uint8_t* pay, uint32_t ch0, uint8
   }
 }
 
+// NP_ENC_DMA_NOBAR (experiment): no workgroup barrier before the
+// next tile's payload DMA with the quad exchange.
+#ifndef NP_ENC_DMA_NOBAR
+#define NP_ENC_DMA_NOBAR 0
+#endif
+
 // One shift of the encode (rows sK .. sK+K-1), SH = 1..3.  With `dma_pay`,
 // the last cq pass starts the next tile's payload DMA once every wave has read
 // the tile.
@@ -356,7 +362,14 @@ __device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArg
     cq_read_p<K>(tile, fresh_v(cqb), XL, XH);
   }
   if (dma_pay) {
-    __syncthreads();  // every wave has its cq registers: the tile is free
+    if constexpr (kEncQx<K> && NP_ENC_DMA_NOBAR) {
+      // wave g's quad items and its share of the next payload tile are the
+      // same 8 KiB (cq_read_q, dma_tile): once its own reads are back, no
+      // other wave touches that region
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    } else {
+      __syncthreads();  // every wave has its cq registers: the tile is free
+    }
     if constexpr (!(kExp & 4)) dma_tile<K>(dma_pay, dma_ch0, tile, g, lane);
   }
   stamp(dbg, st0 + 1);
