@@ -104,15 +104,15 @@ template <int K, int SH>
 constexpr bool kEncConv = SH != 0 && enc_conv(K, SH == 23 ? 2u : static_cast<uint32_t>(SH));
 
 // The forward cq levels of shift sh, ending in Cantor coordinates.
-template <int K, int SH>
+template <int K, int SH, typename POST = NoPost>
 __device__ __forceinline__ void shift_cq(const DevTables& T, const uint32_t* vp, uint32_t index, uint32_t g,
-                                         uint32_t (&XL)[16], uint32_t (&XH)[16]) {
+                                         uint32_t (&XL)[16], uint32_t (&XH)[16], POST post = POST{}) {
   if constexpr (SH == 0) {
-    cq_levels<K, false, false, -1>(T, vp, index, g, XL, XH);
+    cq_levels<K, false, false, -1>(T, vp, index, g, XL, XH, ~0u, post);
   } else {
     static_assert(SH != 23 || kShiftGen<K, 2> == kShiftGen<K, 3>, "shifts 2 and 3 share one instance");
     static_assert(SH != 23 || enc_conv(K, 2) == enc_conv(K, 3), "shifts 2 and 3 share one instance");
-    cq_levels<K, false, false, kShiftGen<K, SH>, kEncConv<K, SH>>(T, vp, index, g, XL, XH);
+    cq_levels<K, false, false, kShiftGen<K, SH>, kEncConv<K, SH>>(T, vp, index, g, XL, XH, ~0u, post);
     if constexpr (!kEncConv<K, SH>) tower_convert(T, XL, XH);  // back to Cantor coordinates for the shard rows
   }
 }
@@ -286,14 +286,16 @@ typedef const __attribute__((address_space(4))) EncLaunch* enc_launch_ptr;
 // before the next LDS reads, which would also wait for the row stores issued
 // after these loads; encode_tile_multi waits with a counted vmcnt instead.
 template <int K>
-__device__ __forceinline__ void dma_tile(const uint8_t* pay, uint32_t ch0, uint8_t* tile, uint32_t w, uint32_t lane) {
+__device__ __forceinline__ void dma_tile(const uint8_t* pay, uint32_t ch0, uint8_t* tile, uint32_t w, uint32_t lane,
+                                         uint32_t j0 = 0, uint32_t nj = 16 * (2 * K / 256)) {
   static_assert(Geo<K>::P == 1 && Geo<K>::W == Geo<K>::Q, "one swizzle row per column");
   constexpr uint32_t kColBytes = 2 * K, kPieces = 2 * K / 256;  // 256-byte pieces per column
   const uint32_t sw0 = swz<K>(16u * w);
   const uint32_t lds0 = static_cast<uint32_t>(
       reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)(tile)));
+  // pieces j0 .. j0 + nj - 1 of the wave's 16 kPieces (all of them by default)
 #pragma unroll
-  for (uint32_t j = 0; j < 16 * kPieces; ++j) {
+  for (uint32_t j = j0; j < j0 + nj; ++j) {
     const uint32_t c = 16u * w + j / kPieces;                   // column (wave-uniform)
     const uint32_t sw = sw0 ^ swz<K>(j / kPieces);              // swz(c): linear in c
     const uint32_t b = (j % kPieces) * 32u + (lane >> 1);       // LDS block of this lane
@@ -311,6 +313,15 @@ __device__ __forceinline__ void dma_tile(const uint8_t* pay, uint32_t ch0, uint8
 // next tile's payload DMA with the quad exchange.
 #ifndef NP_ENC_DMA_NOBAR
 #define NP_ENC_DMA_NOBAR 0
+#endif
+// NP_ENC_DMA_SPREAD (experiment): the 32 LDS-DMA pieces of a wave's share of
+// the next payload tile go out 8 at once and then 3 after each level-0 group
+// of the last shift's cq pass, instead of all 32 at once: a burst fills the
+// wave's memory queue and stalls its issue until HBM drains it
+// (profiles/r04_encode_stamps_hiw.txt: ≈14k ticks in the last shift's
+// exchange phase for even the slowest waves).
+#ifndef NP_ENC_DMA_SPREAD
+#define NP_ENC_DMA_SPREAD 0
 #endif
 
 // One shift of the encode (rows sK .. sK+K-1), SH = 1..3.  With `dma_pay`,
@@ -370,13 +381,21 @@ __device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArg
     } else {
       __syncthreads();  // every wave has its cq registers: the tile is free
     }
-    if constexpr (!(kExp & 4)) dma_tile<K>(dma_pay, dma_ch0, tile, g, lane);
+    if constexpr (!(kExp & 4)) dma_tile<K>(dma_pay, dma_ch0, tile, g, lane, 0, NP_ENC_DMA_SPREAD ? 8 : 32);
   }
   stamp(dbg, st0 + 1);
   const uint32_t row0 = index + 16 * g;
   const uint32_t wanted = (kExp & 2) ? 0u : a.wanted_n;
   const bool nt = rows_nt(a.shards, a.batch_stride, a.shard_len);
-  shift_cq<K, SH>(T, vp, index, g, XL, XH);
+  if constexpr (NP_ENC_DMA_SPREAD && !(kExp & 4)) {
+    static_assert(2 * K / 256 * 16 == 32, "32 pieces per wave");
+    auto post = [&](int t) __attribute__((always_inline)) {
+      if (dma_pay) dma_tile<K>(dma_pay, dma_ch0, tile, g, lane, 8u + 3u * static_cast<uint32_t>(t), 3);
+    };
+    shift_cq<K, SH>(T, vp, index, g, XL, XH, post);
+  } else {
+    shift_cq<K, SH>(T, vp, index, g, XL, XH);
+  }
   stamp(dbg, st0 + 2);
   store_rows(out, a.shard_len, row0, wanted, XL, XH, lane, ncols, full, nt);
   stamp(dbg, st0 + 3);

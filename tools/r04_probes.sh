@@ -134,21 +134,27 @@ p11() {
   TAG=p11v190_ ARGS="--n-wanted 190 --batch 1024 --erase 64" bash tools/exp_one.sh base mt0 || exit $?
 }
 
-# Round-4 probe 13: the encode without the barrier before the next tile's
-# payload DMA (nobar: NP_ENC_DMA_NOBAR=1; parity first), the merge rows loaded
-# during the forward high pass (merge2: NP_MERGE_EARLY=2) with the tile
-# prefetch in place, and the decode's tiles per workgroup (NP_REC_TPW 4 / 16
-# against the launcher's 8) at config 3.
+# Round-4 probe 13: the encode's next-tile payload DMA without the barrier
+# (nobar: NP_ENC_DMA_NOBAR=1), spread over the last cq pass (spread:
+# NP_ENC_DMA_SPREAD=1; spreadnb: both; parity first for the two riskier ones),
+# the merge rows loaded during the forward high pass (merge2: NP_MERGE_EARLY=2),
+# and the decode's tiles per workgroup (NP_REC_TPW 4 / 16 against the
+# launcher's 8) at config 3; cross-lane move rates (permlane_rates).
 p13() {
-  NP_LIB_PATH=$PWD/tools/exp/lib_nobar.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r04/pytest_gpu13_nobar.log 2>&1; rc=$?
-  tail -3 gpurun_out/r04/pytest_gpu13_nobar.log
-  if [ $rc -ne 0 ]; then grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu13_nobar.log | head -20; exit $rc; fi
-  TAG=p13_ bash tools/exp_one.sh base nobar merge2 base nobar merge2 || exit $?
+  for v in nobar spreadnb; do
+    NP_LIB_PATH=$PWD/tools/exp/lib_$v.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r04/pytest_gpu13_$v.log 2>&1; rc=$?
+    tail -2 gpurun_out/r04/pytest_gpu13_$v.log
+    if [ $rc -ne 0 ]; then grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu13_$v.log | head -20; exit $rc; fi
+  done
+  TAG=p13_ bash tools/exp_one.sh base nobar spread spreadnb merge2 base nobar spread spreadnb merge2 || exit $?
   for t in 4 16 8; do
     NP_REC_TPW=$t timeout -k 10 120 python bench.py --no-cpu --steps 10 --warmup 2 > gpurun_out/exp/p13_tpw$t.log 2>&1 || { tail -3 gpurun_out/exp/p13_tpw$t.log; exit 1; }
     python3 -c "
-import json; d=json.loads(open('gpurun_out/exp/p13_tpw$t.log').read().strip().split('\n')[-1]); print('p13_tpw$t', d['value'], {k:v['ms'] for k,v in d['kernels'].items()})"
+import json; d=json.loads(open('gpurun_out/exp/p13_tpw$t.log').read().strip().split('\\n')[-1]); print('p13_tpw$t', d['value'], {k:v['ms'] for k,v in d['kernels'].items()})"
   done
+  [ -x tools/microbench/permlane_rates ] || make -s -C tools/microbench permlane_rates || exit 1
+  timeout -k 10 120 tools/microbench/permlane_rates > gpurun_out/r04/permlane_rates.txt 2>&1 || exit 1
+  cat gpurun_out/r04/permlane_rates.txt
 }
 
 "$@"
