@@ -286,16 +286,14 @@ typedef const __attribute__((address_space(4))) EncLaunch* enc_launch_ptr;
 // before the next LDS reads, which would also wait for the row stores issued
 // after these loads; encode_tile_multi waits with a counted vmcnt instead.
 template <int K>
-__device__ __forceinline__ void dma_tile(const uint8_t* pay, uint32_t ch0, uint8_t* tile, uint32_t w, uint32_t lane,
-                                         uint32_t j0 = 0, uint32_t nj = 16 * (2 * K / 256)) {
+__device__ __forceinline__ void dma_tile(const uint8_t* pay, uint32_t ch0, uint8_t* tile, uint32_t w, uint32_t lane) {
   static_assert(Geo<K>::P == 1 && Geo<K>::W == Geo<K>::Q, "one swizzle row per column");
   constexpr uint32_t kColBytes = 2 * K, kPieces = 2 * K / 256;  // 256-byte pieces per column
   const uint32_t sw0 = swz<K>(16u * w);
   const uint32_t lds0 = static_cast<uint32_t>(
       reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)(tile)));
-  // pieces j0 .. j0 + nj - 1 of the wave's 16 kPieces (all of them by default)
 #pragma unroll
-  for (uint32_t j = j0; j < j0 + nj; ++j) {
+  for (uint32_t j = 0; j < 16 * kPieces; ++j) {
     const uint32_t c = 16u * w + j / kPieces;                   // column (wave-uniform)
     const uint32_t sw = sw0 ^ swz<K>(j / kPieces);              // swz(c): linear in c
     const uint32_t b = (j % kPieces) * 32u + (lane >> 1);       // LDS block of this lane
@@ -309,19 +307,13 @@ __device__ __forceinline__ void dma_tile(const uint8_t* pay, uint32_t ch0, uint8
   }
 }
 
-// NP_ENC_DMA_NOBAR (experiment): no workgroup barrier before the
-// next tile's payload DMA with the quad exchange.
+// NP_ENC_DMA_NOBAR: no workgroup barrier before the next tile's payload DMA
+// with the quad exchange (each wave's DMA share is the LDS region only it
+// reads back).  Measured: encode 1.646 / 1.648 -> 1.638 / 1.638 ms (-0.6 %,
+// profiles/r04_ab.txt probe 13).  Spreading the 32 DMA pieces over the last
+// cq pass instead of issuing them at once measured +0.3 to +0.7 %.
 #ifndef NP_ENC_DMA_NOBAR
-#define NP_ENC_DMA_NOBAR 0
-#endif
-// NP_ENC_DMA_SPREAD (experiment): the 32 LDS-DMA pieces of a wave's share of
-// the next payload tile go out 8 at once and then 3 after each level-0 group
-// of the last shift's cq pass, instead of all 32 at once: a burst fills the
-// wave's memory queue and stalls its issue until HBM drains it
-// (profiles/r04_encode_stamps_hiw.txt: ≈14k ticks in the last shift's
-// exchange phase for even the slowest waves).
-#ifndef NP_ENC_DMA_SPREAD
-#define NP_ENC_DMA_SPREAD 0
+#define NP_ENC_DMA_NOBAR 1
 #endif
 
 // One shift of the encode (rows sK .. sK+K-1), SH = 1..3.  With `dma_pay`,
@@ -381,21 +373,13 @@ __device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArg
     } else {
       __syncthreads();  // every wave has its cq registers: the tile is free
     }
-    if constexpr (!(kExp & 4)) dma_tile<K>(dma_pay, dma_ch0, tile, g, lane, 0, NP_ENC_DMA_SPREAD ? 8 : 32);
+    if constexpr (!(kExp & 4)) dma_tile<K>(dma_pay, dma_ch0, tile, g, lane);
   }
   stamp(dbg, st0 + 1);
   const uint32_t row0 = index + 16 * g;
   const uint32_t wanted = (kExp & 2) ? 0u : a.wanted_n;
   const bool nt = rows_nt(a.shards, a.batch_stride, a.shard_len);
-  if constexpr (NP_ENC_DMA_SPREAD && !(kExp & 4)) {
-    static_assert(2 * K / 256 * 16 == 32, "32 pieces per wave");
-    auto post = [&](int t) __attribute__((always_inline)) {
-      if (dma_pay) dma_tile<K>(dma_pay, dma_ch0, tile, g, lane, 8u + 3u * static_cast<uint32_t>(t), 3);
-    };
-    shift_cq<K, SH>(T, vp, index, g, XL, XH, post);
-  } else {
-    shift_cq<K, SH>(T, vp, index, g, XL, XH);
-  }
+  shift_cq<K, SH>(T, vp, index, g, XL, XH);
   stamp(dbg, st0 + 2);
   store_rows(out, a.shard_len, row0, wanted, XL, XH, lane, ncols, full, nt);
   stamp(dbg, st0 + 3);
