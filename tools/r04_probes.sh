@@ -157,4 +157,13 @@ import json; d=json.loads(open('gpurun_out/exp/p13_tpw$t.log').read().strip().sp
   cat gpurun_out/r04/permlane_rates.txt
 }
 
+# Round-4 probe 14: per-wave phase stamps of the final config-3 encode and
+# decode (NP_EXP=192 build st192).
+p14() {
+  NP_LIB_PATH=$PWD/tools/exp/lib_st192.so timeout -k 10 120 python tools/wave_stamps.py > gpurun_out/r04/wave_stamps_final.log 2>&1 || { tail -5 gpurun_out/r04/wave_stamps_final.log; exit 1; }
+  NP_LIB_PATH=$PWD/tools/exp/lib_st192.so timeout -k 10 120 python tools/enc_stamps.py > gpurun_out/r04/enc_stamps_final.log 2>&1 || { tail -5 gpurun_out/r04/enc_stamps_final.log; exit 1; }
+  head -32 gpurun_out/r04/wave_stamps_final.log
+  head -24 gpurun_out/r04/enc_stamps_final.log
+}
+
 "$@"
