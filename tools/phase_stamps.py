@@ -20,17 +20,21 @@ torch.cuda.set_stream(torch.cuda.Stream())
 s = torch.cuda.current_stream().cuda_stream
 sl = p.make_encoder(ctx).shard_len(plen)
 pay = torch.randint(0, 256, (b, plen), dtype=torch.uint8, device="cuda")
-sh = torch.empty((b, n, sl), dtype=torch.uint8, device="cuda")
+# the stamped encode (NP_EXP bit 6) writes its own stamps past each payload's
+# rows (kernels_fast.hip encode_tile_multi: n shard_len + 4 KiB per tile)
+enc_tiles = (plen // (2 * k) + 255) // 256 + 1
+bstride = n * sl + 4096 * enc_tiles
+sh = torch.zeros((b, bstride), dtype=torch.uint8, device="cuda")
 pres = torch.from_numpy(np.stack([synth.present_mask(i, n, cfg["erase"]) for i in range(b)])).cuda()
 out_len = (sl // 2) * 2 * k
 stride = out_len + 4096
 out = torch.zeros((b, stride), dtype=torch.uint8, device="cuda")
-npa.encode_batch_dev(p, pay.data_ptr(), plen, plen, b, sh.data_ptr(), n * sl, ctx=ctx, stream=s)
+npa.encode_batch_dev(p, pay.data_ptr(), plen, plen, b, sh.data_ptr(), bstride, ctx=ctx, stream=s)
 for it in range(3):
     out.zero_()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    npa.reconstruct_batch_dev2(p, sh.data_ptr(), sl, n * sl, pres.data_ptr(), 0, b, out.data_ptr(), stride,
+    npa.reconstruct_batch_dev2(p, sh.data_ptr(), sl, bstride, pres.data_ptr(), 0, b, out.data_ptr(), stride,
                                ctx=ctx, stream=s)
     e1.record()
     torch.cuda.synchronize()
