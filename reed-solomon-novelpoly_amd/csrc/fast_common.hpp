@@ -108,18 +108,22 @@ __host__ __device__ constexpr uint32_t swz(uint32_t cs) {
 // Byte offset of block 0 of column c; block m is at col_base(c) ^ 8m.  The map
 // is linear in the bits of c, so col_base(c1 | c2) == col_base(c1) ^ col_base(c2)
 // for disjoint bit sets.
-template <int K>
+// EVEN: the swizzle with bit 0 cleared, so blocks 2i and 2i + 1 of a column
+// stay a contiguous, 16-byte aligned pair (the multi-tile encode's payload
+// tile with 16-byte LDS-DMA pieces, kernels_fast.hip NP_ENC_DMA_X4: its cq
+// reads then conflict 2-way).
+template <int K, bool EVEN = false>
 __host__ __device__ constexpr uint32_t col_base_c(uint32_t c) {
   using G = Geo<K>;
   const uint32_t cs = c / G::P, ci = c % G::P;
-  return 8u * cs * G::W + 8u * ((ci * G::Q) ^ swz<K>(cs));
+  return 8u * cs * G::W + 8u * ((ci * G::Q) ^ (swz<K>(cs) & (EVEN ? ~1u : ~0u)));
 }
 
 // Runtime version; the asm keeps the compiler from materialising every block
 // address of a sweep in its own VGPR.
-template <int K>
+template <int K, bool EVEN = false>
 __device__ __forceinline__ uint32_t col_base(uint32_t c) {
-  uint32_t b = col_base_c<K>(c);
+  uint32_t b = col_base_c<K, EVEN>(c);
   asm volatile("" : "+v"(b));
   return b;
 }
@@ -1177,14 +1181,14 @@ __device__ __forceinline__ void tower_convert(const DevTables& T, uint32_t (&L)[
 }
 
 // ---------------------------------------------------------- LDS sweeps ----
-template <int K>
+template <int K, bool EVEN = false>
 __device__ __forceinline__ void cq_read(const uint8_t* tile, uint32_t base, uint32_t (&L)[16], uint32_t (&H)[16]) {
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     uint2 d[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      d[i] = *reinterpret_cast<const uint2*>(tile + (base ^ (col_base_c<K>(i) ^ (8u * u))));
+      d[i] = *reinterpret_cast<const uint2*>(tile + (base ^ (col_base_c<K, EVEN>(i) ^ (8u * u))));
     blks_to_cq(d, &L[4 * u], &H[4 * u]);
   }
 }

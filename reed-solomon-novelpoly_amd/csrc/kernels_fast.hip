@@ -316,6 +316,43 @@ __device__ __forceinline__ void dma_tile(const uint8_t* pay, uint32_t ch0, uint8
 #define NP_ENC_DMA_NOBAR 1
 #endif
 
+// NP_ENC_DMA_X4 (experiment): the next tile's payload by 16-byte LDS-DMA
+// pieces (8 per wave instead of 32 of 4 bytes), which needs the payload tile's
+// swizzle at 16-byte granularity (col_base EVEN).  Hypothesis from the stamps
+// (profiles/r04_encode_stamps_hiw.txt): 32 pieces per wave overfill the
+// wave's memory queue, so the DMA's issue stalls every wave of the CU.
+#ifndef NP_ENC_DMA_X4
+#define NP_ENC_DMA_X4 0
+#endif
+template <int K>
+constexpr bool kEncDmaX4 = NP_ENC_DMA_X4 && K == 256;
+
+// kEncDmaX4: wave w's columns 16w..16w+15 in 8 pieces of two columns (lanes
+// 0-31 the first, 32-63 the second, 16 bytes each): lane l of a piece writes
+// LDS blocks 2(l & 31), 2(l & 31) + 1 of its column, which hold the payload's
+// contiguous blocks 2(l & 31) ^ sw, (2(l & 31) ^ sw) + 1 (sw even).
+template <int K>
+__device__ __forceinline__ void dma_tile_x4(const uint8_t* pay, uint32_t ch0, uint8_t* tile, uint32_t w, uint32_t lane) {
+  static_assert(K == 256, "two 512-byte columns per 1 KiB piece");
+  constexpr uint32_t kColBytes = 2 * K;
+  const uint32_t lds0 = static_cast<uint32_t>(
+      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)(tile)));
+  const uint32_t half = lane >> 5, li = lane & 31u;
+  const uint32_t swh = half ? (swz<K>(1) & ~1u) : 0u;  // the odd column's part of the (linear) swizzle
+#pragma unroll
+  for (uint32_t j = 0; j < 8; ++j) {
+    const uint32_t c0 = 16u * w + 2u * j;  // wave-uniform first column of the piece
+    const uint32_t sw = (swz<K>(c0) & ~1u) ^ swh;
+    const uint8_t* src = pay + static_cast<size_t>(ch0 + c0 + half) * kColBytes + 8u * ((2u * li) ^ sw);
+    const uint32_t dst = uniform(lds0 + c0 * kColBytes);
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" NP_DMA_MOD "\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(dst)
+                 : "memory");
+  }
+}
+
 // One shift of the encode (rows sK .. sK+K-1), SH = 1..3.  With `dma_pay`,
 // the last cq pass starts the next tile's payload DMA once every wave has read
 // the tile.
@@ -373,7 +410,12 @@ __device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArg
     } else {
       __syncthreads();  // every wave has its cq registers: the tile is free
     }
-    if constexpr (!(kExp & 4)) dma_tile<K>(dma_pay, dma_ch0, tile, g, lane);
+    if constexpr (kExp & 4) {
+    } else if constexpr (kEncDmaX4<K>) {
+      dma_tile_x4<K>(dma_pay, dma_ch0, tile, g, lane);
+    } else {
+      dma_tile<K>(dma_pay, dma_ch0, tile, g, lane);
+    }
   }
   stamp(dbg, st0 + 1);
   const uint32_t row0 = index + 16 * g;
@@ -411,7 +453,7 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
   stamp(dbg, 0);
   // whole tiles load by 8-byte vector loads at any address; the LDS-DMA of the
   // next tile's payload (4-byte pieces) only from 8-byte aligned payloads
-  const bool aligned_pay = (reinterpret_cast<uintptr_t>(pay) & 7u) == 0;
+  const bool aligned_pay = (reinterpret_cast<uintptr_t>(pay) & (kEncDmaX4<K> ? 15u : 7u)) == 0;
   auto tile_whole = [&](uint32_t t) __attribute__((always_inline)) {
     return static_cast<size_t>(t * kTile + kTile) * 2 * K <= a.payload_len;
   };
@@ -425,7 +467,7 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else {
     const uint32_t c0 = tid / G::Q, m0 = tid % G::Q;
-    const uint32_t base = col_base<K>(c0) ^ (8u * m0);
+    const uint32_t base = col_base<K, kEncDmaX4<K>>(c0) ^ (8u * m0);
     const size_t gbase = static_cast<size_t>(ch0 + c0) * 2 * K + 8u * m0;
     if (out_vec_ok(pay, 0) && tile_whole(tl)) {
       uint2 v[16];
@@ -433,7 +475,7 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
       for (int i = 0; i < 16; ++i)
         v[i] = (kExp & 4) ? make_uint2(i, tid) : load_once(pay + gbase + static_cast<size_t>(i) * 32 * K);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) *reinterpret_cast<uint2*>(tile + (base ^ col_base_c<K>(16u * i))) = v[i];
+      for (int i = 0; i < 16; ++i) *reinterpret_cast<uint2*>(tile + (base ^ col_base_c<K, kEncDmaX4<K>>(16u * i))) = v[i];
     } else {
 #pragma unroll 1
       for (uint32_t i = 0; i < 16; ++i) {
@@ -442,7 +484,7 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
 #pragma unroll
         for (int e = 0; e < 8; ++e)
           if (g0 + e < a.payload_len) w[e >> 2] |= static_cast<uint32_t>(pay[g0 + e]) << (8 * (e & 3));
-        *reinterpret_cast<uint2*>(tile + (base ^ col_base_c<K>(16u * i))) = make_uint2(w[0], w[1]);
+        *reinterpret_cast<uint2*>(tile + (base ^ col_base_c<K, kEncDmaX4<K>>(16u * i))) = make_uint2(w[0], w[1]);
       }
     }
   }
@@ -455,10 +497,10 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
   __syncthreads();
   stamp(dbg, 1);
 
-  const uint32_t cqb = col_base<K>(4 * lane) ^ (32u * g);
+  const uint32_t cqb = col_base<K, kEncDmaX4<K>>(4 * lane) ^ (32u * g);  // the payload tile's swizzle
   {
     uint32_t CL[16], CH[16];
-    cq_read<K>(tile, cqb, CL, CH);
+    cq_read<K, kEncDmaX4<K>>(tile, cqb, CL, CH);
     store_rows(out, a.shard_len, 16 * g, (kExp & 2) ? 0u : a.wanted_n, CL, CH, lane, ncols, full,
                rows_nt(a.shards, a.batch_stride, a.shard_len));
     stamp(dbg, 2);

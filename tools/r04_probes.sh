@@ -166,4 +166,13 @@ p14() {
   head -24 gpurun_out/r04/enc_stamps_final.log
 }
 
+# Round-4 probe 15: the next tile's payload by 16-byte LDS-DMA pieces
+# (x4: NP_ENC_DMA_X4=1; parity first) against the product at config 3.
+p15() {
+  NP_LIB_PATH=$PWD/tools/exp/lib_x4.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fuzz.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r04/pytest_gpu15_x4.log 2>&1; rc=$?
+  tail -2 gpurun_out/r04/pytest_gpu15_x4.log
+  if [ $rc -ne 0 ]; then grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu15_x4.log | head -20; exit $rc; fi
+  TAG=p15_ bash tools/exp_one.sh base x4 base x4 base x4 || exit $?
+}
+
 "$@"
