@@ -316,13 +316,15 @@ __device__ __forceinline__ void dma_tile(const uint8_t* pay, uint32_t ch0, uint8
 #define NP_ENC_DMA_NOBAR 1
 #endif
 
-// NP_ENC_DMA_X4 (experiment): the next tile's payload by 16-byte LDS-DMA
-// pieces (8 per wave instead of 32 of 4 bytes), which needs the payload tile's
-// swizzle at 16-byte granularity (col_base EVEN).  Hypothesis from the stamps
-// (profiles/r04_encode_stamps_hiw.txt): 32 pieces per wave overfill the
-// wave's memory queue, so the DMA's issue stalls every wave of the CU.
+// NP_ENC_DMA_X4: the next tile's payload by 16-byte LDS-DMA pieces (8 per
+// wave instead of 32 of 4 bytes), which needs the payload tile's swizzle at
+// 16-byte granularity (col_base EVEN; the tile's cq reads then conflict 2-way).
+// From the stamps (profiles/r04_encode_stamps_hiw.txt): 32 pieces per wave
+// overfill the wave's memory queue and the DMA's issue stalls.  Measured:
+// encode 1.625 / 1.630 / 1.625 -> 1.598 / 1.603 / 1.596 ms (-1.7 %,
+// profiles/r04_ab.txt probe 15).
 #ifndef NP_ENC_DMA_X4
-#define NP_ENC_DMA_X4 0
+#define NP_ENC_DMA_X4 1
 #endif
 template <int K>
 constexpr bool kEncDmaX4 = NP_ENC_DMA_X4 && K == 256;
