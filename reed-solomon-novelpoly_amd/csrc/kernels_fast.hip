@@ -329,6 +329,16 @@ __device__ __forceinline__ void dma_tile(const uint8_t* pay, uint32_t ch0, uint8
 template <int K>
 constexpr bool kEncDmaX4 = NP_ENC_DMA_X4 && K == 256;
 
+// NP_ENC_DMA_WAVES (experiment, with kEncDmaX4): only waves 0..W-1 issue the
+// next tile's DMA pieces (16 / W waves' shares each) after a barrier, so that
+// the other waves start the last cq pass instead of waiting to issue theirs.
+#ifndef NP_ENC_DMA_WAVES
+#define NP_ENC_DMA_WAVES 16
+#endif
+#ifndef NP_ENC_DMA_YOUNG
+#define NP_ENC_DMA_YOUNG 0
+#endif
+
 // kEncDmaX4: wave w's columns 16w..16w+15 in 8 pieces of two columns (lanes
 // 0-31 the first, 32-63 the second, 16 bytes each): lane l of a piece writes
 // LDS blocks 2(l & 31), 2(l & 31) + 1 of its column, which hold the payload's
@@ -404,7 +414,15 @@ __device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArg
     cq_read_p<K>(tile, fresh_v(cqb), XL, XH);
   }
   if (dma_pay) {
-    if constexpr (kEncQx<K> && NP_ENC_DMA_NOBAR) {
+    if constexpr (kEncDmaX4<K> && NP_ENC_DMA_WAVES < 16) {
+      constexpr uint32_t W = NP_ENC_DMA_WAVES;
+      __syncthreads();  // every wave has its cq registers: the tile is free
+      const uint32_t gi = NP_ENC_DMA_YOUNG ? g - (16u - W) : g;  // the youngest W waves instead
+      if (gi < W) {
+#pragma unroll
+        for (uint32_t r = 0; r < 16 / W; ++r) dma_tile_x4<K>(dma_pay, dma_ch0, tile, gi + W * r, lane);
+      }
+    } else if constexpr (kEncQx<K> && NP_ENC_DMA_NOBAR) {
       // wave g's quad items and its share of the next payload tile are the
       // same 8 KiB (cq_read_q, dma_tile): once its own reads are back, no
       // other wave touches that region
@@ -412,7 +430,7 @@ __device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArg
     } else {
       __syncthreads();  // every wave has its cq registers: the tile is free
     }
-    if constexpr (kExp & 4) {
+    if constexpr ((kExp & 4) || (kEncDmaX4<K> && NP_ENC_DMA_WAVES < 16)) {
     } else if constexpr (kEncDmaX4<K>) {
       dma_tile_x4<K>(dma_pay, dma_ch0, tile, g, lane);
     } else {
