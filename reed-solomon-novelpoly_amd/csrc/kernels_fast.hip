@@ -338,6 +338,11 @@ constexpr bool kEncDmaX4 = NP_ENC_DMA_X4 && K == 256;
 #ifndef NP_ENC_DMA_YOUNG
 #define NP_ENC_DMA_YOUNG 0
 #endif
+// NP_ENC_DMA_SADDR: the x4 pieces' addresses as a scalar base plus a 32-bit
+// lane offset (1 VALU per piece instead of 7 for 64-bit per-lane addresses).
+#ifndef NP_ENC_DMA_SADDR
+#define NP_ENC_DMA_SADDR 1
+#endif
 
 // kEncDmaX4: wave w's columns 16w..16w+15 in 8 pieces of two columns (lanes
 // 0-31 the first, 32-63 the second, 16 bytes each): lane l of a piece writes
@@ -351,6 +356,24 @@ __device__ __forceinline__ void dma_tile_x4(const uint8_t* pay, uint32_t ch0, ui
       reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)(tile)));
   const uint32_t half = lane >> 5, li = lane & 31u;
   const uint32_t swh = half ? (swz<K>(1) & ~1u) : 0u;  // the odd column's part of the (linear) swizzle
+  if constexpr (NP_ENC_DMA_SADDR) {
+    // scalar base per piece (column 16w + 2j), 32-bit lane offset: the swizzle
+    // is linear, so piece j's offset is the lane's piece-0 offset XOR a constant
+    const uint32_t off0 = 512u * half + 8u * ((2u * li) ^ (swz<K>(16u * w) & ~1u) ^ swh);
+    const uint8_t* base = pay + static_cast<size_t>(ch0 + 16u * w) * kColBytes;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+      const uint32_t off = off0 ^ (8u * (swz<K>(2u * j) & ~1u));
+      const uint8_t* sb = base + 2u * j * kColBytes;
+      const uint32_t dst = uniform(lds0 + (16u * w + 2u * j) * kColBytes);
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" NP_DMA_MOD "\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(off), "s"(sb), "s"(dst)
+                   : "memory");
+    }
+    return;
+  }
 #pragma unroll
   for (uint32_t j = 0; j < 8; ++j) {
     const uint32_t c0 = 16u * w + 2u * j;  // wave-uniform first column of the piece

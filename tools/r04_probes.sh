@@ -175,16 +175,20 @@ p15() {
   TAG=p15_ bash tools/exp_one.sh base x4 base x4 base x4 || exit $?
 }
 
-# Round-4 probe 16: the next tile's DMA from 4 or 8 waves only (after a
-# barrier; 'w4', 'w8', 'w4y' = the youngest 4), parity first, against the
-# product at config 3; then the product's encode stamps (x4 DMA)
-p16() {
-  for v in w4 w8 w4y; do
-    NP_LIB_PATH=$PWD/tools/exp/lib_$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "encode or roundtrip" > gpurun_out/r04/pytest_gpu16_$v.log 2>&1; rc=$?
-    echo "$v: $(tail -1 gpurun_out/r04/pytest_gpu16_$v.log)"
-    [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu16_$v.log | head -20; exit $rc; }
+# Round-4 probe 17: the product with scalar-base DMA addresses (parity
+# suite), against the 64-bit per-lane addresses ('sad0') and the next tile's
+# DMA from 4 or 8 waves only after a barrier ('w4', 'w8'), at config 3; then
+# the product's encode stamps
+p17() {
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fuzz.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r04/pytest_gpu17.log 2>&1; rc=$?
+  echo "product: $(tail -1 gpurun_out/r04/pytest_gpu17.log)"
+  [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu17.log | head -20; exit $rc; }
+  for v in w4 w8; do
+    NP_LIB_PATH=$PWD/tools/exp/lib_$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "encode or roundtrip" > gpurun_out/r04/pytest_gpu17_$v.log 2>&1; rc=$?
+    echo "$v: $(tail -1 gpurun_out/r04/pytest_gpu17_$v.log)"
+    [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu17_$v.log | head -20; exit $rc; }
   done
-  TAG=p16_ bash tools/exp_one.sh base w4 w8 w4y base w4 w8 w4y || exit $?
+  TAG=p17_ bash tools/exp_one.sh base sad0 w4 w8 base sad0 w4 w8 || exit $?
   NP_LIB_PATH=$PWD/tools/exp/lib_st192.so timeout -k 10 120 python tools/enc_stamps.py > gpurun_out/r04/enc_stamps_x4.txt 2>&1 || exit $?
   tail -22 gpurun_out/r04/enc_stamps_x4.txt
 }
