@@ -975,6 +975,21 @@ __device__ __forceinline__ void qbfly_fwd_conv(uint32_t& xl, uint32_t& xh, uint3
   yh ^= xh;
 }
 
+// NP_PRIO_PROGRESS (experiment): a wave lowers its issue priority as it works
+// through a transform pass (3 in the first quarter of the pass's groups, 0 in
+// the last), so the waves of a SIMD that are behind issue first and the four
+// reach the pass's closing barrier together, instead of in age order.
+#ifndef NP_PRIO_PROGRESS
+#define NP_PRIO_PROGRESS 0
+#endif
+template <int F, int NG>
+__device__ __forceinline__ void progress_prio() {
+  if constexpr (NP_PRIO_PROGRESS != 0) {
+    constexpr int q = F * 4 / NG, qp = F == 0 ? -1 : (F - 1) * 4 / NG;
+    if constexpr (q != qp) __builtin_amdgcn_s_setprio(3 - q);
+  }
+}
+
 // GEN: coordinates and subfield levels (kSubLevel).
 // POST(t), when given, runs after group t of the forward transform's level 0
 // (rows 2t and 2t + 1 are final there).
@@ -1002,6 +1017,7 @@ __device__ __forceinline__ void cq_levels(const DevTables& T, const uint32_t* VP
   auto group = [&](auto fc, const Mult& p) __attribute__((always_inline)) {
     constexpr GroupRef r = cq_group<INVERSE>(decltype(fc)::value);
     constexpr int d = 1 << r.b;
+    progress_prio<decltype(fc)::value, 15>();
     const bool live = NP_CQ_LIVE_ALL || !INDEX0 || r.t != 0 || g != 0;  // c == 0: the skew sentinel, no product
     if constexpr (CONV && r.b == 0 && r.t == 0) ct = conv_tab(T);
     constexpr uint32_t span = ((1u << (2 * d)) - 1u) << (r.t * 2 * d);  // the group's rows
@@ -1063,6 +1079,7 @@ __device__ __forceinline__ void hi_levels(const DevTables& T, const uint32_t* VP
     constexpr GroupRef r = hi_group<K, INVERSE>(decltype(fc)::value + FIRST);
     constexpr int dj = 1 << (r.b - 2 - logR);
     constexpr bool live = !INDEX0 || r.t != 0;
+    progress_prio<decltype(fc)::value, hi_groups<K>() - FIRST>();
     if constexpr (!INVERSE && r.b == 4 && r.t == 0) hook.pre();
     auto body = [&](auto sub_c) __attribute__((always_inline)) {
       constexpr bool SUB = decltype(sub_c)::value;

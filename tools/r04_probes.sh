@@ -193,4 +193,17 @@ p17() {
   tail -22 gpurun_out/r04/enc_stamps_x4.txt
 }
 
+# Round-4 probe 18: progress-based issue priority in the transform passes
+# (NP_PRIO_PROGRESS=1 'prio'; with the 4-wave DMA 'priow4'), parity first,
+# against the product and 'w4' at config 3, then 'prio' at config 4
+p18() {
+  for v in prio priow4; do
+    NP_LIB_PATH=$PWD/tools/exp/lib_$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r04/pytest_gpu18_$v.log 2>&1; rc=$?
+    echo "$v: $(tail -1 gpurun_out/r04/pytest_gpu18_$v.log)"
+    [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu18_$v.log | head -20; exit $rc; }
+  done
+  TAG=p18_ bash tools/exp_one.sh base w4 prio priow4 base w4 prio priow4 || exit $?
+  ARGS="--config 4" TAG=p18c4_ bash tools/exp_one.sh base prio || exit $?
+}
+
 "$@"
