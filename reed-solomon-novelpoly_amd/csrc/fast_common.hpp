@@ -433,6 +433,16 @@ __device__ __forceinline__ uint32_t fresh_v(uint32_t v) {  // same for a per-lan
   return v;
 }
 
+// This thread's lane (0..63), recomputed here (v_mbcnt): a loop that takes
+// its lane per iteration from this keeps no thread-id VGPR live across the
+// iterations (which the allocator may spill at its 128-VGPR budget, and a
+// spill reload's vmcnt(0) waits for every load and store in flight).
+__device__ __forceinline__ uint32_t lane_fresh() {
+  uint32_t l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
 template <typename T>
 __device__ __forceinline__ T fresh(T v) {
   static_assert(sizeof(T) == 4 || sizeof(T) == 8, "scalar register value");
@@ -975,16 +985,15 @@ __device__ __forceinline__ void qbfly_fwd_conv(uint32_t& xl, uint32_t& xh, uint3
   yh ^= xh;
 }
 
-// NP_PRIO_PROGRESS (experiment): a wave lowers its issue priority as it works
-// through a transform pass (3 in the first quarter of the pass's groups, 0 in
-// the last), so the waves of a SIMD that are behind issue first and the four
-// reach the pass's closing barrier together, instead of in age order.
-#ifndef NP_PRIO_PROGRESS
-#define NP_PRIO_PROGRESS 0
-#endif
-template <int F, int NG>
+// Progress-based issue priority (PRIO != 0): a wave lowers its issue priority
+// as it works through a transform pass (3 in the first quarter of the pass's
+// groups, 0 in the last), so the waves of a SIMD that are behind issue first
+// and the four reach the pass's closing barrier together, instead of in age
+// order (a SIMD favours its older waves).  The callers choose per kernel
+// (kernels_fast.hip kEncPrio / kRecPrio*).
+template <int F, int NG, int PRIO>
 __device__ __forceinline__ void progress_prio() {
-  if constexpr (NP_PRIO_PROGRESS != 0) {
+  if constexpr (PRIO != 0) {
     constexpr int q = F * 4 / NG, qp = F == 0 ? -1 : (F - 1) * 4 / NG;
     if constexpr (q != qp) __builtin_amdgcn_s_setprio(3 - q);
   }
@@ -999,7 +1008,7 @@ struct NoPost {
 // CONV (forward, tower coordinates): the last level leaves the outputs in
 // Cantor coordinates (qbfly_fwd_conv; VP's level-0 slots staged from out_pools,
 // stage_vpools l0_out).
-template <int K, bool INVERSE, bool INDEX0, int GEN = -1, bool CONV = false, typename POST = NoPost>
+template <int K, bool INVERSE, bool INDEX0, int GEN = -1, bool CONV = false, int PRIO = 0, typename POST = NoPost>
 __device__ __forceinline__ void cq_levels(const DevTables& T, const uint32_t* VP, uint32_t index, uint32_t g,
                                           uint32_t (&L)[16], uint32_t (&H)[16], uint32_t rows = ~0u,
                                           POST post = POST{}) {
@@ -1017,7 +1026,7 @@ __device__ __forceinline__ void cq_levels(const DevTables& T, const uint32_t* VP
   auto group = [&](auto fc, const Mult& p) __attribute__((always_inline)) {
     constexpr GroupRef r = cq_group<INVERSE>(decltype(fc)::value);
     constexpr int d = 1 << r.b;
-    progress_prio<decltype(fc)::value, 15>();
+    progress_prio<decltype(fc)::value, 15, PRIO>();
     const bool live = NP_CQ_LIVE_ALL || !INDEX0 || r.t != 0 || g != 0;  // c == 0: the skew sentinel, no product
     if constexpr (CONV && r.b == 0 && r.t == 0) ct = conv_tab(T);
     constexpr uint32_t span = ((1u << (2 * d)) - 1u) << (r.t * 2 * d);  // the group's rows
@@ -1062,7 +1071,7 @@ struct NoHiHook {
   __device__ __forceinline__ void pre() const {}
   __device__ __forceinline__ void post(int) const {}
 };
-template <int K, bool INVERSE, bool INDEX0, int FIRST = 0, int GEN = -1, typename HOOK = NoHiHook>
+template <int K, bool INVERSE, bool INDEX0, int FIRST = 0, int GEN = -1, int PRIO = 0, typename HOOK = NoHiHook>
 __device__ __forceinline__ void hi_levels(const DevTables& T, const uint32_t* VP, uint32_t index, uint32_t (&L)[16],
                                           uint32_t (&H)[16], HOOK hook = HOOK{}) {
   if constexpr (kExp & 1) return;
@@ -1079,7 +1088,7 @@ __device__ __forceinline__ void hi_levels(const DevTables& T, const uint32_t* VP
     constexpr GroupRef r = hi_group<K, INVERSE>(decltype(fc)::value + FIRST);
     constexpr int dj = 1 << (r.b - 2 - logR);
     constexpr bool live = !INDEX0 || r.t != 0;
-    progress_prio<decltype(fc)::value, hi_groups<K>() - FIRST>();
+    progress_prio<decltype(fc)::value, hi_groups<K>() - FIRST, PRIO>();
     if constexpr (!INVERSE && r.b == 4 && r.t == 0) hook.pre();
     auto body = [&](auto sub_c) __attribute__((always_inline)) {
       constexpr bool SUB = decltype(sub_c)::value;

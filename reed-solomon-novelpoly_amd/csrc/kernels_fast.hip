@@ -57,6 +57,20 @@ __device__ __forceinline__ bool enc_tower(uint32_t index) {
 // K = 256).  SH = 0: a shift >= 4 (n > 4K) in Cantor coordinates.  A runtime
 // choice between instances inside a pass makes the register allocator spill,
 // so each call site is one instance.
+// NP_PRIO_ENC: the encode's transform passes with progress-based issue
+// priority (fast_common.hpp progress_prio).  Measured: config-3 encode
+// 1.601 / 1.602 -> 1.514 / 1.527 ms (-5 %, profiles/r04_ab.txt probe 18).
+// NP_PRIO_DEC (bits: 1 the segments' cq levels, 2 their high levels, 4 the
+// forward transform) for the fast decode: all three measured +1.5 to +2.8 %.
+#ifndef NP_PRIO_ENC
+#define NP_PRIO_ENC 1
+#endif
+#ifndef NP_PRIO_DEC
+#define NP_PRIO_DEC 0
+#endif
+constexpr int kEncPrio = NP_PRIO_ENC;
+constexpr int kRecPrioCq = NP_PRIO_DEC & 1, kRecPrioHi = (NP_PRIO_DEC >> 1) & 1, kRecPrioFwd = (NP_PRIO_DEC >> 2) & 1;
+
 template <int K, int SH>
 constexpr int kShiftGen = static_cast<int>(gen_of((SH == 23 ? 2 : SH) * K));
 
@@ -73,7 +87,7 @@ __device__ __forceinline__ void shift_hi(const DevTables& T, const uint32_t* vp,
   if constexpr (SH == 0) {
     tower_convert(T, XL, XH);  // M is in tower coordinates
     fwd_top<K, 0, -1>(T, vp, index, XL, XH, PL, PH);
-    hi_levels<K, false, false, 1, -1>(T, vp, index, XL, XH);
+    hi_levels<K, false, false, 1, -1, kEncPrio>(T, vp, index, XL, XH);
   } else {
     if constexpr (SH == 23) {
       if (index == 2 * K)
@@ -83,7 +97,7 @@ __device__ __forceinline__ void shift_hi(const DevTables& T, const uint32_t* vp,
     } else {
       fwd_top<K, SH, 0>(T, vp, index, XL, XH, PL, PH);
     }
-    hi_levels<K, false, false, 1, 0>(T, vp, index, XL, XH, hook);  // hi levels: gen_of(index) <= 4
+    hi_levels<K, false, false, 1, 0, kEncPrio>(T, vp, index, XL, XH, hook);  // hi levels: gen_of(index) <= 4
   }
 }
 
@@ -108,11 +122,11 @@ template <int K, int SH, typename POST = NoPost>
 __device__ __forceinline__ void shift_cq(const DevTables& T, const uint32_t* vp, uint32_t index, uint32_t g,
                                          uint32_t (&XL)[16], uint32_t (&XH)[16], POST post = POST{}) {
   if constexpr (SH == 0) {
-    cq_levels<K, false, false, -1>(T, vp, index, g, XL, XH, ~0u, post);
+    cq_levels<K, false, false, -1, false, kEncPrio>(T, vp, index, g, XL, XH, ~0u, post);
   } else {
     static_assert(SH != 23 || kShiftGen<K, 2> == kShiftGen<K, 3>, "shifts 2 and 3 share one instance");
     static_assert(SH != 23 || enc_conv(K, 2) == enc_conv(K, 3), "shifts 2 and 3 share one instance");
-    cq_levels<K, false, false, kShiftGen<K, SH>, kEncConv<K, SH>>(T, vp, index, g, XL, XH, ~0u, post);
+    cq_levels<K, false, false, kShiftGen<K, SH>, kEncConv<K, SH>, kEncPrio>(T, vp, index, g, XL, XH, ~0u, post);
     if constexpr (!kEncConv<K, SH>) tower_convert(T, XL, XH);  // back to Cantor coordinates for the shard rows
   }
 }
@@ -198,7 +212,7 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     cq_read<K>(tile, cqb, CL, CH);
     store_rows(out, a.shard_len, 16 * g, wanted_store, CL, CH, lane, ncols, full, nt);
     tower_convert(T, CL, CH);  // transforms run in tower coordinates
-    cq_levels<K, true, true, 0>(T, VP, 0, g, CL, CH);
+    cq_levels<K, true, true, 0, false, kEncPrio>(T, VP, 0, g, CL, CH);
     if constexpr (kEncQx<K>) {
       // the quad items overlay payload blocks that other waves read: wait for
       // every wave's cq_read (cq_write_p writes back only the blocks it read)
@@ -216,7 +230,7 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     hi_read_q<K>(tile, g, lane, ML, MH);
   else
     hi_read_p<K>(tile, hb, ML, MH);
-  hi_levels<K, true, true, 0, 0>(T, VP, 0, ML, MH);
+  hi_levels<K, true, true, 0, 0, kEncPrio>(T, VP, 0, ML, MH);
 #pragma unroll
   for (int q = 0; q < 16; ++q) asm volatile("" : "+v"(ML[q]), "+v"(MH[q]));  // materialise M once
 
@@ -548,7 +562,7 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
                rows_nt(a.shards, a.batch_stride, a.shard_len));
     stamp(dbg, 2);
     tower_convert(T, CL, CH);  // transforms run in tower coordinates
-    cq_levels<K, true, true, 0>(T, VP, 0, g, CL, CH);
+    cq_levels<K, true, true, 0, false, kEncPrio>(T, VP, 0, g, CL, CH);
     stamp(dbg, 3);
     if constexpr (kEncQx<K>) {
       // the quad items overlay payload blocks that other waves read: wait for
@@ -568,7 +582,7 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
   else
     hi_read_p<K>(tile, hb, ML, MH);
   stamp(dbg, 5);
-  hi_levels<K, true, true, 0, 0>(T, VP, 0, ML, MH);
+  hi_levels<K, true, true, 0, 0, kEncPrio>(T, VP, 0, ML, MH);
 #pragma unroll
   for (int q = 0; q < 16; ++q) asm volatile("" : "+v"(ML[q]), "+v"(MH[q]));  // materialise M once
   stamp(dbg, 6);
@@ -916,7 +930,7 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
     stamp(c.dbg, 3 + 6 * step);
     // absent rows are zero; segment q's transform has gen_of(qK) <= kRecMaxGen
     with_gen<0, kRecMaxGen<K, NQ>, false>(index, [&](auto gc) __attribute__((always_inline)) {
-      cq_levels<K, true, false, decltype(gc)::value>(T, vp, index, g, XL, XH, m);
+      cq_levels<K, true, false, decltype(gc)::value, false, kRecPrioCq>(T, vp, index, g, XL, XH, m);
     });
     stamp(c.dbg, 4 + 6 * step);
     if (step > 0 || after_tile) {
@@ -950,9 +964,9 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
     // groups, whose skew is the zero element (15 of the 32 quad multiplies)
     // (the 2-segment decode keeps its rows prefetch live here: no room for two instances)
     if (NP_REC_IDX0 && NQ == 4 && q == 0)
-      hi_levels<K, true, true, 0, 0>(T, vp, 0, XL, XH);
+      hi_levels<K, true, true, 0, 0, kRecPrioHi>(T, vp, 0, XL, XH);
     else
-      hi_levels<K, true, false, 0, 0>(T, vp, index, XL, XH);
+      hi_levels<K, true, false, 0, 0, kRecPrioHi>(T, vp, index, XL, XH);
     stamp(c.dbg, 6 + 6 * step);
     __builtin_amdgcn_sched_barrier(0);
     fold(step, q);
@@ -1004,7 +1018,7 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
     // ---- forward transform of size K at index 0
     const uint32_t* vp0 = VP + vp_slot<K, NQ>(0, NQ - 1) * G::kVPWords;  // segment 0's tables = FFT(K, 0)'s
     stamp(dbg, 26);
-    hi_levels<K, false, true, 0, 0>(T, vp0, 0, AL, AH);
+    hi_levels<K, false, true, 0, 0, kRecPrioFwd>(T, vp0, 0, AL, AH);
     stamp(dbg, 27);
     __syncthreads();
     hi_write<K>(tile, fresh_v(hb), AL, AH);
@@ -1013,7 +1027,7 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
     if constexpr (!kRowPrefetch<NQ> && NP_MERGE_EARLY == 1)  // the merge's rows load during the FFT's cq pass
       issue_rows(raw, sh, a.shard_len, uniform(msk[NQ - 1]), 16 * g, T.zeros, lane, ncols, full);
     cq_read<K>(tile, fresh_v(cqb), XL, XH);
-    cq_levels<K, false, true, 0>(T, vp0, 0, g, XL, XH, ~uniform(msk[NQ - 1]));  // erased rows only
+    cq_levels<K, false, true, 0, false, kRecPrioFwd>(T, vp0, 0, g, XL, XH, ~uniform(msk[NQ - 1]));  // erased rows only
     stamp(dbg, 29);
   }
   // ---- merge: received systematic rows, postmultiplied recovered ones
@@ -1145,7 +1159,11 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
     // row offsets, sizes and descriptors derived from them out of the tile loop
     // and keeps them live in (spilled) registers across it
     const uint32_t g = fresh(g0);
+#if NP_REC_TID_SPILL  // experiment: the round-4 form, whose tid0 stayed live across tiles (spilled)
     const uint32_t tid = fresh_v(tid0), lane = tid & 63u;
+#else
+    const uint32_t lane = lane_fresh(), tid = 64u * g + lane;
+#endif
     const uint32_t cqb = col_base<K>(4 * lane) ^ (32u * g);
     const size_t shard_len = fresh(a.shard_len);
     uint32_t msk[NQ];
@@ -1180,7 +1198,7 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
       stamp(dbg, 26);
       if constexpr (!kRowPrefetch<NQ> && NP_MERGE_EARLY == 2)  // the merge's rows load during the FFT
         issue_rows(raw, sh, shard_len, uniform(msk[NQ - 1]), 16 * g, T.zeros, lane, ncols, full);
-      hi_levels<K, false, true, 0, 0>(T, vp0, 0, AL, AH);
+      hi_levels<K, false, true, 0, 0, kRecPrioFwd>(T, vp0, 0, AL, AH);
       stamp(dbg, 27);
       __syncthreads();
       hi_write<K>(tile, fresh_v(hb), AL, AH);
@@ -1189,7 +1207,7 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
       if constexpr (!kRowPrefetch<NQ> && NP_MERGE_EARLY == 1)  // the merge's rows load during the FFT's cq pass
         issue_rows(raw, sh, shard_len, uniform(msk[NQ - 1]), 16 * g, T.zeros, lane, ncols, full);
       cq_read<K>(tile, fresh_v(cqb), XL, XH);
-      cq_levels<K, false, true, 0>(T, vp0, 0, g, XL, XH, ~uniform(msk[NQ - 1]));  // erased rows only
+      cq_levels<K, false, true, 0, false, kRecPrioFwd>(T, vp0, 0, g, XL, XH, ~uniform(msk[NQ - 1]));  // erased rows only
       stamp(dbg, 29);
     }
     // ---- merge: received systematic rows, postmultiplied recovered ones

@@ -206,4 +206,23 @@ p18() {
   ARGS="--config 4" TAG=p18c4_ bash tools/exp_one.sh base prio || exit $?
 }
 
+# Round-4 probe 19: the product with progress priority in the encode and the
+# decode's per-tile lane id (parity suite); A/B at config 3 against the encode
+# without priority ('prio0'), the decode's spilled thread id ('tidspill'),
+# priority in the decode's segment cq ('pd1') or high ('pd2') levels, and the
+# 4-wave DMA ('w4'); config 4 and 1200 validators against 'prio0'
+p19() {
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fuzz.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r04/pytest_gpu19.log 2>&1; rc=$?
+  echo "product: $(tail -1 gpurun_out/r04/pytest_gpu19.log)"
+  [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu19.log | head -20; exit $rc; }
+  for v in pd1 pd2 w4; do
+    NP_LIB_PATH=$PWD/tools/exp/lib_$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r04/pytest_gpu19_$v.log 2>&1; rc=$?
+    echo "$v: $(tail -1 gpurun_out/r04/pytest_gpu19_$v.log)"
+    [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu19_$v.log | head -20; exit $rc; }
+  done
+  TAG=p19_ bash tools/exp_one.sh base prio0 tidspill pd1 pd2 w4 base prio0 tidspill pd1 pd2 w4 || exit $?
+  ARGS="--config 4" TAG=p19c4_ bash tools/exp_one.sh base prio0 base prio0 || exit $?
+  TAG=p19v300_ ARGS="--n-wanted 300 --batch 1024 --erase 100" bash tools/exp_one.sh base prio0 || exit $?
+}
+
 "$@"
