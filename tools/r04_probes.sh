@@ -225,4 +225,23 @@ p19() {
   TAG=p19v300_ ARGS="--n-wanted 300 --batch 1024 --erase 100" bash tools/exp_one.sh base prio0 || exit $?
 }
 
+# Round-4 probe 20: probe 19 with the product's parity suite run with
+# serialized kernels first (probe 19's run faulted in
+# test_host_pipeline_all_systematic[12289-4097-73728-3-pageable], a huge-path
+# case whose kernels did not change: a fault now names its kernel), then
+# probe 19's A/B
+p20() {
+  AMD_SERIALIZE_KERNEL=3 timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fuzz.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r04/pytest_gpu20.log 2>&1; rc=$?
+  echo "product (serialized): $(tail -1 gpurun_out/r04/pytest_gpu20.log)"
+  [ $rc -eq 0 ] || { grep -E "FAILED|Error|error|assert" gpurun_out/r04/pytest_gpu20.log | head -30; exit $rc; }
+  for v in pd1 pd2 w4; do
+    NP_LIB_PATH=$PWD/tools/exp/lib_$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "not pipeline" > gpurun_out/r04/pytest_gpu20_$v.log 2>&1; rc=$?
+    echo "$v: $(tail -1 gpurun_out/r04/pytest_gpu20_$v.log)"
+    [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu20_$v.log | head -20; exit $rc; }
+  done
+  TAG=p20_ bash tools/exp_one.sh base prio0 tidspill pd1 pd2 w4 base prio0 tidspill pd1 pd2 w4 || exit $?
+  ARGS="--config 4" TAG=p20c4_ bash tools/exp_one.sh base prio0 base prio0 || exit $?
+  TAG=p20v300_ ARGS="--n-wanted 300 --batch 1024 --erase 100" bash tools/exp_one.sh base prio0 || exit $?
+}
+
 "$@"
