@@ -69,7 +69,12 @@ __device__ __forceinline__ bool enc_tower(uint32_t index) {
 #define NP_PRIO_DEC 0
 #endif
 constexpr int kEncPrio = NP_PRIO_ENC;
-constexpr int kRecPrioCq = NP_PRIO_DEC & 1, kRecPrioHi = (NP_PRIO_DEC >> 1) & 1, kRecPrioFwd = (NP_PRIO_DEC >> 2) & 1;
+// Bit 3 (experiment): one schedule over each barrier-free span of the segment
+// sweep (high levels of step s, fold, premultiply and cq levels of step s+1):
+// priority 3 in the high levels, 2 in the premultiply, 1 then 0 in the cq levels.
+constexpr bool kRecPrioSpan = (NP_PRIO_DEC & 8) != 0;
+constexpr int kRecPrioCq = kRecPrioSpan ? 3 : NP_PRIO_DEC & 1, kRecPrioHi = kRecPrioSpan ? 2 : (NP_PRIO_DEC >> 1) & 1,
+              kRecPrioFwd = (NP_PRIO_DEC >> 2) & 1;
 
 template <int K, int SH>
 constexpr int kShiftGen = static_cast<int>(gen_of((SH == 23 ? 2 : SH) * K));
@@ -906,6 +911,7 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
       issue_rows(raw, (kExp & 32) ? T.zeros : sh, (kExp & 32) ? 0 : shard_len, m, index + 16 * g, T.zeros, c.lane,
                  c.ncols, c.full, q == 0);
     stamp(c.dbg, 2 + 6 * step);
+    if constexpr (kRecPrioSpan) __builtin_amdgcn_s_setprio(2);
     pipelined_rec<16>(
         [&](auto pc) __attribute__((always_inline)) {
           return (cpool_t)(R) + (index + 16 * g + decltype(pc)::value) * kPoolWords;

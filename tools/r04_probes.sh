@@ -244,4 +244,14 @@ p20() {
   TAG=p20v300_ ARGS="--n-wanted 300 --batch 1024 --erase 100" bash tools/exp_one.sh base prio0 || exit $?
 }
 
+# Round-4 probe 21: one priority schedule per barrier-free span of the
+# decode's segment sweep (NP_PRIO_DEC=8 'span'), parity first, against the
+# product and 'pd1' at config 3
+p21() {
+  NP_LIB_PATH=$PWD/tools/exp/lib_span.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "not pipeline" > gpurun_out/r04/pytest_gpu21_span.log 2>&1; rc=$?
+  echo "span: $(tail -1 gpurun_out/r04/pytest_gpu21_span.log)"
+  [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu21_span.log | head -20; exit $rc; }
+  TAG=p21_ bash tools/exp_one.sh base span pd1 base span pd1 base span pd1 || exit $?
+}
+
 "$@"
