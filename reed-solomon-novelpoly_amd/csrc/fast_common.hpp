@@ -991,14 +991,15 @@ __device__ __forceinline__ void qbfly_fwd_conv(uint32_t& xl, uint32_t& xh, uint3
 // and the four reach the pass's closing barrier together, instead of in age
 // order (a SIMD favours its older waves).  The callers choose per kernel
 // (kernels_fast.hip kEncPrio / kRecPrio*).
-// PRIO 1: 3, 2, 1, 0 over the pass's quarters; 2: 3 throughout; 3: 1, 1, 0, 0
-// (passes inside a longer barrier-free span, kernels_fast.hip kRecPrioSpan).
+// PRIO 1: 3, 2, 1, 0 over the pass's quarters; 2: 3 throughout; 3: 1, 1, 0, 0;
+// 4: 3, 3, 2, 2 (passes inside a longer barrier-free span, kernels_fast.hip
+// kRecPrioSpan / kEncPrio).
 template <int F, int NG, int PRIO>
 __device__ __forceinline__ void progress_prio() {
   if constexpr (PRIO != 0) {
     constexpr int q = F * 4 / NG, qp = F == 0 ? -1 : (F - 1) * 4 / NG;
-    constexpr int pr = PRIO == 1 ? 3 - q : PRIO == 2 ? 3 : (q < 2 ? 1 : 0);
-    constexpr int pp = qp < 0 ? -1 : PRIO == 1 ? 3 - qp : PRIO == 2 ? 3 : (qp < 2 ? 1 : 0);
+    constexpr int pr = PRIO == 1 ? 3 - q : PRIO == 2 ? 3 : PRIO == 3 ? (q < 2 ? 1 : 0) : (q < 2 ? 3 : 2);
+    constexpr int pp = qp < 0 ? -1 : PRIO == 1 ? 3 - qp : PRIO == 2 ? 3 : PRIO == 3 ? (qp < 2 ? 1 : 0) : (qp < 2 ? 3 : 2);
     if constexpr (pr != pp) __builtin_amdgcn_s_setprio(pr);
   }
 }

@@ -66,15 +66,24 @@ __device__ __forceinline__ bool enc_tower(uint32_t index) {
 #define NP_PRIO_ENC 1
 #endif
 #ifndef NP_PRIO_DEC
-#define NP_PRIO_DEC 0
+#define NP_PRIO_DEC 8
 #endif
-constexpr int kEncPrio = NP_PRIO_ENC;
-// Bit 3 (experiment): one schedule over each barrier-free span of the segment
-// sweep (high levels of step s, fold, premultiply and cq levels of step s+1):
-// priority 3 in the high levels, 2 in the premultiply, 1 then 0 in the cq levels.
-constexpr bool kRecPrioSpan = (NP_PRIO_DEC & 8) != 0;
-constexpr int kRecPrioCq = kRecPrioSpan ? 3 : NP_PRIO_DEC & 1, kRecPrioHi = kRecPrioSpan ? 2 : (NP_PRIO_DEC >> 1) & 1,
-              kRecPrioFwd = (NP_PRIO_DEC >> 2) & 1;
+// NP_PRIO_ENC=2 (experiment): the encode's span schedule, the cq pass of shift
+// s (3, 3, 2, 2) and the high levels of shift s + 1 (1, 1, 0, 0) that follow
+// it without a barrier.
+constexpr int kEncPrio = NP_PRIO_ENC == 2 ? 3 : NP_PRIO_ENC;
+constexpr int kEncPrioCq = NP_PRIO_ENC == 2 ? 4 : NP_PRIO_ENC;
+// Bit 3 (the default): one schedule over each barrier-free span of the
+// segment sweep (high levels of step s, fold, premultiply and cq levels of
+// step s + 1): priority 3 in the high levels, 2 in the premultiply, 1 then 0 in
+// the cq levels.  Measured: config-3 reconstruct 2.741 / 2.759 / 2.758 ->
+// 2.655 / 2.669 / 2.672 ms (-3.2 %, profiles/r04_ab.txt probe 21).
+// Bit 4 (experiment): the same over the forward transform's spans (its high
+// levels after the last step's: 1, 1, 0, 0; its cq levels and the merge: 3).
+constexpr bool kRecPrioSpan = (NP_PRIO_DEC & 8) != 0, kRecPrioSpanFwd = (NP_PRIO_DEC & 16) != 0;
+constexpr int kRecPrioCq = kRecPrioSpan ? 3 : NP_PRIO_DEC & 1, kRecPrioHi = kRecPrioSpan ? 2 : (NP_PRIO_DEC >> 1) & 1;
+constexpr int kRecPrioFwdHi = kRecPrioSpanFwd ? 3 : (NP_PRIO_DEC >> 2) & 1,
+              kRecPrioFwdCq = kRecPrioSpanFwd ? 2 : (NP_PRIO_DEC >> 2) & 1;
 
 template <int K, int SH>
 constexpr int kShiftGen = static_cast<int>(gen_of((SH == 23 ? 2 : SH) * K));
@@ -127,11 +136,11 @@ template <int K, int SH, typename POST = NoPost>
 __device__ __forceinline__ void shift_cq(const DevTables& T, const uint32_t* vp, uint32_t index, uint32_t g,
                                          uint32_t (&XL)[16], uint32_t (&XH)[16], POST post = POST{}) {
   if constexpr (SH == 0) {
-    cq_levels<K, false, false, -1, false, kEncPrio>(T, vp, index, g, XL, XH, ~0u, post);
+    cq_levels<K, false, false, -1, false, kEncPrioCq>(T, vp, index, g, XL, XH, ~0u, post);
   } else {
     static_assert(SH != 23 || kShiftGen<K, 2> == kShiftGen<K, 3>, "shifts 2 and 3 share one instance");
     static_assert(SH != 23 || enc_conv(K, 2) == enc_conv(K, 3), "shifts 2 and 3 share one instance");
-    cq_levels<K, false, false, kShiftGen<K, SH>, kEncConv<K, SH>, kEncPrio>(T, vp, index, g, XL, XH, ~0u, post);
+    cq_levels<K, false, false, kShiftGen<K, SH>, kEncConv<K, SH>, kEncPrioCq>(T, vp, index, g, XL, XH, ~0u, post);
     if constexpr (!kEncConv<K, SH>) tower_convert(T, XL, XH);  // back to Cantor coordinates for the shard rows
   }
 }
@@ -217,7 +226,7 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     cq_read<K>(tile, cqb, CL, CH);
     store_rows(out, a.shard_len, 16 * g, wanted_store, CL, CH, lane, ncols, full, nt);
     tower_convert(T, CL, CH);  // transforms run in tower coordinates
-    cq_levels<K, true, true, 0, false, kEncPrio>(T, VP, 0, g, CL, CH);
+    cq_levels<K, true, true, 0, false, kEncPrioCq>(T, VP, 0, g, CL, CH);
     if constexpr (kEncQx<K>) {
       // the quad items overlay payload blocks that other waves read: wait for
       // every wave's cq_read (cq_write_p writes back only the blocks it read)
@@ -567,7 +576,7 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
                rows_nt(a.shards, a.batch_stride, a.shard_len));
     stamp(dbg, 2);
     tower_convert(T, CL, CH);  // transforms run in tower coordinates
-    cq_levels<K, true, true, 0, false, kEncPrio>(T, VP, 0, g, CL, CH);
+    cq_levels<K, true, true, 0, false, kEncPrioCq>(T, VP, 0, g, CL, CH);
     stamp(dbg, 3);
     if constexpr (kEncQx<K>) {
       // the quad items overlay payload blocks that other waves read: wait for
@@ -1024,7 +1033,7 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
     // ---- forward transform of size K at index 0
     const uint32_t* vp0 = VP + vp_slot<K, NQ>(0, NQ - 1) * G::kVPWords;  // segment 0's tables = FFT(K, 0)'s
     stamp(dbg, 26);
-    hi_levels<K, false, true, 0, 0, kRecPrioFwd>(T, vp0, 0, AL, AH);
+    hi_levels<K, false, true, 0, 0, kRecPrioFwdHi>(T, vp0, 0, AL, AH);
     stamp(dbg, 27);
     __syncthreads();
     hi_write<K>(tile, fresh_v(hb), AL, AH);
@@ -1033,7 +1042,7 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
     if constexpr (!kRowPrefetch<NQ> && NP_MERGE_EARLY == 1)  // the merge's rows load during the FFT's cq pass
       issue_rows(raw, sh, a.shard_len, uniform(msk[NQ - 1]), 16 * g, T.zeros, lane, ncols, full);
     cq_read<K>(tile, fresh_v(cqb), XL, XH);
-    cq_levels<K, false, true, 0, false, kRecPrioFwd>(T, vp0, 0, g, XL, XH, ~uniform(msk[NQ - 1]));  // erased rows only
+    cq_levels<K, false, true, 0, false, kRecPrioFwdCq>(T, vp0, 0, g, XL, XH, ~uniform(msk[NQ - 1]));  // erased rows only
     stamp(dbg, 29);
   }
   // ---- merge: received systematic rows, postmultiplied recovered ones
@@ -1204,7 +1213,7 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
       stamp(dbg, 26);
       if constexpr (!kRowPrefetch<NQ> && NP_MERGE_EARLY == 2)  // the merge's rows load during the FFT
         issue_rows(raw, sh, shard_len, uniform(msk[NQ - 1]), 16 * g, T.zeros, lane, ncols, full);
-      hi_levels<K, false, true, 0, 0, kRecPrioFwd>(T, vp0, 0, AL, AH);
+      hi_levels<K, false, true, 0, 0, kRecPrioFwdHi>(T, vp0, 0, AL, AH);
       stamp(dbg, 27);
       __syncthreads();
       hi_write<K>(tile, fresh_v(hb), AL, AH);
@@ -1213,7 +1222,7 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
       if constexpr (!kRowPrefetch<NQ> && NP_MERGE_EARLY == 1)  // the merge's rows load during the FFT's cq pass
         issue_rows(raw, sh, shard_len, uniform(msk[NQ - 1]), 16 * g, T.zeros, lane, ncols, full);
       cq_read<K>(tile, fresh_v(cqb), XL, XH);
-      cq_levels<K, false, true, 0, false, kRecPrioFwd>(T, vp0, 0, g, XL, XH, ~uniform(msk[NQ - 1]));  // erased rows only
+      cq_levels<K, false, true, 0, false, kRecPrioFwdCq>(T, vp0, 0, g, XL, XH, ~uniform(msk[NQ - 1]));  // erased rows only
       stamp(dbg, 29);
     }
     // ---- merge: received systematic rows, postmultiplied recovered ones

@@ -254,4 +254,22 @@ p21() {
   TAG=p21_ bash tools/exp_one.sh base span pd1 base span pd1 base span pd1 || exit $?
 }
 
+# Round-4 probe 22: the product with the decode's span priority (parity
+# suite); A/B at config 3 against the span schedule over the forward
+# transform as well ('sf'), the encode's span schedule ('espan') and no decode
+# priority ('dec0'); config 2 and 300 validators against 'dec0'
+p22() {
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fuzz.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r04/pytest_gpu22.log 2>&1; rc=$?
+  echo "product: $(tail -1 gpurun_out/r04/pytest_gpu22.log)"
+  [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu22.log | head -20; exit $rc; }
+  for v in sf espan; do
+    NP_LIB_PATH=$PWD/tools/exp/lib_$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "not pipeline" > gpurun_out/r04/pytest_gpu22_$v.log 2>&1; rc=$?
+    echo "$v: $(tail -1 gpurun_out/r04/pytest_gpu22_$v.log)"
+    [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu22_$v.log | head -20; exit $rc; }
+  done
+  TAG=p22_ bash tools/exp_one.sh base sf espan dec0 base sf espan dec0 || exit $?
+  ARGS="--config 2" TAG=p22c2_ bash tools/exp_one.sh base dec0 base dec0 || exit $?
+  TAG=p22v300_ ARGS="--n-wanted 300 --batch 1024 --erase 100" bash tools/exp_one.sh base dec0 || exit $?
+}
+
 "$@"
