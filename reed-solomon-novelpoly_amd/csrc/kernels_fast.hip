@@ -66,7 +66,7 @@ __device__ __forceinline__ bool enc_tower(uint32_t index) {
 #define NP_PRIO_ENC 1
 #endif
 #ifndef NP_PRIO_DEC
-#define NP_PRIO_DEC 8
+#define NP_PRIO_DEC 24
 #endif
 // NP_PRIO_ENC=2 (experiment): the encode's span schedule, the cq pass of shift
 // s (3, 3, 2, 2) and the high levels of shift s + 1 (1, 1, 0, 0) that follow
@@ -78,8 +78,10 @@ constexpr int kEncPrioCq = NP_PRIO_ENC == 2 ? 4 : NP_PRIO_ENC;
 // step s + 1): priority 3 in the high levels, 2 in the premultiply, 1 then 0 in
 // the cq levels.  Measured: config-3 reconstruct 2.741 / 2.759 / 2.758 ->
 // 2.655 / 2.669 / 2.672 ms (-3.2 %, profiles/r04_ab.txt probe 21).
-// Bit 4 (experiment): the same over the forward transform's spans (its high
+// Bit 4 (the default): the same over the forward transform's spans (its high
 // levels after the last step's: 1, 1, 0, 0; its cq levels and the merge: 3).
+// Measured: 2.684 / 2.696 -> 2.648 / 2.642 ms (-1.7 %, probe 22).  The
+// encode's span schedule (NP_PRIO_ENC=2) measured neutral.
 constexpr bool kRecPrioSpan = (NP_PRIO_DEC & 8) != 0, kRecPrioSpanFwd = (NP_PRIO_DEC & 16) != 0;
 constexpr int kRecPrioCq = kRecPrioSpan ? 3 : NP_PRIO_DEC & 1, kRecPrioHi = kRecPrioSpan ? 2 : (NP_PRIO_DEC >> 1) & 1;
 constexpr int kRecPrioFwdHi = kRecPrioSpanFwd ? 3 : (NP_PRIO_DEC >> 2) & 1,
