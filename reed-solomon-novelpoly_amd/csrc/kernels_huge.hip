@@ -45,6 +45,13 @@
 namespace np {
 namespace {
 
+// NP_PRIO_HUGE (experiment; bit 0 the encode, bit 1 the decode): progress-based
+// issue priority in the sub-transforms' passes (fast_common.hpp progress_prio).
+#ifndef NP_PRIO_HUGE
+#define NP_PRIO_HUGE 0
+#endif
+constexpr int kHugePrioEnc = NP_PRIO_HUGE & 1, kHugePrioDec = (NP_PRIO_HUGE >> 1) & 1;
+
 constexpr int kSK = 1024;                             // sub-transform size
 constexpr uint32_t kSlotBytes = 16u * 1024u * 8u;     // one sub-segment of a tile in thread order
 constexpr uint32_t kHDS = RGeo<kSK>::kHD;
@@ -161,17 +168,17 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
   rres_store_rows(a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(ch0), a.shard_len, I,
                   a.wanted_n, L, H, r, ncols, full, nt);
   tower_convert(T, L, H);
-  rcq_levels<true, GEN, true>(T, I, r, L, H, DL);
+  rcq_levels<true, GEN, true, kHugePrioEnc>(T, I, r, L, H, DL);
   __syncthreads();  // every wave has read its payload blocks
   qi_cq<true>(tile, qc, L, H);
   __syncthreads();
   qi_ha<false>(tile, qc, L, H);
-  ha_levels_st<kSK, true, GEN>(T, I, r, L, H, VS);
+  ha_levels_st<kSK, true, GEN, kHugePrioEnc>(T, I, r, L, H, VS);
   __syncthreads();
   qi_ha<true>(tile, qc, L, H);
   __syncthreads();
   qi_hd<kSK, false>(tile, qc, L, H);
-  hd_levels_st<kSK, true>(T, I, L, H, VS);
+  hd_levels_st<kSK, true, kHugePrioEnc>(T, I, L, H, VS);
   slot_store(slot_at(h, pb, tl, sr.u), r.tid, L, H);  // HD' registers in thread order
 }
 
@@ -220,16 +227,16 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
   uint32_t L[16], H[16];
   slot_load(slot_at(h, pb, tl, sr.u), r.tid, L, H);
   __syncthreads();  // the staged tables
-  hd_levels_st<kSK, false>(T, I, L, H, VS);
+  hd_levels_st<kSK, false, kHugePrioEnc>(T, I, L, H, VS);
   qi_hd<kSK, true>(tile, qc, L, H);
   __syncthreads();
   qi_ha<false>(tile, qc, L, H);
-  ha_levels_st<kSK, false, GEN>(T, I, r, L, H, VS);
+  ha_levels_st<kSK, false, GEN, kHugePrioEnc>(T, I, r, L, H, VS);
   __syncthreads();
   qi_ha<true>(tile, qc, L, H);
   __syncthreads();
   qi_cq<false>(tile, qc, L, H);
-  rcq_levels<false, GEN, true>(T, I, r, L, H, DL);
+  rcq_levels<false, GEN, true, kHugePrioEnc>(T, I, r, L, H, DL);
   tower_convert(T, L, H);  // back to Cantor coordinates for the shard rows
   rres_store_rows(a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(ch0), a.shard_len, I,
                   a.wanted_n, L, H, r, ncols, full, nt);
@@ -310,17 +317,17 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
       }
     }
   }
-  rcq_levels<true, GEN, true>(T, I, r, XL, XH, DL);
+  rcq_levels<true, GEN, true, kHugePrioDec>(T, I, r, XL, XH, DL);
   __syncthreads();  // every wave has read its row tables
   rcq_write<kSK>(tile, fresh_v(r.cqb), XL, XH);
   __syncthreads();
   rh_read<kHA>(tile, fresh_v(r.hab), XL, XH);
-  ha_levels_st<kSK, true, GEN>(T, I, r, XL, XH, VS);
+  ha_levels_st<kSK, true, GEN, kHugePrioDec>(T, I, r, XL, XH, VS);
   __syncthreads();
   rh_write<kHA>(tile, fresh_v(r.hab), XL, XH);
   __syncthreads();
   rh_read<kHDS>(tile, fresh_v(r.hdb), XL, XH);
-  hd_levels_st<kSK, true>(T, I, XL, XH, VS);
+  hd_levels_st<kSK, true, kHugePrioDec>(T, I, XL, XH, VS);
   slot_store(slot_at(h, pb, tl, sr.u), r.tid, XL, XH);
   if (sr.u < h.M) {  // z = D_1024 of segment 0's sub-transform (the lifted low part of D_k)
     uint32_t AL[16], AH[16];
@@ -413,16 +420,16 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
     stage_rh_tables<kSK>(T, VS, 1, I);
     slot_load(slot_at(h, pb, tl, sr.u), r.tid, AL, AH);
     __syncthreads();  // the staged tables
-    hd_levels_st<kSK, false>(T, I, AL, AH, VS);
+    hd_levels_st<kSK, false, kHugePrioDec>(T, I, AL, AH, VS);
     rh_write<kHDS>(tile, fresh_v(r.hdb), AL, AH);
     __syncthreads();
     rh_read<kHA>(tile, fresh_v(r.hab), AL, AH);
-    ha_levels_st<kSK, false, GEN>(T, I, r, AL, AH, VS);
+    ha_levels_st<kSK, false, GEN, kHugePrioDec>(T, I, r, AL, AH, VS);
     __syncthreads();
     rh_write<kHA>(tile, fresh_v(r.hab), AL, AH);
     __syncthreads();
     rcq_read<kSK>(tile, fresh_v(r.cqb), AL, AH);
-    rcq_levels<false, GEN, true>(T, I, r, AL, AH, DL);
+    rcq_levels<false, GEN, true, kHugePrioDec>(T, I, r, AL, AH, DL);
   } else {
 #pragma unroll
     for (int j = 0; j < 16; ++j) AL[j] = AH[j] = 0;

@@ -6,6 +6,14 @@
 namespace np {
 namespace {
 
+// NP_PRIO_RES (experiment; bit 0 the encode, bit 1 the decode): progress-based
+// issue priority in every transform pass of the resident kernels
+// (fast_common.hpp progress_prio).
+#ifndef NP_PRIO_RES
+#define NP_PRIO_RES 0
+#endif
+constexpr int kResPrioEnc = NP_PRIO_RES & 1, kResPrioDec = (NP_PRIO_RES >> 1) & 1;
+
 // ---------------------------------------------------------------- encode ----
 // One workgroup: 64 chunks of one payload.  mod.rs:144-154 /
 // inc_encode.rs:15-48: IFFT(K, 0) of each chunk -> coefficients M (HD
@@ -42,7 +50,7 @@ __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4))) void k_e
     rcq_read_nat<K>(tile, r.cqb, L, H);
     rres_store_rows(out, a.shard_len, 0, wanted_store, L, H, r, ncols, full, nt);
     tower_convert(T, L, H);  // the transforms run in tower coordinates
-    rcq_levels<true, res_gen<K>(0), true>(T, 0, r, L, H, DL);
+    rcq_levels<true, res_gen<K>(0), true, kResPrioEnc>(T, 0, r, L, H, DL);
     __syncthreads();  // every wave has read its payload blocks
     qi_cq<true>(tile, qc, L, H);
   }
@@ -51,13 +59,13 @@ __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4))) void k_e
   {
     uint32_t L[16], H[16];
     qi_ha<false>(tile, qc, L, H);
-    ha_levels_st<K, true>(T, 0, r, L, H, VS);
+    ha_levels_st<K, true, 0, kResPrioEnc>(T, 0, r, L, H, VS);
     __syncthreads();
     qi_ha<true>(tile, qc, L, H);
     __syncthreads();
     qi_hd<K, false>(tile, qc, ML, MH);
   }
-  hd_levels_st<K, true>(T, 0, ML, MH, VS);
+  hd_levels_st<K, true, kResPrioEnc>(T, 0, ML, MH, VS);
 #pragma unroll
   for (int q = 0; q < 16; ++q) asm volatile("" : "+v"(ML[q]), "+v"(MH[q]));  // materialise M once
 
@@ -71,17 +79,17 @@ __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4))) void k_e
       H[q] = MH[q];
     }
     const uint32_t* vs = VS + sh * RStage<K>::kWords;
-    hd_levels_st<K, false>(T, I, L, H, vs);
+    hd_levels_st<K, false, kResPrioEnc>(T, I, L, H, vs);
     __syncthreads();  // the previous CQ pass is done with the tile
     qi_hd<K, true>(tile, qc, L, H);
     __syncthreads();
     qi_ha<false>(tile, qc, L, H);
-    ha_levels_st<K, false, GEN>(T, I, r, L, H, vs);
+    ha_levels_st<K, false, GEN, kResPrioEnc>(T, I, r, L, H, vs);
     __syncthreads();
     qi_ha<true>(tile, qc, L, H);
     __syncthreads();
     qi_cq<false>(tile, qc, L, H);
-    rcq_levels<false, GEN, true>(T, I, r, L, H, DL);
+    rcq_levels<false, GEN, true, kResPrioEnc>(T, I, r, L, H, DL);
     tower_convert(T, L, H);  // back to Cantor coordinates for the shard rows
     rres_store_rows(out, a.shard_len, I, wanted_store, L, H, r, ncols, full, nt);
   };
@@ -174,7 +182,7 @@ __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructAr
     return false;
   }
   const uint32_t* DL = reinterpret_cast<const uint32_t*>(tile + RGeo<K>::kTileBytes);
-  rcq_levels<true, res_gen<K>(I), kRecDeltaST<K, NQ>>(T, I, rr, XL, XH, DL);
+  rcq_levels<true, res_gen<K>(I), kRecDeltaST<K, NQ>, kResPrioDec>(T, I, rr, XL, XH, DL);
   if constexpr ((kExp & 32768) != 0 && STEP == 0) {  // experiment: the first step after its CQ levels
     res_copy_out<K>(out_tile, XL, XH, rr, ncols, out16);
     return false;
@@ -186,7 +194,7 @@ __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructAr
   rh_read<kHA>(tile, fresh_v(rr.hab), XL, XH);
   rstamp(dbg, s0 + 3);
   const uint32_t* vs = DL + kDeltaWords + q * RStage<K>::kWords;
-  ha_levels_st<K, true, res_gen<K>(I)>(T, I, rr, XL, XH, vs);
+  ha_levels_st<K, true, res_gen<K>(I), kResPrioDec>(T, I, rr, XL, XH, vs);
   rstamp(dbg, s0 + 4);
   __syncthreads();
   rh_write<kHA>(tile, fresh_v(rr.hab), XL, XH);
@@ -197,7 +205,7 @@ __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructAr
     dma_row_tables(tile, pools, static_cast<uint32_t>(res_seg<NQ>(STEP + 1)) * K, K, rr.w, rr.l, K / 64);
   }
   rstamp(dbg, s0 + 5);
-  hd_levels_st<K, true>(T, I, XL, XH, vs);
+  hd_levels_st<K, true, kResPrioDec>(T, I, XL, XH, vs);
   rstamp(dbg, s0 + 6);
   // fold x_q into d (kernels_fast.hip rec_segments)
   if constexpr (NQ == 8 && q != 0 && rec8_kappa_res(q) != 1u) {  // d ^= kappa_q x_q, kappa_q in GF(16)
@@ -281,14 +289,14 @@ __device__ __forceinline__ void res_decode_tile(const DevTables& T, const Recons
     return;
   }
   // ---- out = FFT(K, 0)(d), first k rows (inc_reconstruct.rs:80)
-  hd_levels_st<K, false>(T, 0, AL, AH, VS);
+  hd_levels_st<K, false, kResPrioDec>(T, 0, AL, AH, VS);
   rstamp(dbg, 40);
   __syncthreads();  // the last step's HD read is done
   rh_write<kHD>(tile, fresh_v(r.hdb), AL, AH);
   __syncthreads();
   rh_read<kHA>(tile, fresh_v(r.hab), AL, AH);
   rstamp(dbg, 41);
-  ha_levels_st<K, false>(T, 0, r, AL, AH, VS);
+  ha_levels_st<K, false, 0, kResPrioDec>(T, 0, r, AL, AH, VS);
   rstamp(dbg, 42);
   __syncthreads();
   rh_write<kHA>(tile, fresh_v(r.hab), AL, AH);
@@ -299,7 +307,7 @@ __device__ __forceinline__ void res_decode_tile(const DevTables& T, const Recons
     dma_row_tables(tile, pools, 0, K, r.w, r.l, K / 64);
   }
   rstamp(dbg, 43);
-  rcq_levels<false, res_gen<K>(0), kRecDeltaST<K, NQ>>(T, 0, r, AL, AH, DL);
+  rcq_levels<false, res_gen<K>(0), kRecDeltaST<K, NQ>, kResPrioDec>(T, 0, r, AL, AH, DL);
   rstamp(dbg, 44);
   // ---- merge: received systematic rows, postmultiplied recovered ones
   // (inc_reconstruct.rs:46-50, :82-84; tower in, Cantor out)

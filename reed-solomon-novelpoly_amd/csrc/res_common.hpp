@@ -432,21 +432,30 @@ __device__ __forceinline__ void rcq_level(const DevTables& T, uint32_t I, uint32
 
 // Experiment builds (NP_EXP, never the product): bit 8 skips the CQ levels,
 // bit 9 the HA levels, bit 10 the HD levels (tools/res_debug.py).
-template <bool INVERSE, int GEN, bool ST = false>
+// PRIO: progress-based issue priority over the pass's four levels
+// (fast_common.hpp progress_prio).
+template <bool INVERSE, int GEN, bool ST = false, int PRIO = 0>
 __device__ __forceinline__ void rcq_levels(const DevTables& T, uint32_t I, const Res& r, uint32_t (&L)[16],
                                            uint32_t (&H)[16], const uint32_t* DL = nullptr) {
   if constexpr (kExp & (1 | 256)) return;
   if constexpr (INVERSE ? (kExp & 4096) != 0 : (kExp & 2048) != 0) return;  // experiment: one direction only
   const uint32_t w = fresh(r.w), u = fresh_v(r.u);
+  // progress in butterfly groups (8 + 4 + 2 + 1)
   if constexpr (INVERSE) {
+    progress_prio<0, 15, PRIO>();
     rcq_level<true, GEN, 0, ST>(T, I, w, u, L, H, DL, std::make_integer_sequence<int, 8>{});
+    progress_prio<8, 15, PRIO>();
     rcq_level<true, GEN, 1, ST>(T, I, w, u, L, H, DL, std::make_integer_sequence<int, 4>{});
+    progress_prio<12, 15, PRIO>();
     rcq_level<true, GEN, 2, ST>(T, I, w, u, L, H, DL, std::make_integer_sequence<int, 2>{});
     rcq_level<true, GEN, 3, ST>(T, I, w, u, L, H, DL, std::make_integer_sequence<int, 1>{});
   } else {
+    progress_prio<0, 15, PRIO>();
     rcq_level<false, GEN, 3, ST>(T, I, w, u, L, H, DL, std::make_integer_sequence<int, 1>{});
     rcq_level<false, GEN, 2, ST>(T, I, w, u, L, H, DL, std::make_integer_sequence<int, 2>{});
+    progress_prio<3, 15, PRIO>();
     rcq_level<false, GEN, 1, ST>(T, I, w, u, L, H, DL, std::make_integer_sequence<int, 4>{});
+    progress_prio<7, 15, PRIO>();
     rcq_level<false, GEN, 0, ST>(T, I, w, u, L, H, DL, std::make_integer_sequence<int, 8>{});
   }
 }
@@ -538,7 +547,7 @@ __device__ __forceinline__ void stage_rh_tables(const DevTables& T, uint32_t* VS
 // come from the LDS block of the transform (RStage, stage_rh_tables) by
 // ds_read instead of as v_mov copies of the s_loaded pool: 4 v_mov_b64 per
 // group, i.e. up to a fifth of a level-4 butterfly.
-template <int PB0, int R0, int R1, bool INVERSE, int GEN = 0, bool ST = false>
+template <int PB0, int R0, int R1, bool INVERSE, int GEN = 0, bool ST = false, int PRIO = 0>
 __device__ __forceinline__ void rh_levels(const DevTables& T, uint32_t I, uint32_t hi, uint32_t (&L)[16],
                                           uint32_t (&H)[16], const uint32_t* vsb = nullptr) {
   if constexpr (kExp & 1) return;
@@ -551,6 +560,7 @@ __device__ __forceinline__ void rh_levels(const DevTables& T, uint32_t I, uint32
     constexpr GroupRef g = rh_group<R0, R1, INVERSE>(decltype(fc)::value);
     constexpr int d = 1 << g.b;
     constexpr bool SUB = PB0 + g.b >= GEN;
+    progress_prio<decltype(fc)::value, rh_groups<R0, R1>(), PRIO>();
 #pragma unroll
     for (int v = 0; v < d; ++v) {
       const int x = g.t * 2 * d + v, y = x + d;
@@ -595,19 +605,19 @@ __device__ __forceinline__ void hd_levels(const DevTables& T, uint32_t I, uint32
   rh_levels<pb0, 8 - pb0, 4, INVERSE>(T, I, 0u, L, H);
 }
 // The same with the staged VGPR halves: vs = the transform's RStage block.
-template <int K, bool INVERSE, int GEN = 0>
+template <int K, bool INVERSE, int GEN = 0, int PRIO = 0>
 __device__ __forceinline__ void ha_levels_st(const DevTables& T, uint32_t I, const Res& r, uint32_t (&L)[16],
                                              uint32_t (&H)[16], const uint32_t* vs) {
   if constexpr (kExp & 512) return;
   const uint32_t h = fresh(r.w >> 2);
-  rh_levels<4, 0, 4, INVERSE, GEN, true>(T, I, h, L, H, vs + 120u * h);
+  rh_levels<4, 0, 4, INVERSE, GEN, true, PRIO>(T, I, h, L, H, vs + 120u * h);
 }
-template <int K, bool INVERSE>
+template <int K, bool INVERSE, int PRIO = 0>
 __device__ __forceinline__ void hd_levels_st(const DevTables& T, uint32_t I, uint32_t (&L)[16], uint32_t (&H)[16],
                                              const uint32_t* vs) {
   if constexpr (kExp & 1024) return;
   constexpr int pb0 = RGeo<K>::kLogK - 4;
-  rh_levels<pb0, 8 - pb0, 4, INVERSE, 0, true>(T, I, 0u, L, H, vs + 120u * RStage<K>::kNH);
+  rh_levels<pb0, 8 - pb0, 4, INVERSE, 0, true, PRIO>(T, I, 0u, L, H, vs + 120u * RStage<K>::kNH);
 }
 
 // A ^= D_K(X) in the HD layout for one byte plane (inc_afft.rs:17-31,

@@ -272,4 +272,18 @@ p22() {
   TAG=p22v300_ ARGS="--n-wanted 300 --batch 1024 --erase 100" bash tools/exp_one.sh base dec0 || exit $?
 }
 
+# Round-4 probe 23: progress-based priority in the resident kernels' encode
+# ('res1') and decode ('res2') at config 4 and 2000 validators, and in the
+# huge kernels ('huge3') at 10000 validators; parity first
+p23() {
+  for v in res1 res2 huge3; do
+    NP_LIB_PATH=$PWD/tools/exp/lib_$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "not pipeline" > gpurun_out/r04/pytest_gpu23_$v.log 2>&1; rc=$?
+    echo "$v: $(tail -1 gpurun_out/r04/pytest_gpu23_$v.log)"
+    [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu23_$v.log | head -20; exit $rc; }
+  done
+  ARGS="--config 4" TAG=p23c4_ bash tools/exp_one.sh base res1 res2 base res1 res2 || exit $?
+  TAG=p23v2000_ ARGS="--n-wanted 2000 --batch 1024 --erase 667" bash tools/exp_one.sh base res1 res2 || exit $?
+  TAG=p23v10000_ ARGS="--n-wanted 10000 --batch 512 --erase 3334" bash tools/exp_one.sh base huge3 base huge3 || exit $?
+}
+
 "$@"
