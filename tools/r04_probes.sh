@@ -284,6 +284,7 @@ p23() {
   ARGS="--config 4" TAG=p23c4_ bash tools/exp_one.sh base res1 res2 base res1 res2 || exit $?
   TAG=p23v2000_ ARGS="--n-wanted 2000 --batch 1024 --erase 667" bash tools/exp_one.sh base res1 res2 || exit $?
   TAG=p23v10000_ ARGS="--n-wanted 10000 --batch 512 --erase 3334" bash tools/exp_one.sh base huge3 base huge3 || exit $?
+  TAG=p23c3_ bash tools/exp_one.sh base base || exit $?
 }
 
 "$@"
