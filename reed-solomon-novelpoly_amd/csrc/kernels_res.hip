@@ -6,11 +6,15 @@
 namespace np {
 namespace {
 
-// NP_PRIO_RES (experiment; bit 0 the encode, bit 1 the decode): progress-based
-// issue priority in every transform pass of the resident kernels
-// (fast_common.hpp progress_prio).
+// NP_PRIO_RES (bit 0 the encode, bit 1 the decode): progress-based issue
+// priority in every transform pass of the resident kernels (fast_common.hpp
+// progress_prio).  Measured (profiles/r04_ab.txt probe 23): config-4 encode
+// 2.545 / 2.550 -> 2.422 / 2.424 ms, reconstruct 4.376 / 4.381 -> 4.168 /
+// 4.166 ms (-4.8 % each); 2000 validators (k = 512) reconstruct -4.3 %,
+// encode unchanged.  (The huge kernels' sub-transforms, NP_PRIO_HUGE,
+// measured neutral at 10000 validators.)
 #ifndef NP_PRIO_RES
-#define NP_PRIO_RES 0
+#define NP_PRIO_RES 3
 #endif
 constexpr int kResPrioEnc = NP_PRIO_RES & 1, kResPrioDec = (NP_PRIO_RES >> 1) & 1;
 
