@@ -86,21 +86,25 @@ def aggregate_gib_s(world: int, per_rank: int, payload_len: int, elapsed: float,
     return world * per_rank * payload_len / (elapsed / steps) / 2**30
 
 
-ROUND_TAG = "r04"
+# Profile tags of this round, newest first: the closing profiles (r04g: config
+# 3 and 4) and the mid-round ones (r04: config 2).
+ROUND_TAGS = ("r04g", "r04")
 
 
 def load_traffic(config: int):
     """Per-launch HBM bytes (FETCH_SIZE + WRITE_SIZE, calibrated) of each kernel
-    from the committed PMC summary of this round for this config
+    from the newest committed PMC summary of this round for this config
     (tools/profile_round.sh + tools/pmc_summary.py, measured on this same bench
-    command: profiles/r04_pmc_summary.json for config 3, r04_cfg<c>_... else)."""
-    tag = ROUND_TAG if config == 3 else f"{ROUND_TAG}_cfg{config}"
-    p = os.path.join(ROOT, "profiles", f"{tag}_pmc_summary.json")
-    if not os.path.exists(p):
-        return {}
-    with open(p) as f:
-        summary = json.load(f)
-    return {k: v.get("traffic_bytes") for k, v in summary.get("kernels", {}).items()}
+    command: profiles/<tag>_pmc_summary.json for config 3, <tag>_cfg<c>_...
+    else)."""
+    for rt in ROUND_TAGS:
+        tag = rt if config == 3 else f"{rt}_cfg{config}"
+        p = os.path.join(ROOT, "profiles", f"{tag}_pmc_summary.json")
+        if os.path.exists(p):
+            with open(p) as f:
+                summary = json.load(f)
+            return {k: v.get("traffic_bytes") for k, v in summary.get("kernels", {}).items()}
+    return {}
 
 
 def host_cores():
