@@ -83,6 +83,9 @@ constexpr int kEncPrioCq = NP_PRIO_ENC == 2 ? 4 : NP_PRIO_ENC;
 // Measured: 2.684 / 2.696 -> 2.648 / 2.642 ms (-1.7 %, probe 22).  The
 // encode's span schedule (NP_PRIO_ENC=2) measured neutral.
 constexpr bool kRecPrioSpan = (NP_PRIO_DEC & 8) != 0, kRecPrioSpanFwd = (NP_PRIO_DEC & 16) != 0;
+#ifndef NP_PRIO_PREMUL
+#define NP_PRIO_PREMUL 2  // the premultiply's priority in the span schedule (experiment knob)
+#endif
 constexpr int kRecPrioCq = kRecPrioSpan ? 3 : NP_PRIO_DEC & 1, kRecPrioHi = kRecPrioSpan ? 2 : (NP_PRIO_DEC >> 1) & 1;
 constexpr int kRecPrioFwdHi = kRecPrioSpanFwd ? 3 : (NP_PRIO_DEC >> 2) & 1,
               kRecPrioFwdCq = kRecPrioSpanFwd ? 2 : (NP_PRIO_DEC >> 2) & 1;
@@ -922,7 +925,7 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
       issue_rows(raw, (kExp & 32) ? T.zeros : sh, (kExp & 32) ? 0 : shard_len, m, index + 16 * g, T.zeros, c.lane,
                  c.ncols, c.full, q == 0);
     stamp(c.dbg, 2 + 6 * step);
-    if constexpr (kRecPrioSpan) __builtin_amdgcn_s_setprio(2);
+    if constexpr (kRecPrioSpan) __builtin_amdgcn_s_setprio(NP_PRIO_PREMUL);
     pipelined_rec<16>(
         [&](auto pc) __attribute__((always_inline)) {
           return (cpool_t)(R) + (index + 16 * g + decltype(pc)::value) * kPoolWords;

@@ -16,7 +16,12 @@ namespace {
 #ifndef NP_PRIO_RES
 #define NP_PRIO_RES 3
 #endif
+// Bit 2 (experiment): in the decode steps, one schedule over the span from the
+// row tables' barrier to the CQ write's: the premultiply at 3 then 2, the CQ
+// levels 1, 1, 0, 0.
+constexpr bool kResPrioSpan = (NP_PRIO_RES & 4) != 0;
 constexpr int kResPrioEnc = NP_PRIO_RES & 1, kResPrioDec = (NP_PRIO_RES >> 1) & 1;
+constexpr int kResPrioDecCq = kResPrioSpan ? 3 : kResPrioDec;
 
 // ---------------------------------------------------------------- encode ----
 // One workgroup: 64 chunks of one payload.  mod.rs:144-154 /
@@ -170,6 +175,12 @@ __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructAr
     // in, tower out), in two halves of 8 rows (register pressure)
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
+      if constexpr (kResPrioSpan) {
+        if (half == 0)
+          __builtin_amdgcn_s_setprio(3);
+        else
+          __builtin_amdgcn_s_setprio(2);
+      }
       if (half == 1) load_lane_rows<8>(raw, sh, a.shard_len, I, pm, rr, ncols, full, T.zeros, 8);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -186,7 +197,7 @@ __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructAr
     return false;
   }
   const uint32_t* DL = reinterpret_cast<const uint32_t*>(tile + RGeo<K>::kTileBytes);
-  rcq_levels<true, res_gen<K>(I), kRecDeltaST<K, NQ>, kResPrioDec>(T, I, rr, XL, XH, DL);
+  rcq_levels<true, res_gen<K>(I), kRecDeltaST<K, NQ>, kResPrioDecCq>(T, I, rr, XL, XH, DL);
   if constexpr ((kExp & 32768) != 0 && STEP == 0) {  // experiment: the first step after its CQ levels
     res_copy_out<K>(out_tile, XL, XH, rr, ncols, out16);
     return false;

@@ -287,4 +287,18 @@ p23() {
   TAG=p23c3_ bash tools/exp_one.sh base base || exit $?
 }
 
+# Round-4 probe 24: the resident decode's span schedule ('rspan',
+# NP_PRIO_RES=7) at config 4 and 2000 validators; the fast decode's
+# premultiply at priority 3 or 1 instead of 2 ('pm3', 'pm1') at config 3
+p24() {
+  for v in rspan pm3 pm1; do
+    NP_LIB_PATH=$PWD/tools/exp/lib_$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "not pipeline" > gpurun_out/r04/pytest_gpu24_$v.log 2>&1; rc=$?
+    echo "$v: $(tail -1 gpurun_out/r04/pytest_gpu24_$v.log)"
+    [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu24_$v.log | head -20; exit $rc; }
+  done
+  ARGS="--config 4" TAG=p24c4_ bash tools/exp_one.sh base rspan base rspan || exit $?
+  TAG=p24v2000_ ARGS="--n-wanted 2000 --batch 1024 --erase 667" bash tools/exp_one.sh base rspan || exit $?
+  TAG=p24_ bash tools/exp_one.sh base pm3 pm1 base pm3 pm1 || exit $?
+}
+
 "$@"
