@@ -30,6 +30,14 @@
 namespace np {
 namespace {
 
+// NP_PRIO_BIG (experiment; bit 0 the encode, bit 1 the decode): progress-based
+// issue priority in the sub-segment transforms' passes (fast_common.hpp
+// progress_prio).
+#ifndef NP_PRIO_BIG
+#define NP_PRIO_BIG 0
+#endif
+constexpr int kBigPrioEnc = NP_PRIO_BIG & 1, kBigPrioDec = (NP_PRIO_BIG >> 1) & 1;
+
 constexpr int kS = 256;                   // sub-segment (register-layout) size
 constexpr int kTB = Geo<kS>::kThreads;    // 1024 threads
 constexpr size_t kSegScr = 16u * kTB * 8; // one sub-segment of a tile in thread order: 128 KiB
@@ -280,7 +288,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       tower_convert(T, CL, CH);  // the transforms run in tower coordinates
       with_gen<0, kSubMaxGen<KB>, false>(index, [&](auto gc) __attribute__((always_inline)) {
         constexpr int GEN = decltype(gc)::value;  // 0 only at index 0
-        cq_levels<kS, true, GEN == 0, GEN>(T, VP, index, g, CL, CH);
+        cq_levels<kS, true, GEN == 0, GEN, false, kBigPrioEnc>(T, VP, index, g, CL, CH);
       });
       if constexpr (NP_BIG_ENC_QX) {  // quad items (fast_common.hpp cq_write_q): no byte transposes
         __syncthreads();              // they overlay payload blocks that other waves read
@@ -297,7 +305,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       hi_read<kS>(tile, fresh_v(hb), XL, XH);
     with_gen<0, kSubMaxGen<KB>, false>(index, [&](auto gc) __attribute__((always_inline)) {
       constexpr int GEN = decltype(gc)::value;
-      hi_levels<kS, true, GEN == 0, 0, GEN>(T, VP, index, XL, XH);
+      hi_levels<kS, true, GEN == 0, 0, GEN, kBigPrioEnc>(T, VP, index, XL, XH);
     });
     if (s + 1 < static_cast<uint32_t>(SUBS)) {
       scr_store<false>(scrM + s * kSegScr, tid, XL, XH);
@@ -358,7 +366,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       with_gen<1, kEncBigMaxGenK<KB>, true>(index, [&](auto gc) __attribute__((always_inline)) {
         constexpr int GEN = decltype(gc)::value;
         if constexpr (GEN < 0) tower_convert(T, XL, XH);  // a far shift: Cantor coordinates
-        hi_levels<kS, false, false, 0, GEN>(T, VP, index, XL, XH);
+        hi_levels<kS, false, false, 0, GEN, kBigPrioEnc>(T, VP, index, XL, XH);
       });
       if constexpr (NP_BIG_ENC_QX) {
         hi_write_q(tile, g, lane, XL, XH);
@@ -371,7 +379,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       }
       with_gen<1, kEncBigMaxGenK<KB>, true>(index, [&](auto gc) __attribute__((always_inline)) {
         constexpr int GEN = decltype(gc)::value;
-        cq_levels<kS, false, false, GEN>(T, VP, index, g, XL, XH);
+        cq_levels<kS, false, false, GEN, false, kBigPrioEnc>(T, VP, index, g, XL, XH);
         if constexpr (GEN >= 0) tower_convert(T, XL, XH);  // back to Cantor coordinates for the rows
       });
       store_rows(out, a.shard_len, index + 16 * g, a.wanted_n, XL, XH, lane, ncols, full,
@@ -617,7 +625,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       }
       with_gen<0, kRecBigMaxGen<KB, NQ>, false>(index, [&](auto gc) __attribute__((always_inline)) {
         constexpr int GEN = decltype(gc)::value;  // 0 only at index 0
-        cq_levels<kS, true, GEN == 0, GEN>(T, VP, index, gg, XL, XH);
+        cq_levels<kS, true, GEN == 0, GEN, false, kBigPrioDec>(T, VP, index, gg, XL, XH);
       });
       cq_write<kS>(tile, fresh_v(cqb), XL, XH);
     }
@@ -625,7 +633,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
     hi_read<kS>(tile, fresh_v(hb), XL, XH);
     with_gen<0, kRecBigMaxGen<KB, NQ>, false>(index, [&](auto gc) __attribute__((always_inline)) {
       constexpr int GEN = decltype(gc)::value;
-      hi_levels<kS, true, GEN == 0, 0, GEN>(T, VP, index, XL, XH);
+      hi_levels<kS, true, GEN == 0, 0, GEN, kBigPrioDec>(T, VP, index, XL, XH);
     });
     if (qs + 1 < static_cast<uint32_t>(SUBS * NQ)) {
       scr_store<true>(scrY + qs * kSegScr, tid, XL, XH);
@@ -791,7 +799,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
     if (s != 0) scr_load<true>(scrD + s * kSegScr, tid, XL, XH);
     with_gen<0, kSubMaxGen<KB>, false>(index, [&](auto gc) __attribute__((always_inline)) {
       constexpr int GEN = decltype(gc)::value;
-      hi_levels<kS, false, GEN == 0, 0, GEN>(T, VP, index, XL, XH);
+      hi_levels<kS, false, GEN == 0, 0, GEN, kBigPrioDec>(T, VP, index, XL, XH);
     });
     hi_write<kS>(tile, fresh_v(hb), XL, XH);
     __syncthreads();
@@ -800,7 +808,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       cq_read<kS>(tile, cq, XL, XH);
       with_gen<0, kSubMaxGen<KB>, false>(index, [&](auto gc) __attribute__((always_inline)) {
         constexpr int GEN = decltype(gc)::value;
-        cq_levels<kS, false, GEN == 0, GEN>(T, VP, index, gg, XL, XH);
+        cq_levels<kS, false, GEN == 0, GEN, false, kBigPrioDec>(T, VP, index, gg, XL, XH);
       });
 #pragma unroll
       for (int half = 0; half < 2; ++half) {

@@ -301,4 +301,13 @@ p24() {
   TAG=p24_ bash tools/exp_one.sh base pm3 pm1 base pm3 pm1 || exit $?
 }
 
+# Round-4 probe 25: progress-based priority in the big kernels (k = 2048:
+# 7000 validators; 'big3' = encode and decode), parity first
+p25() {
+  NP_LIB_PATH=$PWD/tools/exp/lib_big3.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "not pipeline" > gpurun_out/r04/pytest_gpu25_big3.log 2>&1; rc=$?
+  echo "big3: $(tail -1 gpurun_out/r04/pytest_gpu25_big3.log)"
+  [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu25_big3.log | head -20; exit $rc; }
+  TAG=p25v7000_ ARGS="--n-wanted 7000 --batch 512 --erase 2334" bash tools/exp_one.sh base big3 base big3 || exit $?
+}
+
 "$@"
