@@ -53,9 +53,10 @@ struct DevBuf {
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
-    size_t want = std::max(bytes, cap * 2);
-    hipError_t e = hipMalloc(&p, want);
-    if (e == hipSuccess) cap = want;
+    // exactly the size asked for (the context scratch is capped by its callers:
+    // engine.cpp big_scratch, kBigScratchCap)
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipSuccess) cap = bytes;
     return e;
   }
   void release() {
