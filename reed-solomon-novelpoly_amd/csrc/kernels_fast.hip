@@ -86,7 +86,11 @@ constexpr bool kRecPrioSpan = (NP_PRIO_DEC & 8) != 0, kRecPrioSpanFwd = (NP_PRIO
 #ifndef NP_PRIO_PREMUL
 #define NP_PRIO_PREMUL 2  // the premultiply's priority in the span schedule (3 and 1 measured within noise, probe 24)
 #endif
-constexpr int kRecPrioCq = kRecPrioSpan ? 3 : NP_PRIO_DEC & 1, kRecPrioHi = kRecPrioSpan ? 2 : (NP_PRIO_DEC >> 1) & 1;
+#ifndef NP_PRIO_SPAN_HI
+#define NP_PRIO_SPAN_HI 2  // the high levels' schedule in the span (progress_prio PRIO; experiment knob)
+#endif
+constexpr int kRecPrioCq = kRecPrioSpan ? 3 : NP_PRIO_DEC & 1,
+              kRecPrioHi = kRecPrioSpan ? NP_PRIO_SPAN_HI : (NP_PRIO_DEC >> 1) & 1;
 constexpr int kRecPrioFwdHi = kRecPrioSpanFwd ? 3 : (NP_PRIO_DEC >> 2) & 1,
               kRecPrioFwdCq = kRecPrioSpanFwd ? 2 : (NP_PRIO_DEC >> 2) & 1;
 

@@ -310,4 +310,15 @@ p25() {
   TAG=p25v7000_ ARGS="--n-wanted 7000 --batch 512 --erase 2334" bash tools/exp_one.sh base big3 base big3 || exit $?
 }
 
+# Round-4 probe 26: the fast decode's high levels at 3, 3, 2, 2 inside the span
+# ('hi4'; with the premultiply at 1: 'hi4pm1') at config 3, parity first
+p26() {
+  for v in hi4 hi4pm1; do
+    NP_LIB_PATH=$PWD/tools/exp/lib_$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "not pipeline" > gpurun_out/r04/pytest_gpu26_$v.log 2>&1; rc=$?
+    echo "$v: $(tail -1 gpurun_out/r04/pytest_gpu26_$v.log)"
+    [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r04/pytest_gpu26_$v.log | head -20; exit $rc; }
+  done
+  TAG=p26_ bash tools/exp_one.sh base hi4 hi4pm1 base hi4 hi4pm1 base hi4 hi4pm1 || exit $?
+}
+
 "$@"
