@@ -87,7 +87,7 @@ constexpr bool kRecPrioSpan = (NP_PRIO_DEC & 8) != 0, kRecPrioSpanFwd = (NP_PRIO
 #define NP_PRIO_PREMUL 2  // the premultiply's priority in the span schedule (3 and 1 measured within noise, probe 24)
 #endif
 #ifndef NP_PRIO_SPAN_HI
-#define NP_PRIO_SPAN_HI 2  // the high levels' schedule in the span (progress_prio PRIO; experiment knob)
+#define NP_PRIO_SPAN_HI 2  // the high levels' schedule in the span (progress_prio PRIO; 4 measured within noise, probe 26)
 #endif
 constexpr int kRecPrioCq = kRecPrioSpan ? 3 : NP_PRIO_DEC & 1,
               kRecPrioHi = kRecPrioSpan ? NP_PRIO_SPAN_HI : (NP_PRIO_DEC >> 1) & 1;
