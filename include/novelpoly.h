@@ -49,8 +49,16 @@ typedef enum np_status {
 /* Error payload of the last failing call on this thread (fields as in
  * errors.rs: NeedMoreShards -> {have,min,all}; InconsistentShardLengths ->
  * {first,other,0}; WantedShardCountTooHigh/Low -> {n,0,0};
- * WantedPayloadShardCountTooLow -> {k,0,0}; ParamterMustBePowerOf2 -> {n,k,0}). */
+ * WantedPayloadShardCountTooLow -> {k,0,0}; ParamterMustBePowerOf2 -> {n,k,0};
+ * NP_ERR_DEVICE / NP_ERR_ALLOC -> {hipError_t, call-site id, 0}: the id is the
+ * engine line of the HIP call that returned the error, 0 if not recorded). */
 void np_last_error_detail(size_t out[3]);
+/* The HIP call behind the last NP_ERR_DEVICE / NP_ERR_ALLOC on this thread, as
+ * text ("engine.cpp:<line> <call>: <hipError name>"; "" before any).  An
+ * asynchronous kernel or copy fault is reported by the synchronisation that saw
+ * it; with NP_SYNC_EACH set in the environment the host batch calls synchronise
+ * after every step, so that the step itself is named. */
+const char* np_last_error_site(void);
 /* Human readable message mirroring the thiserror strings of errors.rs. */
 const char* np_status_message(int status);
 

@@ -89,7 +89,9 @@ fn to_error(status: c_int) -> Error {
 		sys::NP_ERR_EMPTY_SHARD => Error::EmptyShard,
 		s => {
 			let msg = unsafe { std::ffi::CStr::from_ptr(sys::np_status_message(s)) };
-			panic!("novelpoly-mi355x: status {s}: {}", msg.to_string_lossy())
+			// device and allocation failures name the HIP call that returned them
+			let site = unsafe { std::ffi::CStr::from_ptr(sys::np_last_error_site()) };
+			panic!("novelpoly-mi355x: status {s}: {} [{}]", msg.to_string_lossy(), site.to_string_lossy())
 		},
 	}
 }

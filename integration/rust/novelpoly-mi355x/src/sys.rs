@@ -45,6 +45,7 @@ pub const NP_ERR_NO_DEVICE: c_int = 103;
 
 extern "C" {
 	pub fn np_last_error_detail(out: *mut usize);
+	pub fn np_last_error_site() -> *const c_char;
 	pub fn np_status_message(status: c_int) -> *const c_char;
 
 	pub fn np_recoverability_subset_size(n_wanted_shards: usize) -> usize;

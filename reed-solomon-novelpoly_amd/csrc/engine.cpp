@@ -8,6 +8,8 @@
 
 #include <algorithm>
 #include <array>
+#include <iterator>
+#include <map>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -31,6 +33,25 @@ int fail(int st, size_t a = 0, size_t b = 0, size_t c = 0) {
   g_detail[2] = c;
   return st;
 }
+
+// Call site of the first failing HIP call since the last status was reported
+// (HIP(expr) below): its engine.cpp line and text.  dev_err turns it into the
+// NP_ERR_DEVICE / NP_ERR_ALLOC detail {hipError_t, line, 0} and the text of
+// np_last_error_site, so a failure names the call that returned it -- for an
+// asynchronous kernel or copy fault that is the synchronisation that saw it
+// (NP_SYNC_EACH=1 below makes the host pipeline synchronise after every step).
+thread_local int g_site_line = 0;
+thread_local const char* g_site_call = nullptr;
+thread_local char g_site_msg[192] = "";
+
+hipError_t at_site(hipError_t e, int line, const char* call) {
+  if (e != hipSuccess && !g_site_line) {
+    g_site_line = line;
+    g_site_call = call;
+  }
+  return e;
+}
+#define HIP(x) at_site((x), __LINE__, #x)
 
 bool is_pow2(size_t x) { return x && !(x & (x - 1)); }
 size_t next_pow2(size_t x) {
@@ -56,7 +77,10 @@ struct DevBuf {
     // exactly the size asked for (the context scratch is capped by its callers:
     // engine.cpp big_scratch, kBigScratchCap)
     hipError_t e = hipMalloc(&p, bytes);
-    if (e == hipSuccess) cap = bytes;
+    if (e == hipSuccess)
+      cap = bytes;
+    else
+      (void)hipGetLastError();  // returned here: not left behind for the next launch's hipGetLastError
     return e;
   }
   void release() {
@@ -79,7 +103,10 @@ struct HostBuf {  // pinned staging that only grows
     p = nullptr;
     cap = 0;
     hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
-    if (e == hipSuccess) cap = bytes;
+    if (e == hipSuccess)
+      cap = bytes;
+    else
+      (void)hipGetLastError();
     return e;
   }
   void release() {
@@ -106,6 +133,7 @@ struct np_ctx {
   std::mutex mu;  // serialises host-API calls (they share the scratch buffers)
   DevBuf d_in, d_out, d_present;
   HostBuf h_in, h_out;
+  HostBuf h_pres;  // pinned staging of present masks (np_reconstruct_batch_dev / _host, np_rs_reconstruct)
   // Per-workgroup scratch of the k = 1024 kernels (kernels_big.hip).  Launches
   // on different streams are ordered through big_done so they never share it.
   DevBuf d_big;
@@ -126,9 +154,17 @@ struct np_ctx {
 namespace {
 
 int dev_err(hipError_t e) {
+  const int line = g_site_line;
+  const char* call = g_site_call;
+  g_site_line = 0;
+  g_site_call = nullptr;
   if (e == hipSuccess) return NP_OK;
-  if (e == hipErrorOutOfMemory) return fail(NP_ERR_ALLOC);
-  return fail(NP_ERR_DEVICE, static_cast<size_t>(e));
+  if (line)
+    std::snprintf(g_site_msg, sizeof g_site_msg, "engine.cpp:%d %s: %s", line, call, hipGetErrorName(e));
+  else
+    std::snprintf(g_site_msg, sizeof g_site_msg, "(call site not recorded): %s", hipGetErrorName(e));
+  return fail(e == hipErrorOutOfMemory ? NP_ERR_ALLOC : NP_ERR_DEVICE, static_cast<size_t>(e),
+              static_cast<size_t>(line));
 }
 
 template <class T>
@@ -137,7 +173,7 @@ hipError_t upload(np_ctx* c, const std::vector<T>& v, const T** dst) {
   hipError_t e = hipMalloc(&p, v.size() * sizeof(T));
   if (e != hipSuccess) return e;
   c->table_allocs.push_back(p);
-  e = hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+  e = HIP(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
   *dst = static_cast<const T*>(p);
   return e;
 }
@@ -174,12 +210,12 @@ constexpr size_t kBigScratchCap = size_t(2) << 30;  // bytes of big-kernel scrat
 hipError_t big_scratch(np_ctx* c, size_t want, hipStream_t s, uint8_t** out, size_t* bytes) {
   want = std::min(want, kBigScratchCap);
   hipError_t e = hipSuccess;
-  if (!c->big_done) e = hipEventCreateWithFlags(&c->big_done, hipEventDisableTiming);
+  if (!c->big_done) e = HIP(hipEventCreateWithFlags(&c->big_done, hipEventDisableTiming));
   if (e == hipSuccess && c->big_used) {
-    if (want > c->d_big.cap) e = hipEventSynchronize(c->big_done);  // about to free the old buffer
-    if (e == hipSuccess) e = hipStreamWaitEvent(s, c->big_done, 0);
+    if (want > c->d_big.cap) e = HIP(hipEventSynchronize(c->big_done));  // about to free the old buffer
+    if (e == hipSuccess) e = HIP(hipStreamWaitEvent(s, c->big_done, 0));
   }
-  if (e == hipSuccess) e = c->d_big.ensure(want);
+  if (e == hipSuccess) e = HIP(c->d_big.ensure(want));
   *out = c->d_big.as<uint8_t>();
   *bytes = c->d_big.cap;
   return e;
@@ -188,7 +224,7 @@ hipError_t big_scratch(np_ctx* c, size_t want, hipStream_t s, uint8_t** out, siz
 hipError_t big_done(np_ctx* c, hipStream_t s, hipError_t e) {
   if (e != hipSuccess) return e;
   c->big_used = true;
-  return hipEventRecord(c->big_done, s);
+  return HIP(hipEventRecord(c->big_done, s));
 }
 
 // Scratch slots of a k = 512 / 1024 launch over `tiles` tiles: one per resident workgroup.
@@ -224,8 +260,8 @@ RecPath rec_path(uint32_t n, uint32_t k, size_t shard_len) {
 
 // Caller holds the context lock.
 hipError_t launch_encode(np_ctx* c, const np::EncodeArgs& a, hipStream_t s) {
-  if (np::fast_encode_supported(a.n, a.k)) return np::launch_encode_fast(c->T, a, s);
-  if (np::res_encode_supported(a.n, a.k) && np::res_enabled()) return np::launch_encode_res(c->T, a, s);
+  if (np::fast_encode_supported(a.n, a.k)) return HIP(np::launch_encode_fast(c->T, a, s));
+  if (np::res_encode_supported(a.n, a.k) && np::res_enabled()) return HIP(np::launch_encode_res(c->T, a, s));
   const size_t huge_per = np::huge_encode_scratch_per_payload(a.shard_len, a.n, a.k);
   if (np::huge_encode_supported(a.n, a.k) && huge_on(a.k) && huge_per <= kBigScratchCap) {
     // slices of the batch whose tile slots fit the context scratch
@@ -238,7 +274,7 @@ hipError_t launch_encode(np_ctx* c, const np::EncodeArgs& a, hipStream_t s) {
       uint8_t* scr = nullptr;
       size_t bytes = 0;
       hipError_t e = big_scratch(c, sub.batch * huge_per, s, &scr, &bytes);
-      if (e == hipSuccess) e = np::launch_encode_huge(c->T, sub, scr, s);
+      if (e == hipSuccess) e = HIP(np::launch_encode_huge(c->T, sub, scr, s));
       e = big_done(c, s, e);
       if (e != hipSuccess) return e;
     }
@@ -249,10 +285,10 @@ hipError_t launch_encode(np_ctx* c, const np::EncodeArgs& a, hipStream_t s) {
     uint8_t* scr = nullptr;
     size_t bytes = 0;
     hipError_t e = big_scratch(c, big_slots(c, a.batch * tiles, a.n, a.k, false) * np::big_encode_scratch_per_tile(a.k), s, &scr, &bytes);
-    if (e == hipSuccess) e = np::launch_encode_big(c->T, a, scr, bytes, s);
+    if (e == hipSuccess) e = HIP(np::launch_encode_big(c->T, a, scr, bytes, s));
     return big_done(c, s, e);
   }
-  return np::launch_encode_generic(c->T, a, s);
+  return HIP(np::launch_encode_generic(c->T, a, s));
 }
 
 // Payload `b0` onward of a (a slice of the batch; status follows when set).
@@ -290,9 +326,9 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
       size_t bytes = 0;
       hipError_t e = big_scratch(c, sub.batch * (stride + own_status), s, &scr, &bytes);
       if (!a.status) sub.status = reinterpret_cast<uint32_t*>(scr + sub.batch * stride);
-      if (e == hipSuccess) e = np::launch_prefix_locator(c->T, sub, scr, s);
+      if (e == hipSuccess) e = HIP(np::launch_prefix_locator(c->T, sub, scr, s));
       sub.prefix = scr;
-      if (e == hipSuccess) e = res ? np::launch_reconstruct_res(c->T, sub, s) : np::launch_reconstruct_fast(c->T, sub, s);
+      if (e == hipSuccess) e = res ? HIP(np::launch_reconstruct_res(c->T, sub, s)) : HIP(np::launch_reconstruct_fast(c->T, sub, s));
       e = big_done(c, s, e);
       if (e != hipSuccess) return e;
     }
@@ -312,7 +348,7 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
       uint16_t* loc = reinterpret_cast<uint16_t*>(side0);
       uint8_t* mode = side0 + (a.locators ? 0 : 2 * static_cast<size_t>(a.n) * sub.batch);
       if (!a.status) sub.status = reinterpret_cast<uint32_t*>(mode + (sub.batch + 15) / 16 * 16);
-      if (e == hipSuccess) e = np::launch_reconstruct_huge(c->T, sub, scr, mode, loc, s);
+      if (e == hipSuccess) e = HIP(np::launch_reconstruct_huge(c->T, sub, scr, mode, loc, s));
       e = big_done(c, s, e);
       if (e != hipSuccess) return e;
     }
@@ -334,8 +370,8 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
       if (e == hipSuccess && bytes < rec_bytes + 8 * per_tile) e = hipErrorInvalidValue;
       if (!a.status) sub.status = reinterpret_cast<uint32_t*>(scr + sub.batch * np::big_record_stride(a.n));
       sub.prefix = scr;
-      if (e == hipSuccess) e = np::launch_big_records(c->T, sub, scr, s);
-      if (e == hipSuccess) e = np::launch_reconstruct_big(c->T, sub, scr + rec_bytes, bytes - rec_bytes, s);
+      if (e == hipSuccess) e = HIP(np::launch_big_records(c->T, sub, scr, s));
+      if (e == hipSuccess) e = HIP(np::launch_reconstruct_big(c->T, sub, scr + rec_bytes, bytes - rec_bytes, s));
       e = big_done(c, s, e);
       if (e != hipSuccess) return e;
     }
@@ -351,12 +387,12 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
     size_t bytes = 0;
     hipError_t e = big_scratch(c, std::max<size_t>(1, b.batch * (loc_bytes + own_status)), s, &scr, &bytes);
     if (!a.status) b.status = reinterpret_cast<uint32_t*>(scr + b.batch * loc_bytes);
-    if (e == hipSuccess) e = np::launch_payload_status(b, s);
+    if (e == hipSuccess) e = HIP(np::launch_payload_status(b, s));
     if (!a.locators) {
       b.locators = reinterpret_cast<uint16_t*>(scr);
-      if (e == hipSuccess) e = np::launch_error_locator(c->T, a.n, b.present, b.batch, reinterpret_cast<uint16_t*>(scr), s);
+      if (e == hipSuccess) e = HIP(np::launch_error_locator(c->T, a.n, b.present, b.batch, reinterpret_cast<uint16_t*>(scr), s));
     }
-    if (e == hipSuccess) e = np::launch_reconstruct_generic(c->T, b, s);
+    if (e == hipSuccess) e = HIP(np::launch_reconstruct_generic(c->T, b, s));
     e = big_done(c, s, e);
     if (e != hipSuccess) return e;
   }
@@ -424,6 +460,8 @@ void np_last_error_detail(size_t out[3]) {
   out[1] = g_detail[1];
   out[2] = g_detail[2];
 }
+
+const char* np_last_error_site(void) { return g_site_msg; }
 
 const char* np_status_message(int st) {
   switch (st) {  // errors.rs:4-28
@@ -561,6 +599,7 @@ void np_ctx_destroy(np_ctx* c) {
   c->pipe_pres.release();
   c->h_in.release();
   c->h_out.release();
+  c->h_pres.release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -571,7 +610,7 @@ int np_ctx_device(np_ctx* c) { return c ? c->device : -1; }
 int np_ctx_synchronize(np_ctx* c) {
   if (!c) return fail(NP_ERR_INVALID_ARGUMENT);
   (void)hipSetDevice(c->device);
-  return dev_err(hipStreamSynchronize(c->stream));
+  return dev_err(HIP(hipStreamSynchronize(c->stream)));
 }
 
 // --------------------------------------------------------------- encode ----
@@ -585,17 +624,17 @@ int np_rs_encode(np_ctx* c, const np_code_params* p, const uint8_t* payload, siz
   std::lock_guard<std::mutex> g(c->mu);
   (void)hipSetDevice(c->device);
   const size_t out_bytes = p->wanted_n * shard_len;
-  hipError_t e = c->d_in.ensure(len);
-  if (e == hipSuccess) e = c->d_out.ensure(std::max<size_t>(out_bytes, 1));
-  if (e == hipSuccess) e = c->h_in.ensure(len);
-  if (e == hipSuccess) e = c->h_out.ensure(std::max<size_t>(out_bytes, 1));
+  hipError_t e = HIP(c->d_in.ensure(len));
+  if (e == hipSuccess) e = HIP(c->d_out.ensure(std::max<size_t>(out_bytes, 1)));
+  if (e == hipSuccess) e = HIP(c->h_in.ensure(len));
+  if (e == hipSuccess) e = HIP(c->h_out.ensure(std::max<size_t>(out_bytes, 1)));
   if (e != hipSuccess) return dev_err(e);
   std::memcpy(c->h_in.p, payload, len);
-  e = hipMemcpyAsync(c->d_in.p, c->h_in.p, len, hipMemcpyHostToDevice, c->stream);
+  e = HIP(hipMemcpyAsync(c->d_in.p, c->h_in.p, len, hipMemcpyHostToDevice, c->stream));
   np::EncodeArgs a = enc_args(p, c->d_in.as<uint8_t>(), len, len, 1, c->d_out.as<uint8_t>(), out_bytes);
-  if (e == hipSuccess) e = launch_encode(c, a, c->stream);
-  if (e == hipSuccess) e = hipMemcpyAsync(c->h_out.p, c->d_out.p, out_bytes, hipMemcpyDeviceToHost, c->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) e = HIP(launch_encode(c, a, c->stream));
+  if (e == hipSuccess) e = HIP(hipMemcpyAsync(c->h_out.p, c->d_out.p, out_bytes, hipMemcpyDeviceToHost, c->stream));
+  if (e == hipSuccess) e = HIP(hipStreamSynchronize(c->stream));
   if (e != hipSuccess) return dev_err(e);
   std::memcpy(shards_out, c->h_out.p, out_bytes);
   return NP_OK;
@@ -620,36 +659,121 @@ int np_encode_batch_dev(np_ctx* c, const np_code_params* p, const uint8_t* d_pay
   std::lock_guard<std::mutex> g(c->mu);
   (void)hipSetDevice(c->device);
   np::EncodeArgs a = enc_args(p, d_payloads, len, pstride, batch, d_shards, bstride);
-  return dev_err(launch_encode(c, a, pick(c, stream)));
+  return dev_err(HIP(launch_encode(c, a, pick(c, stream))));
 }
+
+}  // extern "C"
 
 // ------------------------------------------------- host-memory pipeline ----
 // the caller's view of encode / reconstruct, buffers in host
 // memory.  The batch goes in sub-batches of about kPipeSlotBytes over
 // np_ctx::kPipe streams; each sub-batch is H2D -> kernel -> D2H on its
 // stream, so the copies of one overlap the kernels and the opposite-direction
-// copies of the others (PCIe is full duplex).  Host buffers allocated with
-// hipHostMalloc / registered with hipHostRegister are copied by DMA directly;
-// pageable ones are staged by the runtime and overlap less.
+// copies of the others (PCIe is full duplex).
+//
+// No pageable pointer is ever handed to a HIP copy.  Every host span of a
+// call is one of
+//  - pinned by the caller (hipHostMalloc, torch pin_memory, hipHostRegister;
+//    mapped_host_range finds it): DMA, or the present-row gather kernel,
+//    straight from / to it;
+//  - pinned in place for the call through the process-wide PinRegistry
+//    (pageable spans of at least kPinMinBytes): the same;
+//  - staged: host threads copy it into / out of the context's pinned staging
+//    slots, and the DMA or the gather runs from / to those.
+// Round 4 still let the runtime copy pageable spans whose rows were not
+// 4-byte aligned (hipMemcpy2DAsync from a numpy array, right after the same
+// pages had been registered and unregistered), and one GPU run faulted in
+// that call.
 namespace {
 
 constexpr size_t kPipeSlotBytes = size_t(64) << 20;
+// Pageable spans below this are staged: registering and unregistering them
+// costs more than copying them.
+constexpr size_t kPinMinBytes = size_t(1) << 20;
+
+// The page ranges this library registered in place, process-wide.
+// hipHostRegister pins whole pages, so the range pinned for one span can share
+// its first and last page with a neighbouring span: the adjacent slice of the
+// same caller buffer on another thread (np_*_host_multi), or another call's
+// buffer.  Each registered range is refcounted under one lock: a span inside a
+// registered range takes a reference, a span that only partly overlaps one is
+// staged instead, and the range is unregistered when its last reference goes
+// -- after the streams of every call that used it have drained.
+class PinRegistry {
+ public:
+  // Registered base of a range holding [p, p + bytes), or 0 (stage instead).
+  uintptr_t acquire(const void* p, size_t bytes) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p) & ~uintptr_t(4095);
+    const uintptr_t z = (reinterpret_cast<uintptr_t>(p) + bytes + 4095) & ~uintptr_t(4095);
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = ranges_.upper_bound(a);  // the first range starting above a
+    if (it != ranges_.begin()) {
+      auto pv = std::prev(it);
+      if (pv->second.end >= z) {
+        ++pv->second.refs;
+        return pv->first;
+      }
+      if (pv->second.end > a) return 0;
+    }
+    if (it != ranges_.end() && it->first < z) return 0;
+    if (hipHostRegister(reinterpret_cast<void*>(a), z - a, hipHostRegisterMapped | hipHostRegisterPortable) !=
+        hipSuccess) {
+      (void)hipGetLastError();  // refused (e.g. the caller registered an overlapping range): stage
+      return 0;
+    }
+    ranges_[a] = Range{z, 1};
+    return a;
+  }
+  void release(uintptr_t base) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = ranges_.find(base);
+    if (it == ranges_.end() || --it->second.refs) return;
+    (void)hipHostUnregister(reinterpret_cast<void*>(base));
+    ranges_.erase(it);
+  }
+
+ private:
+  struct Range {
+    uintptr_t end;
+    size_t refs;
+  };
+  std::mutex mu_;
+  std::map<uintptr_t, Range> ranges_;
+};
+
+PinRegistry& pins() {
+  static PinRegistry* r = new PinRegistry;  // never destroyed: calls may run during static destruction
+  return *r;
+}
 
 hipError_t pipe_init(np_ctx* c) {
-  for (int i = 0; i < np_ctx::kPipe; ++i)
+  for (int i = 0; i < np_ctx::kPipe; ++i) {
     if (!c->pipe_s[i]) {
-      hipError_t e = hipStreamCreateWithFlags(&c->pipe_s[i], hipStreamNonBlocking);
+      hipError_t e = HIP(hipStreamCreateWithFlags(&c->pipe_s[i], hipStreamNonBlocking));
       if (e != hipSuccess) return e;
     }
+    if (!c->pipe_ev[i]) {
+      hipError_t e = HIP(hipEventCreateWithFlags(&c->pipe_ev[i], hipEventDisableTiming));
+      if (e != hipSuccess) return e;
+    }
+  }
   return hipSuccess;
 }
 
 hipError_t pipe_sync(np_ctx* c, hipError_t e) {
   for (int i = 0; i < np_ctx::kPipe; ++i) {
-    const hipError_t r = hipStreamSynchronize(c->pipe_s[i]);
+    const hipError_t r = HIP(hipStreamSynchronize(c->pipe_s[i]));
     if (e == hipSuccess) e = r;
   }
   return e;
+}
+
+// NP_SYNC_EACH=1: the host pipeline waits for its stream after every step, so
+// that an asynchronous fault is reported at the step that caused it (its line
+// and name in np_last_error_site) instead of at the final synchronisation.
+hipError_t after(hipError_t e, hipStream_t s, int line, const char* step) {
+  if (e != hipSuccess || !std::getenv("NP_SYNC_EACH")) return e;
+  return at_site(hipStreamSynchronize(s), line, step);
 }
 
 // Rows of each payload the reconstruct kernels read: on the fast, resident,
@@ -678,7 +802,7 @@ constexpr uint32_t kGatherBlocks = 32;
 // allocation mapped into the device address space (hipHostMalloc, torch's
 // pin_memory, hipHostRegister), else nullptr (pageable memory).
 const uint8_t* mapped_host_range(const uint8_t* p, size_t bytes) {
-  if (bytes == 0 || std::getenv("NP_NO_GATHER")) return nullptr;
+  if (bytes == 0) return nullptr;
   hipPointerAttribute_t a0{}, a1{};
   if (hipPointerGetAttributes(&a0, p) != hipSuccess || hipPointerGetAttributes(&a1, p + bytes - 1) != hipSuccess) {
     (void)hipGetLastError();
@@ -691,28 +815,73 @@ const uint8_t* mapped_host_range(const uint8_t* p, size_t bytes) {
   return d0;
 }
 
-// Pins the pages of [p, p + bytes) in place and maps them for the device
-// (hipHostRegister); returns the registered base for unpin, or nullptr when the
-// runtime refuses (the range overlaps a registered one, ...).
-void* pin_range(const void* p, size_t bytes) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p) & ~uintptr_t(4095);
-  const uintptr_t z = (reinterpret_cast<uintptr_t>(p) + bytes + 4095) & ~uintptr_t(4095);
-  if (hipHostRegister(reinterpret_cast<void*>(a), z - a, hipHostRegisterMapped) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  return reinterpret_cast<void*>(a);
-}
-
-// How pageable buffers of the host reconstruct go: "pin" (default) registers
-// them for the call, "gather" copies the present rows into pinned staging on
-// host threads (NP_PAGEABLE).
+// Pageable buffers are pinned in place (default) or, with NP_PAGEABLE=stage,
+// always staged through pinned memory by host threads (read per call).
 bool pageable_pin() {
   const char* m = std::getenv("NP_PAGEABLE");
-  return !m || std::strcmp(m, "gather") != 0;
+  return !m || (std::strcmp(m, "stage") != 0 && std::strcmp(m, "gather") != 0);
+}
+
+// A host span for the length of a call: its device address when the caller
+// pinned it or it was pinned in place here, else nullptr (staged).  Holds its
+// registry reference until destroyed, so it must outlive every stream
+// operation on the span (the calls synchronise their streams before return).
+class HostSpan {
+ public:
+  HostSpan(const void* p, size_t bytes, bool may_pin) {
+    const uint8_t* b = static_cast<const uint8_t*>(p);
+    dev_ = mapped_host_range(b, bytes);
+    if (dev_ || !may_pin || bytes < kPinMinBytes) return;
+    base_ = pins().acquire(p, bytes);
+    if (base_) dev_ = mapped_host_range(b, bytes);
+  }
+  ~HostSpan() {
+    if (base_) pins().release(base_);
+  }
+  HostSpan(const HostSpan&) = delete;
+  HostSpan& operator=(const HostSpan&) = delete;
+  const uint8_t* dev() const { return dev_; }
+  bool pinned() const { return dev_ != nullptr; }
+
+ private:
+  const uint8_t* dev_ = nullptr;
+  uintptr_t base_ = 0;
+};
+
+// Per-slot bookkeeping of a staged pipeline: a slot's pinned staging may be
+// refilled once the sub-batch that last used it is done (its event), whose
+// staged outputs are then handed to the caller (copy_out(b0, cnt, slot)).
+struct SlotRing {
+  np_ctx* c;
+  size_t b0[np_ctx::kPipe] = {}, cnt[np_ctx::kPipe] = {};
+  template <class F>
+  void drain(int sl, hipError_t& e, F copy_out) {
+    if (!cnt[sl]) return;
+    const hipError_t r = HIP(hipEventSynchronize(c->pipe_ev[sl]));
+    if (e == hipSuccess) e = r;
+    if (r == hipSuccess) copy_out(b0[sl], cnt[sl], sl);
+    cnt[sl] = 0;
+  }
+  hipError_t mark(int sl, hipStream_t s, size_t first, size_t count) {
+    const hipError_t e = HIP(hipEventRecord(c->pipe_ev[sl], s));
+    if (e == hipSuccess) b0[sl] = first, cnt[sl] = count;
+    return e;
+  }
+};
+
+// cnt blocks of `len` bytes, src + b * sstride -> dst + b * dstride, on host
+// threads in pieces of at most 1 MiB.
+void copy_blocks(uint8_t* dst, size_t dstride, const uint8_t* src, size_t sstride, size_t len, size_t cnt) {
+  const size_t pieces = (len + (size_t(1) << 20) - 1) >> 20;
+  parallel_for(cnt * pieces, [&](size_t i) {
+    const size_t b = i / pieces, off = (i % pieces) << 20, l = std::min<size_t>(len - off, size_t(1) << 20);
+    stream_copy(dst + b * dstride + off, src + b * sstride + off, l);
+  });
 }
 
 }  // namespace
+
+extern "C" {
 
 int np_encode_batch_host(np_ctx* c, const np_code_params* p, const uint8_t* payloads, size_t len, size_t pstride,
                          size_t batch, uint8_t* shards, size_t bstride) {
@@ -725,36 +894,51 @@ int np_encode_batch_host(np_ctx* c, const np_code_params* p, const uint8_t* payl
   if (batch == 0) return NP_OK;
   std::lock_guard<std::mutex> g(c->mu);
   (void)hipSetDevice(c->device);
-  // pageable buffers pinned in place for the call (NP_PAGEABLE=pin): the
-  // copies then run as DMA from / to pinned memory, at the PCIe rate
   const size_t span_in = (batch - 1) * pstride + len, span_out = (batch - 1) * bstride + row_bytes;
-  void* pinned_in = nullptr;
-  void* pinned_out = nullptr;
-  if (pageable_pin()) {
-    if (!mapped_host_range(payloads, span_in)) pinned_in = pin_range(payloads, span_in);
-    if (!mapped_host_range(shards, span_out)) pinned_out = pin_range(shards, span_out);
-  }
+  const bool may_pin = pageable_pin();
+  const HostSpan hin(payloads, span_in, may_pin), hout(shards, span_out, may_pin);
+  const bool st_in = !hin.pinned(), st_out = !hout.pinned();
   hipError_t e = pipe_init(c);
   const size_t sb = std::min(batch, std::max<size_t>(1, kPipeSlotBytes / (len + row_bytes)));
   for (int i = 0; e == hipSuccess && i < np_ctx::kPipe; ++i) {
-    e = c->pipe_in[i].ensure(sb * len);
-    if (e == hipSuccess) e = c->pipe_out[i].ensure(sb * row_bytes);
+    e = HIP(c->pipe_in[i].ensure(sb * len));
+    if (e == hipSuccess) e = HIP(c->pipe_out[i].ensure(sb * row_bytes));
+    if (e == hipSuccess && st_in) e = HIP(c->pipe_hin[i].ensure(sb * len));
+    if (e == hipSuccess && st_out) e = HIP(c->pipe_hout[i].ensure(sb * row_bytes));
   }
-  size_t slot = 0;
+  SlotRing ring{c};
+  auto copy_out = [&](size_t b0, size_t cnt, int sl) {  // staged shard rows -> the caller's buffer
+    if (st_out) copy_blocks(shards + b0 * bstride, bstride, c->pipe_hout[sl].as<uint8_t>(), row_bytes, row_bytes, cnt);
+  };
+  int slot = 0;
   for (size_t b0 = 0; e == hipSuccess && b0 < batch; b0 += sb, slot = (slot + 1) % np_ctx::kPipe) {
     const size_t cnt = std::min(sb, batch - b0);
     hipStream_t s = c->pipe_s[slot];
     uint8_t* din = c->pipe_in[slot].as<uint8_t>();
     uint8_t* dout = c->pipe_out[slot].as<uint8_t>();
-    e = hipMemcpy2DAsync(din, len, payloads + b0 * pstride, pstride, len, cnt, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = launch_encode(c, enc_args(p, din, len, len, cnt, dout, row_bytes), s);
+    ring.drain(slot, e, copy_out);  // the slot's staging is free again
+    if (e != hipSuccess) break;
+    if (st_in) {
+      uint8_t* h = c->pipe_hin[slot].as<uint8_t>();
+      copy_blocks(h, len, payloads + b0 * pstride, pstride, len, cnt);
+      e = HIP(hipMemcpyAsync(din, h, cnt * len, hipMemcpyHostToDevice, s));
+    } else {
+      e = HIP(hipMemcpy2DAsync(din, len, payloads + b0 * pstride, pstride, len, cnt, hipMemcpyHostToDevice, s));
+    }
+    e = after(e, s, __LINE__, "payloads H2D");
+    if (e == hipSuccess) e = HIP(launch_encode(c, enc_args(p, din, len, len, cnt, dout, row_bytes), s));
+    e = after(e, s, __LINE__, "encode kernels");
     if (e == hipSuccess)
-      e = hipMemcpy2DAsync(shards + b0 * bstride, bstride, dout, row_bytes, row_bytes, cnt, hipMemcpyDeviceToHost, s);
+      e = st_out ? HIP(hipMemcpyAsync(c->pipe_hout[slot].p, dout, cnt * row_bytes, hipMemcpyDeviceToHost, s))
+                 : HIP(hipMemcpy2DAsync(shards + b0 * bstride, bstride, dout, row_bytes, row_bytes, cnt,
+                                        hipMemcpyDeviceToHost, s));
+    e = after(e, s, __LINE__, "shard rows D2H");
+    if (e == hipSuccess && (st_in || st_out)) e = ring.mark(slot, s, b0, cnt);
   }
-  e = pipe_sync(c, e);
-  if (pinned_in) (void)hipHostUnregister(pinned_in);
-  if (pinned_out) (void)hipHostUnregister(pinned_out);
-  return dev_err(e);
+  // the pending slots, oldest first: `slot` is the next one the loop would
+  // have used, i.e. the one used longest ago
+  for (int i = 0; i < np_ctx::kPipe; ++i) ring.drain((slot + i) % np_ctx::kPipe, e, copy_out);
+  return dev_err(pipe_sync(c, e));
 }
 
 int np_reconstruct_batch_host(np_ctx* c, const np_code_params* p, const uint8_t* shards, size_t shard_len,
@@ -773,109 +957,76 @@ int np_reconstruct_batch_host(np_ctx* c, const np_code_params* p, const uint8_t*
   if (!shards || !out || bstride < p->n * shard_len || out_stride < olen) return fail(NP_ERR_INVALID_ARGUMENT);
   if (batch == 0) return NP_OK;
   // only the rows the kernels read cross PCIe; the device stride stays n rows
-  const size_t rows = rows_needed(p, shard_len, present, batch), in_bytes = rows * shard_len, dstride = p->n * shard_len;
+  const size_t n = p->n, rows = rows_needed(p, shard_len, present, batch), in_bytes = rows * shard_len,
+               dstride = n * shard_len;
   std::lock_guard<std::mutex> g(c->mu);
   (void)hipSetDevice(c->device);
-  // Pinned shards: a kernel reads only the present rows over PCIe (the
-  // gather: 682 of 1024 rows at config 3, 1366 of 4096 at config 4); pageable
-  // ones go by one 2-D DMA of the first `rows` rows of every payload.  The
-  // outputs go by DMA either way (the link shares badly between
-  // kernel reads of host memory and any D2H, but a DMA D2H is the best of it).
-  // (4-byte aligned rows only: k_copy_rows moves 16- or 4-byte pieces there;
-  // other layouts keep the DMA, which any alignment runs at full rate)
-  const bool gather_ok = ((reinterpret_cast<uintptr_t>(shards) | bstride | shard_len) & 3) == 0;
   const size_t span_in = (batch - 1) * bstride + in_bytes, span_out = (batch - 1) * out_stride + olen;
-  const uint8_t* mapped = gather_ok ? mapped_host_range(shards, span_in) : nullptr;
-  // Pageable buffers pinned in place for the call (NP_PAGEABLE=pin): the
-  // gather kernel then reads the present rows of the caller's own shards, and
-  // the outputs go by DMA straight into the caller's buffer
-  void* pinned_in = nullptr;
-  void* pinned_out = nullptr;
-  if (gather_ok && !mapped && !std::getenv("NP_NO_GATHER") && pageable_pin()) {
-    pinned_in = pin_range(shards, span_in);
-    if (pinned_in) mapped = mapped_host_range(shards, span_in);
-    if (mapped && !mapped_host_range(out, span_out)) pinned_out = pin_range(out, span_out);
-  }
-  // Pageable shards of a decode (rows == n): host threads copy the present
-  // rows into pinned staging, from where k_copy_rows gathers them as from
-  // pinned shards; outputs come back through pinned staging as well.  Only
-  // the present rows are read from the caller's memory and cross PCIe.
-  const bool host_gather = !mapped && rows == p->n && !std::getenv("NP_NO_GATHER");
-  // Outputs of the staged pageable path: through pinned staging and host
-  // threads, or (NP_PAGEABLE_OUT=direct) by the runtime's pageable D2H, which
-  // measured slower in the pipeline (profiles/r04_e2e_cfg4.json).
-  const char* pout = std::getenv("NP_PAGEABLE_OUT");
-  const bool staged_out = host_gather && !(pout && std::strcmp(pout, "direct") == 0);
+  const bool may_pin = pageable_pin();
+  const HostSpan hin(shards, span_in, may_pin), hout(out, span_out, may_pin);
+  const bool st_in = !hin.pinned(), st_out = !hout.pinned();
+  // The present rows go by the gather kernel (k_copy_rows: 682 of 1024 rows
+  // cross PCIe at config 3, 1366 of 4096 at config 4) when the rows are 4-byte
+  // aligned in the source (it moves 16- or 4-byte pieces), else the first
+  // `rows` rows of every payload by one 2-D DMA.  The outputs go by DMA either
+  // way (the link shares badly between kernel reads of host
+  // memory and any D2H, but a DMA D2H is the best of it).
+  const bool gather = st_in ? (shard_len & 3) == 0 : ((reinterpret_cast<uintptr_t>(shards) | bstride | shard_len) & 3) == 0;
   hipError_t e = pipe_init(c);
   const size_t sb = std::min(batch, std::max<size_t>(1, kPipeSlotBytes / (in_bytes + olen)));
   const size_t slot_in = (sb - 1) * dstride + in_bytes;
   for (int i = 0; e == hipSuccess && i < np_ctx::kPipe; ++i) {
-    e = c->pipe_in[i].ensure(slot_in);
-    if (e == hipSuccess) e = c->pipe_out[i].ensure(sb * olen);
-    if (host_gather) {
-      if (e == hipSuccess) e = c->pipe_hin[i].ensure(slot_in);
-      if (e == hipSuccess && staged_out) e = c->pipe_hout[i].ensure(sb * olen);
-      if (e == hipSuccess && !c->pipe_ev[i]) e = hipEventCreateWithFlags(&c->pipe_ev[i], hipEventDisableTiming);
-    }
+    e = HIP(c->pipe_in[i].ensure(slot_in));
+    if (e == hipSuccess) e = HIP(c->pipe_out[i].ensure(sb * olen));
+    if (e == hipSuccess && st_in) e = HIP(c->pipe_hin[i].ensure(slot_in));
+    if (e == hipSuccess && st_out) e = HIP(c->pipe_hout[i].ensure(sb * olen));
   }
   const uint8_t* hin_dev[np_ctx::kPipe] = {};
-  for (int i = 0; host_gather && e == hipSuccess && i < np_ctx::kPipe; ++i) {
+  for (int i = 0; st_in && gather && e == hipSuccess && i < np_ctx::kPipe; ++i) {
     hin_dev[i] = mapped_host_range(c->pipe_hin[i].as<uint8_t>(), slot_in);
-    if (!hin_dev[i]) e = hipErrorInvalidValue;  // hipHostMalloc memory is mapped
+    if (!hin_dev[i]) e = HIP(hipErrorInvalidValue);  // hipHostMalloc memory is mapped
   }
-  // pend_cnt[sl]: payloads of slot sl whose pinned staging is still in use
-  // (the gather kernel, and with staged outputs the D2H into pipe_hout)
-  size_t pend_b0[np_ctx::kPipe] = {}, pend_cnt[np_ctx::kPipe] = {};
-  auto drain = [&](int sl) {  // slot sl's staging is free again (its outputs -> the caller's buffer)
-    if (!pend_cnt[sl]) return;
-    const hipError_t r = hipEventSynchronize(c->pipe_ev[sl]);
-    if (e == hipSuccess) e = r;
-    if (r == hipSuccess && staged_out) {
-      const uint8_t* src = c->pipe_hout[sl].as<uint8_t>();
-      const size_t b0 = pend_b0[sl], pieces = (olen + (1u << 20) - 1) >> 20;
-      parallel_for(pend_cnt[sl] * pieces, [&](size_t i) {
-        const size_t b = i / pieces, off = (i % pieces) << 20, len = std::min<size_t>(olen - off, size_t(1) << 20);
-        stream_copy(out + (b0 + b) * out_stride + off, src + b * olen + off, len);
-      });
-    }
-    pend_cnt[sl] = 0;
+  // the whole present mask up front, through pinned staging, before any
+  // sub-batch reads it
+  if (e == hipSuccess) e = HIP(c->pipe_pres.ensure(batch * n));
+  if (e == hipSuccess) e = HIP(c->h_pres.ensure(batch * n));
+  if (e == hipSuccess) {
+    std::memcpy(c->h_pres.p, present, batch * n);
+    e = HIP(hipMemcpyAsync(c->pipe_pres.p, c->h_pres.p, batch * n, hipMemcpyHostToDevice, c->pipe_s[0]));
+  }
+  if (e == hipSuccess) e = HIP(hipStreamSynchronize(c->pipe_s[0]));
+  SlotRing ring{c};
+  auto copy_out = [&](size_t b0, size_t cnt, int sl) {  // staged outputs -> the caller's buffer
+    if (st_out) copy_blocks(out + b0 * out_stride, out_stride, c->pipe_hout[sl].as<uint8_t>(), olen, olen, cnt);
   };
-  // the whole present mask up front, synchronously: from pageable memory an
-  // asynchronous copy per sub-batch would wait for its stream, and with it the
-  // enqueueing of the next sub-batches
-  if (e == hipSuccess) e = c->pipe_pres.ensure(batch * p->n);
-  if (e == hipSuccess) e = hipMemcpy(c->pipe_pres.p, present, batch * p->n, hipMemcpyHostToDevice);
-  size_t slot = 0;
+  int slot = 0;
   for (size_t b0 = 0; e == hipSuccess && b0 < batch; b0 += sb, slot = (slot + 1) % np_ctx::kPipe) {
     const size_t cnt = std::min(sb, batch - b0);
     hipStream_t s = c->pipe_s[slot];
     uint8_t* din = c->pipe_in[slot].as<uint8_t>();
     uint8_t* dout = c->pipe_out[slot].as<uint8_t>();
-    const uint8_t* dpres = c->pipe_pres.as<uint8_t>() + b0 * p->n;
-    if (host_gather) {
-      drain(static_cast<int>(slot));  // the slot's previous sub-batch is done with its staging
-      if (e != hipSuccess) break;
-      uint8_t* hin = c->pipe_hin[slot].as<uint8_t>();
-      const size_t nrows = cnt * p->n;
+    const uint8_t* dpres = c->pipe_pres.as<uint8_t>() + b0 * n;
+    ring.drain(slot, e, copy_out);  // the slot's staging is free again
+    if (e != hipSuccess) break;
+    const uint8_t* src = shards + b0 * bstride;
+    const uint8_t* src_dev = st_in ? hin_dev[slot] : hin.dev() + b0 * bstride;
+    size_t pitch = bstride;
+    if (st_in) {  // host threads copy the present rows among the first `rows` into the slot's staging
+      uint8_t* h = c->pipe_hin[slot].as<uint8_t>();
+      const size_t nrows = cnt * rows;
       parallel_for((nrows + 63) / 64, [&](size_t i) {  // 64 rows per task
         for (size_t r = 64 * i; r < std::min(nrows, 64 * i + 64); ++r) {
-          const size_t b = r / p->n, v = r % p->n;
-          if (present[(b0 + b) * p->n + v])
-            stream_copy(hin + b * dstride + v * shard_len, shards + (b0 + b) * bstride + v * shard_len, shard_len);
+          const size_t b = r / rows, v = r % rows;
+          if (present[(b0 + b) * n + v]) stream_copy(h + b * dstride + v * shard_len, src + b * bstride + v * shard_len, shard_len);
         }
       });
-      e = np::launch_copy_rows(hin_dev[slot], dstride, din, dstride, shard_len, dpres, static_cast<uint32_t>(p->n),
-                               static_cast<uint32_t>(rows), cnt, kGatherBlocks, s);
-      if (!staged_out) {  // the input staging is free once the gather kernel is done
-        if (e == hipSuccess) e = hipEventRecord(c->pipe_ev[slot], s);
-        if (e == hipSuccess) pend_b0[slot] = b0, pend_cnt[slot] = cnt;
-      }
-    } else {
-    e = mapped ? np::launch_copy_rows(mapped + b0 * bstride, bstride, din, dstride, shard_len, dpres,
-                                      static_cast<uint32_t>(p->n), static_cast<uint32_t>(rows), cnt, kGatherBlocks, s)
-               : hipMemcpy2DAsync(din, dstride, shards + b0 * bstride, bstride, in_bytes, cnt, hipMemcpyHostToDevice,
-                                  s);
+      src = h;
+      pitch = dstride;
     }
+    e = gather ? HIP(np::launch_copy_rows(src_dev, pitch, din, dstride, shard_len, dpres, static_cast<uint32_t>(n),
+                                          static_cast<uint32_t>(rows), cnt, kGatherBlocks, s))
+               : HIP(hipMemcpy2DAsync(din, dstride, src, pitch, in_bytes, cnt, hipMemcpyHostToDevice, s));
+    e = after(e, s, __LINE__, gather ? "present-row gather" : "shard rows H2D");
     if (e == hipSuccess) {
       np::ReconstructArgs a{};
       a.shards = din;
@@ -884,27 +1035,23 @@ int np_reconstruct_batch_host(np_ctx* c, const np_code_params* p, const uint8_t*
       a.present = dpres;
       a.locators = nullptr;  // computed on the device
       a.batch = cnt;
-      a.n = static_cast<uint32_t>(p->n);
+      a.n = static_cast<uint32_t>(n);
       a.k = static_cast<uint32_t>(p->k);
       a.out = dout;
       a.out_stride = olen;
-      e = launch_reconstruct(c, a, s);
+      e = HIP(launch_reconstruct(c, a, s));
     }
-    if (staged_out) {
-      if (e == hipSuccess)
-        e = hipMemcpyAsync(c->pipe_hout[slot].p, dout, cnt * olen, hipMemcpyDeviceToHost, s);
-      if (e == hipSuccess) e = hipEventRecord(c->pipe_ev[slot], s);
-      if (e == hipSuccess) pend_b0[slot] = b0, pend_cnt[slot] = cnt;
-    } else if (e == hipSuccess) {
-      e = hipMemcpy2DAsync(out + b0 * out_stride, out_stride, dout, olen, olen, cnt, hipMemcpyDeviceToHost, s);
-    }
+    e = after(e, s, __LINE__, "reconstruct kernels");
+    if (e == hipSuccess)
+      e = st_out ? HIP(hipMemcpyAsync(c->pipe_hout[slot].p, dout, cnt * olen, hipMemcpyDeviceToHost, s))
+                 : HIP(hipMemcpy2DAsync(out + b0 * out_stride, out_stride, dout, olen, olen, cnt,
+                                        hipMemcpyDeviceToHost, s));
+    e = after(e, s, __LINE__, "outputs D2H");
+    if (e == hipSuccess && (st_in || st_out)) e = ring.mark(slot, s, b0, cnt);
   }
-  // the remaining slots in submission order (a failed call still waits for its streams)
-  for (size_t i = 1; host_gather && i <= np_ctx::kPipe; ++i) drain(static_cast<int>((slot + i) % np_ctx::kPipe));
-  e = pipe_sync(c, e);
-  if (pinned_in) (void)hipHostUnregister(pinned_in);
-  if (pinned_out) (void)hipHostUnregister(pinned_out);
-  return dev_err(e);
+  // the pending slots, oldest first (a failed call still waits for its streams)
+  for (int i = 0; i < np_ctx::kPipe; ++i) ring.drain((slot + i) % np_ctx::kPipe, e, copy_out);
+  return dev_err(pipe_sync(c, e));
 }
 
 // ---------------------------------------------------------- reconstruct ----
@@ -912,7 +1059,7 @@ int np_error_locator_dev(np_ctx* c, size_t n, const uint8_t* d_present, size_t b
                          void* stream) {
   if (!c || !d_present || !d_loc || !is_pow2(n) || n > np::kFieldSize) return fail(NP_ERR_INVALID_ARGUMENT);
   (void)hipSetDevice(c->device);
-  return dev_err(np::launch_error_locator(c->T, static_cast<uint32_t>(n), d_present, batch, d_loc, pick(c, stream)));
+  return dev_err(HIP(np::launch_error_locator(c->T, static_cast<uint32_t>(n), d_present, batch, d_loc, pick(c, stream))));
 }
 
 namespace {
@@ -942,7 +1089,7 @@ int reconstruct_dev2(np_ctx* c, const np_code_params* p, const uint8_t* d_shards
   a.out_stride = out_stride;
   a.status = reinterpret_cast<uint32_t*>(d_status);
   a.trusted = trusted;
-  return dev_err(launch_reconstruct(c, a, pick(c, stream)));
+  return dev_err(HIP(launch_reconstruct(c, a, pick(c, stream))));
 }
 
 }  // namespace
@@ -988,9 +1135,12 @@ int np_reconstruct_batch_dev(np_ctx* c, const np_code_params* p, const uint8_t* 
   if (shard_len == 0 || (shard_len & 1)) return fail(NP_ERR_EMPTY_SHARD);
   if (!d_shards || !d_out || bstride < p->n * shard_len || out_stride < (shard_len / 2) * 2 * p->k)
     return fail(NP_ERR_INVALID_ARGUMENT);
-  hipError_t e = c->d_present.ensure(std::max<size_t>(batch * p->n, 1));
+  // the present mask through pinned staging (no pageable pointer reaches a HIP copy, §4.7)
+  hipError_t e = HIP(c->d_present.ensure(std::max<size_t>(batch * p->n, 1)));
+  if (e == hipSuccess) e = HIP(c->h_pres.ensure(std::max<size_t>(batch * p->n, 1)));
   if (e != hipSuccess) return dev_err(e);
-  e = hipMemcpyAsync(c->d_present.p, present, batch * p->n, hipMemcpyHostToDevice, s);
+  std::memcpy(c->h_pres.p, present, batch * p->n);
+  e = HIP(hipMemcpyAsync(c->d_present.p, c->h_pres.p, batch * p->n, hipMemcpyHostToDevice, s));
   if (e != hipSuccess) return dev_err(e);
   np::ReconstructArgs a{};
   a.shards = d_shards;
@@ -1003,11 +1153,11 @@ int np_reconstruct_batch_dev(np_ctx* c, const np_code_params* p, const uint8_t* 
   a.k = static_cast<uint32_t>(p->k);
   a.out = d_out;
   a.out_stride = out_stride;
-  e = launch_reconstruct(c, a, s);
+  e = HIP(launch_reconstruct(c, a, s));
   if (e != hipSuccess) return dev_err(e);
-  // present mask was copied from pageable host memory: make the call
-  // synchronous with respect to it before returning.
-  return dev_err(hipStreamSynchronize(s));
+  // the staged present mask is the context's: the call returns once the
+  // stream is done with it
+  return dev_err(HIP(hipStreamSynchronize(s)));
 }
 
 int np_rs_reconstruct(np_ctx* c, const np_code_params* p, const uint8_t* const* shards, const size_t* lens,
@@ -1037,12 +1187,14 @@ int np_rs_reconstruct(np_ctx* c, const np_code_params* p, const uint8_t* const* 
   const size_t sl = 2 * syms;
   std::lock_guard<std::mutex> g(c->mu);
   (void)hipSetDevice(c->device);
-  hipError_t e = c->h_in.ensure(n * sl);
-  if (e == hipSuccess) e = c->d_in.ensure(n * sl);
-  if (e == hipSuccess) e = c->d_out.ensure(need);
-  if (e == hipSuccess) e = c->h_out.ensure(need);
-  if (e == hipSuccess) e = c->d_present.ensure(n);
+  hipError_t e = HIP(c->h_in.ensure(n * sl));
+  if (e == hipSuccess) e = HIP(c->d_in.ensure(n * sl));
+  if (e == hipSuccess) e = HIP(c->d_out.ensure(need));
+  if (e == hipSuccess) e = HIP(c->h_out.ensure(need));
+  if (e == hipSuccess) e = HIP(c->d_present.ensure(n));
+  if (e == hipSuccess) e = HIP(c->h_pres.ensure(n));
   if (e != hipSuccess) return dev_err(e);
+  std::memcpy(c->h_pres.p, present.data(), n);
   uint8_t* stage = c->h_in.as<uint8_t>();
   for (size_t i = 0; i < n; ++i) {
     uint8_t* row = stage + i * sl;
@@ -1054,8 +1206,8 @@ int np_rs_reconstruct(np_ctx* c, const np_code_params* p, const uint8_t* const* 
     }
   }
   hipStream_t s = c->stream;
-  e = hipMemcpyAsync(c->d_in.p, stage, n * sl, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(c->d_present.p, present.data(), n, hipMemcpyHostToDevice, s);
+  e = HIP(hipMemcpyAsync(c->d_in.p, stage, n * sl, hipMemcpyHostToDevice, s));
+  if (e == hipSuccess) e = HIP(hipMemcpyAsync(c->d_present.p, c->h_pres.p, n, hipMemcpyHostToDevice, s));
   if (e == hipSuccess) {
     np::ReconstructArgs a{};
     a.shards = c->d_in.as<uint8_t>();
@@ -1068,10 +1220,10 @@ int np_rs_reconstruct(np_ctx* c, const np_code_params* p, const uint8_t* const* 
     a.k = static_cast<uint32_t>(k);
     a.out = c->d_out.as<uint8_t>();
     a.out_stride = need;
-    e = launch_reconstruct(c, a, s);
+    e = HIP(launch_reconstruct(c, a, s));
   }
-  if (e == hipSuccess) e = hipMemcpyAsync(c->h_out.p, c->d_out.p, need, hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess) e = HIP(hipMemcpyAsync(c->h_out.p, c->d_out.p, need, hipMemcpyDeviceToHost, s));
+  if (e == hipSuccess) e = HIP(hipStreamSynchronize(s));
   if (e != hipSuccess) return dev_err(e);
   std::memcpy(out, c->h_out.p, need);
   *out_len = need;
@@ -1103,10 +1255,10 @@ int np_rs_reconstruct_from_systematic(np_ctx* c, const np_code_params* p, const 
   if (!out || !out_len || cap < need) return fail(NP_ERR_INVALID_ARGUMENT, need);
   std::lock_guard<std::mutex> g(c->mu);
   (void)hipSetDevice(c->device);
-  hipError_t e = c->h_in.ensure(k * sl);
-  if (e == hipSuccess) e = c->d_in.ensure(k * sl);
-  if (e == hipSuccess) e = c->d_out.ensure(need);
-  if (e == hipSuccess) e = c->h_out.ensure(need);
+  hipError_t e = HIP(c->h_in.ensure(k * sl));
+  if (e == hipSuccess) e = HIP(c->d_in.ensure(k * sl));
+  if (e == hipSuccess) e = HIP(c->d_out.ensure(need));
+  if (e == hipSuccess) e = HIP(c->h_out.ensure(need));
   if (e != hipSuccess) return dev_err(e);
   uint8_t* stage = c->h_in.as<uint8_t>();
   for (size_t j = 0; j < k; ++j) {
@@ -1114,11 +1266,11 @@ int np_rs_reconstruct_from_systematic(np_ctx* c, const np_code_params* p, const 
     if (lens[j] < sl) std::memset(stage + j * sl + lens[j], 0, sl - lens[j]);  // WrappedShard zero pad
   }
   hipStream_t s = c->stream;
-  e = hipMemcpyAsync(c->d_in.p, stage, k * sl, hipMemcpyHostToDevice, s);
+  e = HIP(hipMemcpyAsync(c->d_in.p, stage, k * sl, hipMemcpyHostToDevice, s));
   if (e == hipSuccess) e = np::launch_systematic(c->d_in.as<uint8_t>(), sl, k * sl, static_cast<uint32_t>(k), 1,
                                                  c->d_out.as<uint8_t>(), need, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(c->h_out.p, c->d_out.p, need, hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess) e = HIP(hipMemcpyAsync(c->h_out.p, c->d_out.p, need, hipMemcpyDeviceToHost, s));
+  if (e == hipSuccess) e = HIP(hipStreamSynchronize(s));
   if (e != hipSuccess) return dev_err(e);
   std::memcpy(out, c->h_out.p, need);
   *out_len = need;
@@ -1135,8 +1287,8 @@ int np_reconstruct_from_systematic_batch_dev(np_ctx* c, const np_code_params* p,
   if (!d_shards || !d_out || bstride < p->k * shard_len || out_stride < (shard_len / 2) * 2 * p->k)
     return fail(NP_ERR_INVALID_ARGUMENT);
   (void)hipSetDevice(c->device);
-  return dev_err(np::launch_systematic(d_shards, shard_len, bstride, static_cast<uint32_t>(p->k), batch, d_out,
-                                       out_stride, pick(c, stream)));
+  return dev_err(HIP(np::launch_systematic(d_shards, shard_len, bstride, static_cast<uint32_t>(p->k), batch, d_out,
+                                       out_stride, pick(c, stream))));
 }
 
 // ------------------------------------------------------------ multi-GPU ----
@@ -1217,6 +1369,13 @@ int np_encode_batch_host_multi(np_ctx* const* ctxs, size_t nctx, const np_code_p
                                size_t len, size_t pstride, size_t batch, uint8_t* shards, size_t bstride) {
   if (!payloads || !shards) return fail(NP_ERR_INVALID_ARGUMENT);
   if (int st = check_params(p)) return st;
+  // Pageable spans pinned once for all devices' ranges: the
+  // workers' spans then lie inside one registration, and adjacent ranges that
+  // share a page never register or unregister it under each other's copies.
+  const size_t sl = np_shard_len(p, len), row_bytes = p->wanted_n * sl;
+  const bool whole = batch && len && pstride >= len && bstride >= row_bytes && pageable_pin();
+  const HostSpan hin(payloads, whole ? (batch - 1) * pstride + len : 0, whole),
+      hout(shards, whole ? (batch - 1) * bstride + row_bytes : 0, whole);
   return run_multi(ctxs, nctx, batch, [&](size_t i, size_t b0, size_t cnt) {
     return np_encode_batch_host(ctxs[i], p, payloads + b0 * pstride, len, pstride, cnt, shards + b0 * bstride,
                                 bstride);
@@ -1228,6 +1387,14 @@ int np_reconstruct_batch_host_multi(np_ctx* const* ctxs, size_t nctx, const np_c
                                     size_t batch, uint8_t* out, size_t out_stride) {
   if (!shards || !present || !out || !p) return fail(NP_ERR_INVALID_ARGUMENT);
   if (int st = check_params(p)) return st;
+  // pinned once for all ranges, as in np_encode_batch_host_multi; a worker
+  // ships at most the rows the whole batch needs
+  const size_t olen = (shard_len / 2) * 2 * p->k;
+  const bool whole = batch && shard_len && !(shard_len & 1) && bstride >= p->n * shard_len && out_stride >= olen &&
+                     pageable_pin();
+  const size_t rows = whole ? rows_needed(p, shard_len, present, batch) : 0;
+  const HostSpan hin(shards, whole ? (batch - 1) * bstride + rows * shard_len : 0, whole),
+      hout(out, whole ? (batch - 1) * out_stride + olen : 0, whole);
   return run_multi(ctxs, nctx, batch, [&](size_t i, size_t b0, size_t cnt) {
     return np_reconstruct_batch_host(ctxs[i], p, shards + b0 * bstride, shard_len, bstride, present + b0 * p->n,
                                      cnt, out + b0 * out_stride, out_stride);
@@ -1239,36 +1406,36 @@ int np_afft_dev(np_ctx* c, uint16_t* d, size_t size, size_t index, size_t cols, 
   if (!c || !d || !is_pow2(size) || size > np::kFieldSize || index + size > np::kFieldSize)
     return fail(NP_ERR_INVALID_ARGUMENT);
   (void)hipSetDevice(c->device);
-  return dev_err(np::launch_afft(c->T, d, static_cast<uint32_t>(size), static_cast<uint32_t>(index), cols, false,
-                                 pick(c, stream)));
+  return dev_err(HIP(np::launch_afft(c->T, d, static_cast<uint32_t>(size), static_cast<uint32_t>(index), cols, false,
+                                 pick(c, stream))));
 }
 
 int np_inverse_afft_dev(np_ctx* c, uint16_t* d, size_t size, size_t index, size_t cols, void* stream) {
   if (!c || !d || !is_pow2(size) || size > np::kFieldSize || index + size > np::kFieldSize)
     return fail(NP_ERR_INVALID_ARGUMENT);
   (void)hipSetDevice(c->device);
-  return dev_err(np::launch_afft(c->T, d, static_cast<uint32_t>(size), static_cast<uint32_t>(index), cols, true,
-                                 pick(c, stream)));
+  return dev_err(HIP(np::launch_afft(c->T, d, static_cast<uint32_t>(size), static_cast<uint32_t>(index), cols, true,
+                                 pick(c, stream))));
 }
 
 int np_walsh_dev(np_ctx* c, uint16_t* d, size_t size, void* stream) {
   if (!c || !d || !is_pow2(size) || size > np::kFieldSize) return fail(NP_ERR_INVALID_ARGUMENT);
   (void)hipSetDevice(c->device);
-  return dev_err(np::launch_walsh(d, static_cast<uint32_t>(size), pick(c, stream)));
+  return dev_err(HIP(np::launch_walsh(d, static_cast<uint32_t>(size), pick(c, stream))));
 }
 
 int np_mul_dev(np_ctx* c, const uint16_t* a, const uint16_t* m, uint16_t* o, size_t count, void* stream) {
   if (!c || !a || !m || !o) return fail(NP_ERR_INVALID_ARGUMENT);
   (void)hipSetDevice(c->device);
-  return dev_err(np::launch_mul(c->T, a, m, o, count, pick(c, stream)));
+  return dev_err(HIP(np::launch_mul(c->T, a, m, o, count, pick(c, stream))));
 }
 
 int np_encode_low_dev(np_ctx* c, const uint16_t* d, size_t k, uint16_t* cw, size_t n, size_t cols, void* stream) {
   if (!c || !d || !cw || !is_pow2(n) || !is_pow2(k) || 2 * k > n || n > np::kFieldSize)
     return fail(NP_ERR_INVALID_ARGUMENT);
   (void)hipSetDevice(c->device);
-  return dev_err(
-      np::launch_encode_low(c->T, d, static_cast<uint32_t>(k), cw, static_cast<uint32_t>(n), cols, pick(c, stream)));
+  return dev_err(HIP(
+      np::launch_encode_low(c->T, d, static_cast<uint32_t>(k), cw, static_cast<uint32_t>(n), cols, pick(c, stream))));
 }
 
 int np_decode_main_dev(np_ctx* c, uint16_t* cw, size_t upto, const uint8_t* d_present, const uint16_t* d_loc,
@@ -1276,8 +1443,8 @@ int np_decode_main_dev(np_ctx* c, uint16_t* cw, size_t upto, const uint8_t* d_pr
   if (!c || !cw || !d_present || !d_loc || !is_pow2(n) || n > np::kFieldSize || upto > n)
     return fail(NP_ERR_INVALID_ARGUMENT);
   (void)hipSetDevice(c->device);
-  return dev_err(np::launch_decode_main(c->T, cw, static_cast<uint32_t>(upto), d_present, d_loc,
-                                        static_cast<uint32_t>(n), cols, pick(c, stream)));
+  return dev_err(HIP(np::launch_decode_main(c->T, cw, static_cast<uint32_t>(upto), d_present, d_loc,
+                                        static_cast<uint32_t>(n), cols, pick(c, stream))));
 }
 
 }  // extern "C"

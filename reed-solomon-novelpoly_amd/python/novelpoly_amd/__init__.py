@@ -48,6 +48,7 @@ def lib() -> C.CDLL:
         vp = C.c_void_p
         sig = {
             "np_last_error_detail": (None, [C.POINTER(_sz)]),
+            "np_last_error_site": (C.c_char_p, []),
             "np_status_message": (C.c_char_p, [C.c_int]),
             "np_version": (C.c_char_p, []),
             "np_recoverability_subset_size": (_sz, [_sz]),
@@ -185,6 +186,8 @@ def _raise(st: int):
     cls = _BY_CODE.get(st)
     if cls is None:
         msg = lib().np_status_message(st).decode()
+        if st in (DeviceError.code, 102):  # NP_ERR_DEVICE / NP_ERR_ALLOC: the failing HIP call
+            msg += f" [{lib().np_last_error_site().decode()}]"
         raise DeviceError(st, msg)
     raise cls(*tuple(det)[: _ARITY.get(st, 3)])
 

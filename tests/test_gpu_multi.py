@@ -80,6 +80,42 @@ def test_host_batch_multi(gpu, oracle):
         assert out[b, :plen].tobytes() == pay[b].tobytes()
 
 
+@pytest.mark.parametrize("nctx", [2, 3])
+def test_host_batch_multi_pageable_unaligned_split(gpu, oracle, nctx):
+    """the ranges of a host multi call are adjacent slices of one
+    pageable caller buffer, and with a row stride that is no multiple of the
+    page size neighbouring ranges share a page.  The engine pins the whole
+    spans once before the worker threads start (engine.cpp
+    np_*_batch_host_multi, PinRegistry), so no worker registers or
+    unregisters a page under another's copies.  Guard bytes around every
+    buffer; every payload against the oracle."""
+    ctxs = [npa.Context(0) for _ in range(nctx)]
+    p = npa.CodeParams.derive_parameters(1024, 342)
+    n, k = p.n(), p.k()
+    plen, batch = 512 * 101 + 3, 7  # shard_len 204
+    sl = p.make_encoder(gpu).shard_len(plen)
+    bstride, ostride, g = n * sl + 100, (sl // 2) * 2 * k + 37, 4096 + 5
+    pay = np.stack([np.frombuffer(synth.payload(950 + b, plen), np.uint8) for b in range(batch)])
+    sh_b = np.full(batch * bstride + 2 * g, 0xC3, np.uint8)
+    sh = sh_b[g:g + batch * bstride].reshape(batch, bstride)
+    sh[...] = 0
+    npa.encode_batch_host_multi(ctxs, p, pay.ctypes.data, plen, plen, batch, sh.ctypes.data, bstride)
+    pres = np.stack([synth.present_mask(950 + b, n, 342) for b in range(batch)])
+    out_b = np.full(batch * ostride + 2 * g, 0xC3, np.uint8)
+    out = out_b[g:g + batch * ostride].reshape(batch, ostride)
+    npa.reconstruct_batch_host_multi(ctxs, p, sh.ctypes.data, sl, bstride, pres.ctypes.data, batch, out.ctypes.data,
+                                     ostride)
+    for base in (sh_b, out_b):
+        assert (base[:g] == 0xC3).all() and (base[-g:] == 0xC3).all()
+    olen = (sl // 2) * 2 * k
+    for b in range(batch):
+        st, want = oracle.encode(pay[b].tobytes(), n, k, n)
+        assert st == 0 and sh[b, :n * sl].tobytes() == b"".join(want), b
+        st, rec = oracle.reconstruct([sh[b, i * sl:(i + 1) * sl].tobytes() if pres[b, i] else None for i in range(n)],
+                                     n, k)
+        assert st == 0 and out[b, :olen].tobytes() == rec, b
+
+
 def test_multi_reports_need_more_shards(gpu):
     """A host-memory multi call fails like the crate (NeedMoreShards) when one
     range holds a payload with fewer than k present shards."""

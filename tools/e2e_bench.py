@@ -62,25 +62,17 @@ def rec():
     npa.reconstruct_batch_host(p, h_sh.data_ptr(), sl, n * sl, pres.ctypes.data, B, h_out.data_ptr(), olen, ctx=ctx)
 
 
-# pinned shards: the engine gathers the present rows with a kernel reading
-# mapped host memory; NP_NO_GATHER=1 forces the pageable-memory path (one 2-D
-# DMA of the first rows_needed rows of every payload) for comparison
-os.environ["NP_NO_GATHER"] = "1"
-t_dma = timed(rec)
-ok_dma = torch.equal(h_out[:, :plen], h_pay)
-del os.environ["NP_NO_GATHER"]
 h_out.zero_()
 t_rec = timed(rec)
-ok = torch.equal(h_out[:, :plen], h_pay) and ok_dma
+ok = torch.equal(h_out[:, :plen], h_pay)
 # bytes crossing PCIe: encode P in + n*sl out; reconstruct the rows the engine
 # reads (engine.cpp rows_needed: the k systematic rows when every payload of the
 # batch has them all, else all n rows), of those only the present ones on the
-# gather path, (+ flags) in, and 2k*sl/2 out
-# pageable shards and output (numpy).  Default (NP_PAGEABLE=pin): the engine
-# pins them in place for the call (hipHostRegister) and goes as from pinned
-# memory; NP_PAGEABLE=gather: host threads copy the present rows into pinned
-# staging (engine.cpp host_gather), outputs back through pinned staging;
-# NP_NO_GATHER=1: the runtime's pageable 2-D DMA of every row (rounds 1-3)
+# gather path, (+ flags) in, and 2k*sl/2 out.
+# Pageable shards and output (numpy).  Default (NP_PAGEABLE=pin): the engine
+# pins them in place for the call (PinRegistry) and goes as from pinned
+# memory; NP_PAGEABLE=stage: host threads copy the present rows into pinned
+# staging and the outputs back out of it (engine.cpp, host-memory pipeline).
 pg_sh = h_sh.numpy().copy()
 pg_out = np.zeros((B, olen), dtype=np.uint8)
 pg_pay = h_pay.numpy().copy()
@@ -92,23 +84,47 @@ def rec_pageable():
                                ctx=ctx)
 
 
-t_enc_pg = timed(lambda: npa.encode_batch_host(p, pg_pay.ctypes.data, plen, plen, B, pg_enc.ctypes.data, n * sl,
-                                               ctx=ctx))
+def enc_pageable():
+    npa.encode_batch_host(p, pg_pay.ctypes.data, plen, plen, B, pg_enc.ctypes.data, n * sl, ctx=ctx)
+
+
 wb = p.wanted_n * sl  # the rows encode writes
+t_enc_pg = timed(enc_pageable)
 ok_pg = bool((pg_enc[:, :wb] == h_sh.numpy().reshape(B, -1)[:, :wb]).all())
 t_pg = timed(rec_pageable)
 ok_pg = ok_pg and bool((pg_out[:, :plen] == h_pay.numpy()).all())
 pg_out[:] = 0
-os.environ["NP_PAGEABLE"] = "gather"
+pg_enc[:] = 0
+os.environ["NP_PAGEABLE"] = "stage"
 t_pg_st = timed(rec_pageable)
+t_enc_st = timed(enc_pageable)
 del os.environ["NP_PAGEABLE"]
 ok_pg = ok_pg and bool((pg_out[:, :plen] == h_pay.numpy()).all())
-pg_out[:] = 0
-os.environ["NP_NO_GATHER"] = "1"
-t_pg_dma = timed(rec_pageable)
-del os.environ["NP_NO_GATHER"]
-ok_pg = ok_pg and bool((pg_out[:, :plen] == h_pay.numpy()).all())
+ok_pg = ok_pg and bool((pg_enc[:, :wb] == h_sh.numpy().reshape(B, -1)[:, :wb]).all())
 ok = ok and ok_pg
+
+
+# one payload per call (small calls pay no registration below 1 MiB)
+def one_call_ms(fn, reps=20):
+    fn()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    return round((time.perf_counter() - t0) / reps * 1e3, 3)
+
+
+lat = {
+    "encode_pinned_ms": one_call_ms(lambda: npa.encode_batch_host(p, h_pay.data_ptr(), plen, plen, 1, h_sh.data_ptr(),
+                                                                  n * sl, ctx=ctx)),
+    "encode_pageable_ms": one_call_ms(lambda: npa.encode_batch_host(p, pg_pay.ctypes.data, plen, plen, 1,
+                                                                    pg_enc.ctypes.data, n * sl, ctx=ctx)),
+    "reconstruct_pinned_ms": one_call_ms(lambda: npa.reconstruct_batch_host(p, h_sh.data_ptr(), sl, n * sl,
+                                                                            pres.ctypes.data, 1, h_out.data_ptr(),
+                                                                            olen, ctx=ctx)),
+    "reconstruct_pageable_ms": one_call_ms(lambda: npa.reconstruct_batch_host(p, pg_sh.ctypes.data, sl, n * sl,
+                                                                              pres.ctypes.data, 1, pg_out.ctypes.data,
+                                                                              olen, ctx=ctx)),
+}
 rows_dma = k if all(pres[b, :k].all() for b in range(B)) else n
 rows = float(pres[:, :rows_dma].sum()) / B
 res = {
@@ -121,15 +137,13 @@ res = {
                     # the two directions one after the other: kernel reads of host memory and a
                     # concurrent D2H share the link badly (tools/microbench/h2d_gather.hip)
                     "pcie_serial_bound_GiB_s": round(B * plen / (B * rows * sl / (bw_h2d * 1e9) + B * olen / (bw_d2h * 1e9)) / 2**30, 2)},
-    "reconstruct_dma": {"GiB_s": round(B * plen / t_dma / 2**30, 2), "ms": round(t_dma * 1e3, 2), "rows_copied": rows_dma,
-                        "pcie_bound_GiB_s": round(B * plen / max(B * rows_dma * sl / (bw_h2d * 1e9), B * olen / (bw_d2h * 1e9)) / 2**30, 2)},
     "encode_pageable_pinned_in_place": {"GiB_s": round(B * plen / t_enc_pg / 2**30, 2), "ms": round(t_enc_pg * 1e3, 2)},
     "reconstruct_pageable_pinned_in_place": {"GiB_s": round(B * plen / t_pg / 2**30, 2), "ms": round(t_pg * 1e3, 2),
                                              "rows_copied": rows},
-    "reconstruct_pageable_host_gather": {"GiB_s": round(B * plen / t_pg_st / 2**30, 2), "ms": round(t_pg_st * 1e3, 2),
-                                         "rows_copied": rows, "host_threads": min(16, os.cpu_count() or 1)},
-    "reconstruct_pageable_all_rows_dma": {"GiB_s": round(B * plen / t_pg_dma / 2**30, 2),
-                                          "ms": round(t_pg_dma * 1e3, 2), "rows_copied": rows_dma},
+    "reconstruct_pageable_staged": {"GiB_s": round(B * plen / t_pg_st / 2**30, 2), "ms": round(t_pg_st * 1e3, 2),
+                                    "rows_copied": rows, "host_threads": min(16, os.cpu_count() or 1)},
+    "encode_pageable_staged": {"GiB_s": round(B * plen / t_enc_st / 2**30, 2), "ms": round(t_enc_st * 1e3, 2)},
+    "one_payload_call": lat,
     "roundtrip_ok": bool(ok),
 }
 print(json.dumps(res))
