@@ -250,54 +250,7 @@ __device__ __forceinline__ Mult staged_mult(const uint32_t (&sp)[12], const uint
 }
 
 // x ^= c*y on four byte-planar symbols (pool layout: field_tables.cpp).
-#ifndef NP_QMUL_MERGED
-#define NP_QMUL_MERGED 0
-#endif
-// One output plane: acc ^= XOR of the 6 lookups of both input planes (asm
-// fragment of a merged quad multiply; operands named as in qmul_merged).
-#define NP_QPLANE_ASM(ACC, VA, VB, VC, VD, SA, SB, SC, SD, SE, SF)                                    \
-  "v_perm_b32 %[t0], %[" SA "], %[" VA "], %[s0]\n\t"                                               \
-  "v_perm_b32 %[t1], %[" SB "], %[" VB "], %[s1]\n\t"                                               \
-  "v_perm_b32 %[t2], %[" SC "], %[" SC "], %[s2]\n\t"                                               \
-  "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t"                                         \
-  "v_perm_b32 %[t1], %[" SD "], %[" VC "], %[s3]\n\t"                                               \
-  "v_perm_b32 %[t2], %[" SE "], %[" VD "], %[s4]\n\t"                                               \
-  "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t"                                         \
-  "v_perm_b32 %[t1], %[" SF "], %[" SF "], %[s5]\n\t"                                               \
-  "v_bitop3_b32 %[" ACC "], %[" ACC "], %[t0], %[t1] bitop3:0x96\n\t"
-
-// The selectors of both planes (32-bit shifts: one asm block per multiply,
-// no hazard s_nop between the pieces of a multiply).
-#define NP_SEL_ASM                                   \
-  "v_and_b32 %[s0], 0x07070707, %[yl]\n\t"          \
-  "v_lshrrev_b32 %[s1], 3, %[yl]\n\t"               \
-  "v_lshrrev_b32 %[s2], 6, %[yl]\n\t"               \
-  "v_and_b32 %[s3], 0x07070707, %[yh]\n\t"          \
-  "v_lshrrev_b32 %[s4], 3, %[yh]\n\t"               \
-  "v_lshrrev_b32 %[s5], 6, %[yh]\n\t"               \
-  "v_and_b32 %[s1], 0x07070707, %[s1]\n\t"          \
-  "v_and_b32 %[s2], 0x03030303, %[s2]\n\t"          \
-  "v_and_b32 %[s4], 0x07070707, %[s4]\n\t"          \
-  "v_and_b32 %[s5], 0x03030303, %[s5]\n\t"
-
-__device__ __forceinline__ void qmul_merged(uint32_t& xl, uint32_t& xh, uint32_t yl, uint32_t yh, const Mult& m) {
-  uint32_t s0, s1, s2, s3, s4, s5, t0, t1, t2;
-  asm volatile(NP_SEL_ASM NP_QPLANE_ASM("xl", "v0", "v1", "v2", "v3", "a0", "a1", "a2", "a3", "a4", "a5")
-                   NP_QPLANE_ASM("xh", "v4", "v5", "v6", "v7", "a6", "a7", "a8", "a9", "a10", "a11")
-               : [xl] "+v"(xl), [xh] "+v"(xh), [s0] "=&v"(s0), [s1] "=&v"(s1), [s2] "=&v"(s2), [s3] "=&v"(s3),
-                 [s4] "=&v"(s4), [s5] "=&v"(s5), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2)
-               : [yl] "v"(yl), [yh] "v"(yh), [v0] "v"(m.v[0]), [v1] "v"(m.v[1]), [v2] "v"(m.v[2]),
-                 [v3] "v"(m.v[3]), [v4] "v"(m.v[4]), [v5] "v"(m.v[5]), [v6] "v"(m.v[6]), [v7] "v"(m.v[7]),
-                 [a0] "s"(m.s[0]), [a1] "s"(m.s[1]), [a2] "s"(m.s[2]), [a3] "s"(m.s[3]), [a4] "s"(m.s[4]),
-                 [a5] "s"(m.s[5]), [a6] "s"(m.s[6]), [a7] "s"(m.s[7]), [a8] "s"(m.s[8]), [a9] "s"(m.s[9]),
-                 [a10] "s"(m.s[10]), [a11] "s"(m.s[11]));
-}
-
 __device__ __forceinline__ void qmul(uint32_t& xl, uint32_t& xh, uint32_t yl, uint32_t yh, const Mult& m) {
-  if constexpr (NP_QMUL_MERGED) {
-    qmul_merged(xl, xh, yl, yh, m);
-    return;
-  }
   uint32_t s[6];
   selectors(yl, yh, s);
   qplane(xl, s, m.v[0], m.v[1], m.v[2], m.v[3], m.s[0], m.s[1], m.s[2], m.s[3], m.s[4], m.s[5]);
@@ -347,27 +300,6 @@ __device__ __forceinline__ void qplane_sub_set(uint32_t& out, uint32_t s0, uint3
 
 // x ^= c*y, c in GF(2^8), tower coordinates.
 __device__ __forceinline__ void qmul_sub(uint32_t& xl, uint32_t& xh, uint32_t yl, uint32_t yh, const Mult& m) {
-  if constexpr (NP_QMUL_MERGED) {
-    // one asm block; both planes read the a-plane tables (equal to the b-plane
-    // ones: field_tables.hpp, e_i = beta_i)
-    uint32_t s0, s1, s2, s3, s4, s5, t0, t1, t2;
-    asm volatile(NP_SEL_ASM
-                 "v_perm_b32 %[t0], %[sa], %[va], %[s0]\n\t"
-                 "v_perm_b32 %[t1], %[sb], %[vb], %[s1]\n\t"
-                 "v_perm_b32 %[t2], %[sc], %[sc], %[s2]\n\t"
-                 "v_bitop3_b32 %[xl], %[xl], %[t0], %[t1] bitop3:0x96\n\t"
-                 "v_xor_b32 %[xl], %[xl], %[t2]\n\t"
-                 "v_perm_b32 %[t0], %[sa], %[va], %[s3]\n\t"
-                 "v_perm_b32 %[t1], %[sb], %[vb], %[s4]\n\t"
-                 "v_perm_b32 %[t2], %[sc], %[sc], %[s5]\n\t"
-                 "v_bitop3_b32 %[xh], %[xh], %[t0], %[t1] bitop3:0x96\n\t"
-                 "v_xor_b32 %[xh], %[xh], %[t2]"
-                 : [xl] "+v"(xl), [xh] "+v"(xh), [s0] "=&v"(s0), [s1] "=&v"(s1), [s2] "=&v"(s2), [s3] "=&v"(s3),
-                   [s4] "=&v"(s4), [s5] "=&v"(s5), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2)
-                 : [yl] "v"(yl), [yh] "v"(yh), [va] "v"(m.v[0]), [vb] "v"(m.v[1]), [sa] "s"(m.s[0]),
-                   [sb] "s"(m.s[1]), [sc] "s"(m.s[2]));
-    return;
-  }
   uint32_t s[6];
   selectors(yl, yh, s);
   qplane_sub(xl, s[0], s[1], s[2], m.v[0], m.v[1], m.s[0], m.s[1], m.s[2]);
@@ -521,15 +453,10 @@ __device__ __forceinline__ void cq_to_blks(const uint32_t* cl, const uint32_t* c
   d[3] = make_uint2(vperm(r1.y, r0.y, 0x07060302u), vperm(r3.y, r2.y, 0x07060302u));
 }
 
-// NP_UNALIGNED: vector accesses at any even address (rows_vec_ok below).
-#ifndef NP_UNALIGNED
-#define NP_UNALIGNED 1
-#endif
-
 // 4 symbols (columns 4l..4l+3 of one shard row) to / from global memory.
 // `full` (wave-uniform) = whole 256-column tile present and 8-byte aligned rows.
 // Partial tiles: lanes whose four columns all exist still use one 8-byte
-// access (any even address, NP_UNALIGNED below).
+// access (any even address, rows_vec_ok below).
 __device__ __forceinline__ void store4(uint8_t* rowp, uint2 v, uint32_t lane, uint32_t ncols, bool full) {
   if (full) {
     *reinterpret_cast<uint2*>(rowp + 8u * lane) = v;
@@ -545,7 +472,7 @@ __device__ __forceinline__ void store4(uint8_t* rowp, uint2 v, uint32_t lane, ui
 }
 
 __device__ __forceinline__ uint2 load4(const uint8_t* rowp, uint32_t lane, uint32_t ncols, bool full) {
-  if (full || (NP_UNALIGNED && 4 * lane + 4 <= ncols)) return *reinterpret_cast<const uint2*>(rowp + 8u * lane);
+  if (full || 4 * lane + 4 <= ncols) return *reinterpret_cast<const uint2*>(rowp + 8u * lane);
   uint32_t w[2] = {0, 0};
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -579,26 +506,12 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 // policy: payload loads of the single-tile and k = 1024 encodes (config 4
 // encode -5 %, config 2 neutral) and the k = 1024 reconstruct's output
 // (whole lines; -1 %).
-#ifndef NP_PAYLOAD_NT
-#define NP_PAYLOAD_NT 1
-#endif
-#ifndef NP_OUT8_NT
-#define NP_OUT8_NT 1
-#endif
 __device__ __forceinline__ uint2 load_once(const uint8_t* p) {
-#if NP_PAYLOAD_NT
   const uint64_t v = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p));
   return make_uint2(static_cast<uint32_t>(v), static_cast<uint32_t>(v >> 32));
-#else
-  return *reinterpret_cast<const uint2*>(p);
-#endif
 }
 __device__ __forceinline__ void store_once(uint8_t* p, uint2 v) {
-#if NP_OUT8_NT
   __builtin_nontemporal_store(static_cast<uint64_t>(v.x) | (static_cast<uint64_t>(v.y) << 32), reinterpret_cast<uint64_t*>(p));
-#else
-  *reinterpret_cast<uint2*>(p) = v;
-#endif
 }
 
 // Raw buffer descriptor (V#) over [base, base + bytes): buffer loads and
@@ -616,30 +529,24 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uin
 // rates), so odd or 2-mod-4 chunk counts -- rows 2- or 4-byte aligned, e.g.
 // the reference bench's 10 MB payloads at k = 512 -- keep the vector path
 // instead of per-symbol accesses.  The parity tests with odd chunk counts pin
-// it.  NP_UNALIGNED=0 restores 8- / 16-byte alignment requirements.
+// it.
 __device__ __forceinline__ bool rows_vec_ok(const void* p, size_t stride, size_t len) {
-  constexpr uintptr_t m = NP_UNALIGNED ? 1u : 7u;
-  return ((reinterpret_cast<uintptr_t>(p) | stride | len) & m) == 0;
+  return ((reinterpret_cast<uintptr_t>(p) | stride | len) & 1u) == 0;
 }
-// Streaming row stores: 0 always, 1 for rows of whole 128-byte lines, 2 for
-// 8-byte aligned rows.
-#ifndef NP_ROW_NT_MODE
-#define NP_ROW_NT_MODE 1
-#endif
+// Streaming row stores for rows of whole 128-byte lines only (streaming partial
+// lines made the 10 MB encode 3.8 ms instead of 2.3).
 __device__ __forceinline__ bool rows_nt(const void* p, size_t stride, size_t len) {
   const uintptr_t v = reinterpret_cast<uintptr_t>(p) | stride | len;
-  return NP_ROW_NT_MODE == 0 ? true : NP_ROW_NT_MODE == 1 ? (v & 127u) == 0 : (v & 7u) == 0;
+  return (v & 127u) == 0;
 }
-__device__ __forceinline__ bool out_vec_ok(const void* p, size_t stride) {
-  return NP_UNALIGNED || ((reinterpret_cast<uintptr_t>(p) | stride) & 15u) == 0;
-}
+__device__ __forceinline__ bool out_vec_ok(const void*, size_t) { return true; }  // any address (rows_vec_ok)
 
 // Shard rows row0..row0+15 (those below wanted_n) from cq registers.
 // Shard rows are written once and never read back by the encode: streaming
 // (nontemporal, the nt bit of the buffer store) stores leave L2 to the tiles
 // and tables; config 3 encode -3.3 %.
-#ifndef NP_ROW_STORE_CPOL
-#define NP_ROW_STORE_CPOL 2
+#ifndef kRowStoreCpol
+#define kRowStoreCpol 2
 #endif
 // nt (rows_nt): streaming stores; otherwise the default policy.
 __device__ __forceinline__ void store_rows(uint8_t* out, size_t shard_len, uint32_t row0, uint32_t wanted_n,
@@ -652,7 +559,7 @@ __device__ __forceinline__ void store_rows(uint8_t* out, size_t shard_len, uint3
       for (int p = 0; p < 16; ++p) {
         const uint2 v = cq_row(L[p], H[p]);
         __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, r, 8u * lane,
-                                              static_cast<uint32_t>(p * shard_len), NP_ROW_STORE_CPOL);
+                                              static_cast<uint32_t>(p * shard_len), kRowStoreCpol);
       }
     } else {
 #pragma unroll
@@ -661,7 +568,7 @@ __device__ __forceinline__ void store_rows(uint8_t* out, size_t shard_len, uint3
         __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, r, 8u * lane, static_cast<uint32_t>(p * shard_len), 0);
       }
     }
-  } else if (NP_UNALIGNED && 4 * lane + 4 <= ncols) {  // partial tile, lanes with all four columns
+  } else if (4 * lane + 4 <= ncols) {  // partial tile, lanes with all four columns
 #pragma unroll
     for (int p = 0; p < 16; ++p)
       if (row0 + p < wanted_n) *reinterpret_cast<uint2*>(out + static_cast<size_t>(row0 + p) * shard_len + 8u * lane) = cq_row(L[p], H[p]);
@@ -700,44 +607,9 @@ __device__ __forceinline__ void pipelined(const DevTables& T, CF cval, GF group)
   pipe_step<0, NG>(T, cval, group, pa, pb);
 }
 
-// NP_PIPE_WAIT: group f starts with an explicit wait for every outstanding
-// scalar / LDS load (the tables of group f, issued during group f-1), and only
-// then issues the prefetch of group f+1 (SGPR half by s_load, VGPR half by
-// ds_read).  Without it the compiler's wait for group f's tables also waits
-// for the prefetch issued just before (scalar loads return out of order, so
-// the only wait it can use is lgkmcnt(0)): the prefetch never overlaps.
-// Measured neutral (config 3 +0.3 %, config 4 within its run-to-run noise):
-// the table fetches do not bound the kernels, so off.  Loading the row
-// tables' VGPR half by vector loads instead of s_load + v_mov measured +7 %
-// on the decode.
-#ifndef NP_PIPE_WAIT
-#define NP_PIPE_WAIT 0
-#endif
-constexpr uint16_t kWaitLgkm0 = 0xC07F;  // s_waitcnt lgkmcnt(0), vmcnt / expcnt untouched (gfx9 encoding)
-
-struct VHalf {
-  uint32_t v[8];
-};
-
-template <bool SUB>
-__device__ __forceinline__ void vhalf_load(const uint32_t* vp, VHalf& h) {
-  const uint4 a = *reinterpret_cast<const uint4*>(vp);
-  h.v[0] = a.x, h.v[1] = a.y, h.v[2] = a.z, h.v[3] = a.w;
-  if constexpr (!SUB) {
-    const uint4 b = *reinterpret_cast<const uint4*>(vp + 4);
-    h.v[4] = b.x, h.v[5] = b.y, h.v[6] = b.z, h.v[7] = b.w;
-  }
-}
-
-template <bool SUB>
-__device__ __forceinline__ Mult mult_from(const uint32_t (&sp)[12], const VHalf& h) {
-  Mult m;
-#pragma unroll
-  for (int i = 0; i < (SUB ? 6 : 12); ++i) m.s[i] = sp[i];
-#pragma unroll
-  for (int i = 0; i < (SUB ? 4 : 8); ++i) m.v[i] = h.v[i];
-  return m;
-}
+// (Measured and not kept: an explicit lgkmcnt(0) wait at each group's start,
+// so that the next group's table prefetch overlaps -- neutral, config 3
+// +0.3 %; the row tables' VGPR half by vector loads -- +7 % on the decode.)
 
 // Same with group f's tables at rec(Int<f>) (a wave-uniform global address).
 __device__ __forceinline__ void pool_at(cpool_t q, uint32_t (&p)[20]) {
@@ -750,7 +622,6 @@ __device__ __forceinline__ void pool_at(cpool_t q, uint32_t (&p)[20]) {
 template <int F, int NG, typename RF, typename NF, typename GF>
 __device__ __forceinline__ void rpipe_step(RF& rec, NF& need, GF& group, uint32_t (&cur)[20], uint32_t (&nxt)[20]) {
   if constexpr (F < NG) {
-    if constexpr (NP_PIPE_WAIT) __builtin_amdgcn_s_waitcnt(kWaitLgkm0);  // see spipe_step
     if constexpr (F + 1 < NG) {
       if (need(Int<F + 1>{})) pool_at(rec(Int<F + 1>{}), nxt);
     }
@@ -781,26 +652,15 @@ struct NoOut {
 };
 template <int F, int NG, bool TW, typename CF, typename VF, typename SF, typename GF, typename OF>
 __device__ __forceinline__ void spipe_step(const DevTables& T, CF& cval, VF& vaddr, SF& subf, GF& group, OF& outf,
-                                           uint32_t (&cur)[12], uint32_t (&nxt)[12], VHalf& curv, VHalf& nxtv) {
+                                           uint32_t (&cur)[12], uint32_t (&nxt)[12]) {
   if constexpr (F < NG) {
-    if constexpr (NP_PIPE_WAIT) {
-      __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
-      if constexpr (F + 1 < NG) {
-        spool_of<TW, decltype(subf(Int<F + 1>{}))::value, decltype(outf(Int<F + 1>{}))::value>(
-            T, cval(Int<F + 1>{}), nxt);
-        vhalf_load<decltype(subf(Int<F + 1>{}))::value>(vaddr(Int<F + 1>{}), nxtv);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      group(Int<F>{}, mult_from<decltype(subf(Int<F>{}))::value>(cur, curv));
-    } else {
-      if constexpr (F + 1 < NG)
-        spool_of<TW, decltype(subf(Int<F + 1>{}))::value, decltype(outf(Int<F + 1>{}))::value>(
-            T, cval(Int<F + 1>{}), nxt);
-      __builtin_amdgcn_sched_barrier(0);
-      group(Int<F>{}, staged_mult<decltype(subf(Int<F>{}))::value>(cur, vaddr(Int<F>{})));
-    }
+    if constexpr (F + 1 < NG)
+      spool_of<TW, decltype(subf(Int<F + 1>{}))::value, decltype(outf(Int<F + 1>{}))::value>(T, cval(Int<F + 1>{}),
+                                                                                             nxt);
     __builtin_amdgcn_sched_barrier(0);
-    spipe_step<F + 1, NG, TW>(T, cval, vaddr, subf, group, outf, nxt, cur, nxtv, curv);
+    group(Int<F>{}, staged_mult<decltype(subf(Int<F>{}))::value>(cur, vaddr(Int<F>{})));
+    __builtin_amdgcn_sched_barrier(0);
+    spipe_step<F + 1, NG, TW>(T, cval, vaddr, subf, group, outf, nxt, cur);
   }
 }
 
@@ -808,10 +668,8 @@ template <int NG, bool TW = false, typename CF, typename VF, typename SF, typena
 __device__ __forceinline__ void pipelined_staged(const DevTables& T, CF cval, VF vaddr, SF subf, GF group,
                                                  OF outf = OF{}) {
   uint32_t pa[12], pb[12];
-  VHalf va, vb;
   spool_of<TW, decltype(subf(Int<0>{}))::value, decltype(outf(Int<0>{}))::value>(T, cval(Int<0>{}), pa);
-  if constexpr (NP_PIPE_WAIT) vhalf_load<decltype(subf(Int<0>{}))::value>(vaddr(Int<0>{}), va);
-  spipe_step<0, NG, TW>(T, cval, vaddr, subf, group, outf, pa, pb, va, vb);
+  spipe_step<0, NG, TW>(T, cval, vaddr, subf, group, outf, pa, pb);
 }
 
 // LDS slot of the multiplier of group t at level b of a size-K transform:
@@ -927,12 +785,6 @@ __device__ __forceinline__ void with_gen(uint32_t index, F&& f) {
   with_gen_from<(MING > 0 ? MING : 0), MAXG, FALLBACK>(g, f);
 }
 
-#ifndef NP_CQ_LIVE_ALL
-#define NP_CQ_LIVE_ALL 1  // measured: encode -2 % (no phi copies around the g == 0 skip branches; the zero element's table yields 0)
-#endif
-#ifndef NP_CQ_NO_SKIP
-#define NP_CQ_NO_SKIP 0
-#endif
 // The VGPR half (dwords 2..3) of the conversion's table, by a scalar load: the
 // compiler otherwise reads it with a vector load (it cannot prove that the row
 // stores do not alias the tables), and that load's vmcnt(0) wait also waits
@@ -1032,10 +884,9 @@ __device__ __forceinline__ void cq_levels(const DevTables& T, const uint32_t* VP
     constexpr GroupRef r = cq_group<INVERSE>(decltype(fc)::value);
     constexpr int d = 1 << r.b;
     progress_prio<decltype(fc)::value, 15, PRIO>();
-    const bool live = NP_CQ_LIVE_ALL || !INDEX0 || r.t != 0 || g != 0;  // c == 0: the skew sentinel, no product
     if constexpr (CONV && r.b == 0 && r.t == 0) ct = conv_tab(T);
     constexpr uint32_t span = ((1u << (2 * d)) - 1u) << (r.t * 2 * d);  // the group's rows
-    if (!NP_CQ_NO_SKIP && (rows & span) == 0) return;
+    if ((rows & span) == 0) return;
     auto body = [&](auto sub_c) __attribute__((always_inline)) {
       constexpr bool SUB = decltype(sub_c)::value;
 #pragma unroll
@@ -1046,9 +897,9 @@ __device__ __forceinline__ void cq_levels(const DevTables& T, const uint32_t* VP
         } else if (INVERSE) {
           L[y] ^= L[x];
           H[y] ^= H[x];
-          if (live) qmul_mode<SUB>(L[x], H[x], L[y], H[y], p);
+          qmul_mode<SUB>(L[x], H[x], L[y], H[y], p);
         } else {
-          if (live) qmul_mode<SUB>(L[x], H[x], L[y], H[y], p);
+          qmul_mode<SUB>(L[x], H[x], L[y], H[y], p);
           L[y] ^= L[x];
           H[y] ^= H[x];
         }
@@ -1189,9 +1040,6 @@ __device__ __forceinline__ void add_derivative(uint32_t (&A)[16], uint32_t (&X)[
 // the high plane through the b slots of tower_pools[kFieldSize].
 template <int NR>
 __device__ __forceinline__ void tower_convert(const DevTables& T, uint32_t (&L)[NR], const uint32_t (&H)[NR]) {
-#ifdef NP_NO_CONVERT
-  return;
-#endif
   const cpool_t q = (cpool_t)(T.tower_pools) + 65536u * kPoolWords;
   const uint32_t sa = q[8 + 3], sb = q[8 + 4], sc = q[8 + 5];
   const uint64_t vv = tower_conv_vhalf(q);

@@ -30,15 +30,11 @@
 namespace np {
 namespace {
 
-// NP_PRIO_BIG (bit 0 the encode, bit 1 the decode): progress-based issue
-// priority in the sub-segment transforms' passes (fast_common.hpp
-// progress_prio).  Measured at 7000 validators (k = 2048, profiles/r04_ab.txt
-// probe 25): encode 1.818 / 1.799 -> 1.715 / 1.745 ms (-4 %), reconstruct
-// 2.807 / 2.815 -> 2.796 / 2.805 ms.
-#ifndef NP_PRIO_BIG
-#define NP_PRIO_BIG 3
-#endif
-constexpr int kBigPrioEnc = NP_PRIO_BIG & 1, kBigPrioDec = (NP_PRIO_BIG >> 1) & 1;
+// Progress-based issue priority in the sub-segment transforms' passes, encode
+// and decode (fast_common.hpp progress_prio).  Measured at 7000 validators
+// (k = 2048, profiles/r04_ab.txt probe 25): encode 1.818 / 1.799 -> 1.715 /
+// 1.745 ms (-4 %), reconstruct 2.807 / 2.815 -> 2.796 / 2.805 ms.
+constexpr int kBigPrioEnc = 1, kBigPrioDec = 1;
 
 constexpr int kS = 256;                   // sub-segment (register-layout) size
 constexpr int kTB = Geo<kS>::kThreads;    // 1024 threads
@@ -194,9 +190,6 @@ __device__ __forceinline__ void top_forward(uint2 (&w)[SUBS], uint32_t c, const 
 // ------------------------------------------------------------------ encode ----
 // The shift's top-level outputs W are written once and read once: streaming
 // (-6 % on the encode); the coefficients M keep the default policy.
-#ifndef NP_W_NT
-#define NP_W_NT true
-#endif
 // Sub-segment transforms of the shifts run in tower coordinates while
 // gen_of(index) <= kEncBigMaxGen (index < 4096: n <= 4096, config 4); their
 // levels below gen_of(index) with the full map.  Farther shifts of larger codes
@@ -220,9 +213,6 @@ constexpr size_t enc_scratch() {
 // (the high layout of k_encode_multi; the top levels and the scratch are
 // per thread and position, so they follow it unchanged).  The decode keeps
 // the natural format: D_256 needs position bits 0-3 in one wave.
-#ifndef NP_BIG_ENC_QX
-#define NP_BIG_ENC_QX 1
-#endif
 
 template <int KB>
 __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_big(
@@ -245,7 +235,6 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   const bool full =
       ncols == kTile && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
   const uint32_t cqb = col_base<kS>(4 * lane) ^ (32u * g);
-  const uint32_t hb = col_base<kS>(tid / G::R) ^ (8u * (tid % G::R));
   const bool fast_in = out_vec_ok(pay, 0) &&
                        static_cast<size_t>(ch0 + kTile) * 2 * KB <= a.payload_len;
 
@@ -292,19 +281,13 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
         constexpr int GEN = decltype(gc)::value;  // 0 only at index 0
         cq_levels<kS, true, GEN == 0, GEN, false, kBigPrioEnc>(T, VP, index, g, CL, CH);
       });
-      if constexpr (NP_BIG_ENC_QX) {  // quad items (fast_common.hpp cq_write_q): no byte transposes
-        __syncthreads();              // they overlay payload blocks that other waves read
-        cq_write_q(tile, g, lane, CL, CH);
-      } else {
-        cq_write<kS>(tile, cq, CL, CH);
-      }
+      // quad items (fast_common.hpp cq_write_q): no byte transposes
+      __syncthreads();  // they overlay payload blocks that other waves read
+      cq_write_q(tile, g, lane, CL, CH);
     }
     __syncthreads();
     uint32_t XL[16], XH[16];
-    if constexpr (NP_BIG_ENC_QX)
-      hi_read_q(tile, g, lane, XL, XH);
-    else
-      hi_read<kS>(tile, fresh_v(hb), XL, XH);
+    hi_read_q(tile, g, lane, XL, XH);
     with_gen<0, kSubMaxGen<KB>, false>(index, [&](auto gc) __attribute__((always_inline)) {
       constexpr int GEN = decltype(gc)::value;
       hi_levels<kS, true, GEN == 0, 0, GEN, kBigPrioEnc>(T, VP, index, XL, XH);
@@ -352,7 +335,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       top_forward<SUBS>(w, c, tm);
       scr_q_store<false>(tile, j, tid, w[0]);
 #pragma unroll
-      for (int r = 1; r < SUBS; ++r) scr_q_store<NP_W_NT>(scrW + r * kSegScr, j, tid, w[r]);
+      for (int r = 1; r < SUBS; ++r) scr_q_store<true>(scrW + r * kSegScr, j, tid, w[r]);
     }
 #pragma unroll 1
     for (uint32_t s = 0; s < SUBS; ++s) {
@@ -364,21 +347,15 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       __syncthreads();  // the tile (W_0 read) and the tables are free
       stage_vpools<kS, kTB>(T, index, VP, gen_of(index) <= kEncBigMaxGenK<KB>);
       __syncthreads();
-      if (s != 0) scr_load<NP_W_NT>(scrW + s * kSegScr, tid, XL, XH);
+      if (s != 0) scr_load<true>(scrW + s * kSegScr, tid, XL, XH);
       with_gen<1, kEncBigMaxGenK<KB>, true>(index, [&](auto gc) __attribute__((always_inline)) {
         constexpr int GEN = decltype(gc)::value;
         if constexpr (GEN < 0) tower_convert(T, XL, XH);  // a far shift: Cantor coordinates
         hi_levels<kS, false, false, 0, GEN, kBigPrioEnc>(T, VP, index, XL, XH);
       });
-      if constexpr (NP_BIG_ENC_QX) {
-        hi_write_q(tile, g, lane, XL, XH);
-        __syncthreads();
-        cq_read_q(tile, g, lane, XL, XH);
-      } else {
-        hi_write<kS>(tile, fresh_v(hb), XL, XH);
-        __syncthreads();
-        cq_read<kS>(tile, fresh_v(cqb), XL, XH);
-      }
+      hi_write_q(tile, g, lane, XL, XH);
+      __syncthreads();
+      cq_read_q(tile, g, lane, XL, XH);
       with_gen<1, kEncBigMaxGenK<KB>, true>(index, [&](auto gc) __attribute__((always_inline)) {
         constexpr int GEN = decltype(gc)::value;
         cq_levels<kS, false, false, GEN, false, kBigPrioEnc>(T, VP, index, g, XL, XH);
@@ -491,7 +468,7 @@ __device__ __forceinline__ void tile_copy_out(const ReconstructArgs& a, const ui
                                               uint32_t col0, uint32_t ncols, uint32_t s) {
   using G = Geo<kS>;
   uint8_t* outp = a.out + static_cast<size_t>(pb) * a.out_stride + static_cast<size_t>(col0) * 2 * KB + 512u * s;
-  const bool al_o = NP_UNALIGNED || ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 7u) == 0;
+  const bool al_o = true;  // 8-byte stores at any address (rows_vec_ok)
   // opaque thread id, one output pointer stepped per column: otherwise the 16
   // per-lane 64-bit column addresses are hoisted out of the callers' loops and
   // spilled, and every reload waits (vmcnt(0)) for the stores before it
@@ -536,11 +513,8 @@ __device__ __forceinline__ void big_copy_systematic(const ReconstructArgs& a, co
 
 // Quad positions whose scratch loads phase 2 issues together (NQ <= 4);
 // 2 measured +3 % at config 4.
-#ifndef NP_REC_JB
-#define NP_REC_JB 1
-#endif
 template <int NQ>
-constexpr int kRecJB = NQ <= 4 ? NP_REC_JB : 1;
+constexpr int kRecJB = 1;
 
 template <int KB, int NQ>
 __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k_reconstruct_big(

@@ -32,11 +32,8 @@
 #include <cstdlib>
 
 #include "fast_common.hpp"
-// The next tile's payload is read once: streaming (nt) LDS-DMA loads keep L2
-// for the tables and the row stores; config 3 encode -4 %.
-#ifndef NP_DMA_MOD
-#define NP_DMA_MOD " nt"
-#endif
+// (The next tile's payload is read once: its LDS-DMA loads stream (nt),
+// keeping L2 for the tables and the row stores; config 3 encode -4 %.)
 
 namespace np {
 namespace {
@@ -57,42 +54,20 @@ __device__ __forceinline__ bool enc_tower(uint32_t index) {
 // K = 256).  SH = 0: a shift >= 4 (n > 4K) in Cantor coordinates.  A runtime
 // choice between instances inside a pass makes the register allocator spill,
 // so each call site is one instance.
-// NP_PRIO_ENC: the encode's transform passes with progress-based issue
-// priority (fast_common.hpp progress_prio).  Measured: config-3 encode
-// 1.601 / 1.602 -> 1.514 / 1.527 ms (-5 %, profiles/r04_ab.txt probe 18).
-// NP_PRIO_DEC (bits: 1 the segments' cq levels, 2 their high levels, 4 the
-// forward transform) for the fast decode: all three measured +1.5 to +2.8 %.
-#ifndef NP_PRIO_ENC
-#define NP_PRIO_ENC 1
-#endif
-#ifndef NP_PRIO_DEC
-#define NP_PRIO_DEC 24
-#endif
-// NP_PRIO_ENC=2 (experiment): the encode's span schedule, the cq pass of shift
-// s (3, 3, 2, 2) and the high levels of shift s + 1 (1, 1, 0, 0) that follow
-// it without a barrier.
-constexpr int kEncPrio = NP_PRIO_ENC == 2 ? 3 : NP_PRIO_ENC;
-constexpr int kEncPrioCq = NP_PRIO_ENC == 2 ? 4 : NP_PRIO_ENC;
-// Bit 3 (the default): one schedule over each barrier-free span of the
-// segment sweep (high levels of step s, fold, premultiply and cq levels of
-// step s + 1): priority 3 in the high levels, 2 in the premultiply, 1 then 0 in
-// the cq levels.  Measured: config-3 reconstruct 2.741 / 2.759 / 2.758 ->
-// 2.655 / 2.669 / 2.672 ms (-3.2 %, profiles/r04_ab.txt probe 21).
-// Bit 4 (the default): the same over the forward transform's spans (its high
-// levels after the last step's: 1, 1, 0, 0; its cq levels and the merge: 3).
-// Measured: 2.684 / 2.696 -> 2.648 / 2.642 ms (-1.7 %, probe 22).  The
-// encode's span schedule (NP_PRIO_ENC=2) measured neutral.
-constexpr bool kRecPrioSpan = (NP_PRIO_DEC & 8) != 0, kRecPrioSpanFwd = (NP_PRIO_DEC & 16) != 0;
-#ifndef NP_PRIO_PREMUL
-#define NP_PRIO_PREMUL 2  // the premultiply's priority in the span schedule (3 and 1 measured within noise, probe 24)
-#endif
-#ifndef NP_PRIO_SPAN_HI
-#define NP_PRIO_SPAN_HI 2  // the high levels' schedule in the span (progress_prio PRIO; 4 measured within noise, probe 26)
-#endif
-constexpr int kRecPrioCq = kRecPrioSpan ? 3 : NP_PRIO_DEC & 1,
-              kRecPrioHi = kRecPrioSpan ? NP_PRIO_SPAN_HI : (NP_PRIO_DEC >> 1) & 1;
-constexpr int kRecPrioFwdHi = kRecPrioSpanFwd ? 3 : (NP_PRIO_DEC >> 2) & 1,
-              kRecPrioFwdCq = kRecPrioSpanFwd ? 2 : (NP_PRIO_DEC >> 2) & 1;
+// Issue priority (s_setprio, fast_common.hpp progress_prio; DESIGN.md §4.2,
+// §4.3).  Encode: every transform pass by progress (priority 3 in its first
+// quarter of butterfly groups down to 0 in the last): config-3 encode 1.601 /
+// 1.602 -> 1.514 / 1.527 ms (-5 %, profiles/r04_ab.txt probe 18).  Decode: one
+// schedule over each barrier-free span of the segment sweep (high levels of
+// step s, fold, premultiply and cq levels of step s + 1): priority 2 in the
+// high levels (progress schedule 2), 2 in the premultiply, 3 then 0 in the cq
+// levels: config-3 reconstruct -3.2 % (probe 21); the forward transform's
+// spans likewise (its high levels 3, its cq levels and the merge 2): -1.7 %
+// (probe 22).  Per-pass priority in the decode measured +1.5 to +2.8 %, the
+// encode's span schedule neutral, premultiply priorities 1 and 3 and high-level
+// schedule 4 within noise (probes 24, 26).
+constexpr int kEncPrio = 1, kEncPrioCq = 1;
+constexpr int kRecPrioPremul = 2, kRecPrioCq = 3, kRecPrioHi = 2, kRecPrioFwdHi = 3, kRecPrioFwdCq = 2;
 
 template <int K, int SH>
 constexpr int kShiftGen = static_cast<int>(gen_of((SH == 23 ? 2 : SH) * K));
@@ -124,18 +99,14 @@ __device__ __forceinline__ void shift_hi(const DevTables& T, const uint32_t* vp,
   }
 }
 
-// NP_ENC_CONV: shifts whose level 0 multiplies by full elements (gen_of(sK)
-// >= 1: every shift at k = 256) leave the tower inside that level
-// (cq_levels CONV, qbfly_fwd_conv) instead of converting the 16 rows after it.
-// Measured: config-3 encode 1.656 / 1.663 -> 1.629 / 1.631 ms (-1.8 %,
-// profiles/r04_ab.txt).
-#ifndef NP_ENC_CONV
-#define NP_ENC_CONV 1
-#endif
+// Shifts whose level 0 multiplies by full elements (gen_of(sK) >= 1: every
+// shift at k = 256) leave the tower inside that level (cq_levels CONV,
+// qbfly_fwd_conv) instead of converting the 16 rows after it.  Measured:
+// config-3 encode 1.656 / 1.663 -> 1.629 / 1.631 ms (-1.8 %, profiles/r04_ab.txt).
 // Whether shift sh of a size-K encode fuses its conversion; the staging of its
 // tables must agree (stage_vpools l0_out).  SH = 23 stands for shifts 2 and 3.
 __host__ __device__ constexpr bool enc_conv(int K, uint32_t sh) {
-  return NP_ENC_CONV && sh >= 1 && sh <= 3 && gen_of(sh * static_cast<uint32_t>(K)) >= 1;
+  return sh >= 1 && sh <= 3 && gen_of(sh * static_cast<uint32_t>(K)) >= 1;
 }
 template <int K, int SH>
 constexpr bool kEncConv = SH != 0 && enc_conv(K, SH == 23 ? 2u : static_cast<uint32_t>(SH));
@@ -154,21 +125,11 @@ __device__ __forceinline__ void shift_cq(const DevTables& T, const uint32_t* vp,
   }
 }
 
-// NP_ENC_HIW_EARLY: the multi-tile encode writes each shift's high-layout quads
-// to LDS right after their last (level-4) butterfly group instead of after
-// the whole high pass.  Measured: encode -1.9 % at config 3 (1.686 -> 1.655
-// ms, two runs each, profiles/r04_ab.txt).
-#ifndef NP_ENC_HIW_EARLY
-#define NP_ENC_HIW_EARLY 1
-#endif
-
 // The fast encodes exchange layouts through quad items (cq_write_q ..
-// hi_read_q, fast_common.hpp): no byte transposes.
-#ifndef NP_ENC_QX
-#define NP_ENC_QX 1
-#endif
-template <int K>
-constexpr bool kEncQx = NP_ENC_QX != 0;
+// hi_read_q, fast_common.hpp): no byte transposes.  The multi-tile encode
+// writes each shift's high-layout quads to LDS right after their last
+// (level-4) butterfly group instead of after the whole high pass: encode
+// -1.9 % at config 3 (1.686 -> 1.655 ms, profiles/r04_ab.txt).
 
 // One workgroup: 256 chunks of one payload.  mod.rs:144-154 / inc_encode.rs:15-48.
 template <int K>
@@ -236,23 +197,15 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     store_rows(out, a.shard_len, 16 * g, wanted_store, CL, CH, lane, ncols, full, nt);
     tower_convert(T, CL, CH);  // transforms run in tower coordinates
     cq_levels<K, true, true, 0, false, kEncPrioCq>(T, VP, 0, g, CL, CH);
-    if constexpr (kEncQx<K>) {
-      // the quad items overlay payload blocks that other waves read: wait for
-      // every wave's cq_read (cq_write_p writes back only the blocks it read)
-      __syncthreads();
-      cq_write_q(tile, g, lane, CL, CH);
-    } else {
-      cq_write_p<K>(tile, cqb, CL, CH);
-    }
+    // the quad items overlay payload blocks that other waves read: wait for
+    // every wave's cq_read
+    __syncthreads();
+    cq_write_q(tile, g, lane, CL, CH);
   }
   __syncthreads();
   // ---- high layout: inverse levels 4.. -> coefficients M
-  const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
   uint32_t ML[16], MH[16];
-  if constexpr (kEncQx<K>)
-    hi_read_q<K>(tile, g, lane, ML, MH);
-  else
-    hi_read_p<K>(tile, hb, ML, MH);
+  hi_read_q<K>(tile, g, lane, ML, MH);
   hi_levels<K, true, true, 0, 0, kEncPrio>(T, VP, 0, ML, MH);
 #pragma unroll
   for (int q = 0; q < 16; ++q) asm volatile("" : "+v"(ML[q]), "+v"(MH[q]));  // materialise M once
@@ -268,15 +221,9 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     if (!resident && sh + 1 < nshift && (sh + 1) * K < a.wanted_n)
       stage_vpools<K, G::kThreads>(T, (sh + 1) * K, VP + ((sh + 1) & 1u) * G::kVPWords, sh + 1 < 4,
                                    enc_conv(K, sh + 1));
-    if constexpr (kEncQx<K>) {
-      hi_write_q<K>(tile, g, lane, XL, XH);
-      __syncthreads();
-      cq_read_q(tile, g, lane, XL, XH);
-    } else {
-      hi_write_p<K>(tile, fresh_v(hb), XL, XH);
-      __syncthreads();
-      cq_read_p<K>(tile, fresh_v(cqb), XL, XH);
-    }
+    hi_write_q<K>(tile, g, lane, XL, XH);
+    __syncthreads();
+    cq_read_q(tile, g, lane, XL, XH);
     shift_cq<K, SH>(T, vp, index, g, XL, XH);
     store_rows(out, a.shard_len, index + 16 * g, wanted_store, XL, XH, lane, ncols, full, nt);
   };
@@ -314,72 +261,18 @@ struct EncLaunch {
 };
 typedef const __attribute__((address_space(4))) EncLaunch* enc_launch_ptr;
 
-// The tile's payload blocks by LDS-DMA, 4 bytes per lane: wave w fills LDS
-// bytes [8 KiB w, 8 KiB (w + 1)) = columns 16w..16w+15, in LDS order; each
-// lane reads the payload dword that the swizzled LDS image holds there
-// (col_base: block m of column c at byte 512c + 8 (m ^ swz(c)) for K = 256).
-// Written as asm (M0 = the piece's LDS address, set in the same statement,
-// cdna_hip_programming.md §5.7): hipcc then adds no vmcnt(0) of its own
-// before the next LDS reads, which would also wait for the row stores issued
-// after these loads; encode_tile_multi waits with a counted vmcnt instead.
+// The next tile's payload by 16-byte LDS-DMA pieces (8 per wave instead of 32
+// of 4 bytes), which needs the payload tile's swizzle at 16-byte granularity
+// (col_base EVEN; the tile's cq reads then conflict 2-way).  From the stamps
+// (profiles/r04_encode_stamps_hiw.txt): 32 pieces per wave overfill the wave's
+// memory queue and the DMA's issue stalls.  Measured: encode 1.625 / 1.630 /
+// 1.625 -> 1.598 / 1.603 / 1.596 ms (-1.7 %, profiles/r04_ab.txt probe 15).
+// The pieces' addresses are a scalar base plus a 32-bit lane offset (1 VALU per
+// piece instead of 7 for 64-bit per-lane addresses; -0.5 %, probe 17).  Issuing
+// all pieces from 4 waves after a barrier measured -0.8 % on top, neutral with
+// the issue priority (probe 18).
 template <int K>
-__device__ __forceinline__ void dma_tile(const uint8_t* pay, uint32_t ch0, uint8_t* tile, uint32_t w, uint32_t lane) {
-  static_assert(Geo<K>::P == 1 && Geo<K>::W == Geo<K>::Q, "one swizzle row per column");
-  constexpr uint32_t kColBytes = 2 * K, kPieces = 2 * K / 256;  // 256-byte pieces per column
-  const uint32_t sw0 = swz<K>(16u * w);
-  const uint32_t lds0 = static_cast<uint32_t>(
-      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)(tile)));
-#pragma unroll
-  for (uint32_t j = 0; j < 16 * kPieces; ++j) {
-    const uint32_t c = 16u * w + j / kPieces;                   // column (wave-uniform)
-    const uint32_t sw = sw0 ^ swz<K>(j / kPieces);              // swz(c): linear in c
-    const uint32_t b = (j % kPieces) * 32u + (lane >> 1);       // LDS block of this lane
-    const uint8_t* src = pay + static_cast<size_t>(ch0 + c) * kColBytes + 8u * (b ^ sw) + 4u * (lane & 1u);
-    const uint32_t dst = uniform(lds0 + c * kColBytes + 256u * (j % kPieces));
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" NP_DMA_MOD "\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(src), "s"(dst)
-                 : "memory");
-  }
-}
-
-// NP_ENC_DMA_NOBAR: no workgroup barrier before the next tile's payload DMA
-// with the quad exchange (each wave's DMA share is the LDS region only it
-// reads back).  Measured: encode 1.646 / 1.648 -> 1.638 / 1.638 ms (-0.6 %,
-// profiles/r04_ab.txt probe 13).  Spreading the 32 DMA pieces over the last
-// cq pass instead of issuing them at once measured +0.3 to +0.7 %.
-#ifndef NP_ENC_DMA_NOBAR
-#define NP_ENC_DMA_NOBAR 1
-#endif
-
-// NP_ENC_DMA_X4: the next tile's payload by 16-byte LDS-DMA pieces (8 per
-// wave instead of 32 of 4 bytes), which needs the payload tile's swizzle at
-// 16-byte granularity (col_base EVEN; the tile's cq reads then conflict 2-way).
-// From the stamps (profiles/r04_encode_stamps_hiw.txt): 32 pieces per wave
-// overfill the wave's memory queue and the DMA's issue stalls.  Measured:
-// encode 1.625 / 1.630 / 1.625 -> 1.598 / 1.603 / 1.596 ms (-1.7 %,
-// profiles/r04_ab.txt probe 15).
-#ifndef NP_ENC_DMA_X4
-#define NP_ENC_DMA_X4 1
-#endif
-template <int K>
-constexpr bool kEncDmaX4 = NP_ENC_DMA_X4 && K == 256;
-
-// NP_ENC_DMA_WAVES (experiment, with kEncDmaX4): only waves 0..W-1 issue the
-// next tile's DMA pieces (16 / W waves' shares each) after a barrier, so that
-// the other waves start the last cq pass instead of waiting to issue theirs.
-#ifndef NP_ENC_DMA_WAVES
-#define NP_ENC_DMA_WAVES 16
-#endif
-#ifndef NP_ENC_DMA_YOUNG
-#define NP_ENC_DMA_YOUNG 0
-#endif
-// NP_ENC_DMA_SADDR: the x4 pieces' addresses as a scalar base plus a 32-bit
-// lane offset (1 VALU per piece instead of 7 for 64-bit per-lane addresses).
-#ifndef NP_ENC_DMA_SADDR
-#define NP_ENC_DMA_SADDR 1
-#endif
+constexpr bool kEncDmaX4 = K == 256;
 
 // kEncDmaX4: wave w's columns 16w..16w+15 in 8 pieces of two columns (lanes
 // 0-31 the first, 32-63 the second, 16 bytes each): lane l of a piece writes
@@ -393,34 +286,19 @@ __device__ __forceinline__ void dma_tile_x4(const uint8_t* pay, uint32_t ch0, ui
       reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)(tile)));
   const uint32_t half = lane >> 5, li = lane & 31u;
   const uint32_t swh = half ? (swz<K>(1) & ~1u) : 0u;  // the odd column's part of the (linear) swizzle
-  if constexpr (NP_ENC_DMA_SADDR) {
-    // scalar base per piece (column 16w + 2j), 32-bit lane offset: the swizzle
-    // is linear, so piece j's offset is the lane's piece-0 offset XOR a constant
-    const uint32_t off0 = 512u * half + 8u * ((2u * li) ^ (swz<K>(16u * w) & ~1u) ^ swh);
-    const uint8_t* base = pay + static_cast<size_t>(ch0 + 16u * w) * kColBytes;
-#pragma unroll
-    for (uint32_t j = 0; j < 8; ++j) {
-      const uint32_t off = off0 ^ (8u * (swz<K>(2u * j) & ~1u));
-      const uint8_t* sb = base + 2u * j * kColBytes;
-      const uint32_t dst = uniform(lds0 + (16u * w + 2u * j) * kColBytes);
-      uint32_t keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" NP_DMA_MOD "\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep)
-                   : "v"(off), "s"(sb), "s"(dst)
-                   : "memory");
-    }
-    return;
-  }
+  // scalar base per piece (column 16w + 2j), 32-bit lane offset: the swizzle
+  // is linear, so piece j's offset is the lane's piece-0 offset XOR a constant
+  const uint32_t off0 = 512u * half + 8u * ((2u * li) ^ (swz<K>(16u * w) & ~1u) ^ swh);
+  const uint8_t* base = pay + static_cast<size_t>(ch0 + 16u * w) * kColBytes;
 #pragma unroll
   for (uint32_t j = 0; j < 8; ++j) {
-    const uint32_t c0 = 16u * w + 2u * j;  // wave-uniform first column of the piece
-    const uint32_t sw = (swz<K>(c0) & ~1u) ^ swh;
-    const uint8_t* src = pay + static_cast<size_t>(ch0 + c0 + half) * kColBytes + 8u * ((2u * li) ^ sw);
-    const uint32_t dst = uniform(lds0 + c0 * kColBytes);
+    const uint32_t off = off0 ^ (8u * (swz<K>(2u * j) & ~1u));
+    const uint8_t* sb = base + 2u * j * kColBytes;
+    const uint32_t dst = uniform(lds0 + (16u * w + 2u * j) * kColBytes);
     uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" NP_DMA_MOD "\n\ts_mov_b32 m0, %0"
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
-                 : "v"(src), "s"(dst)
+                 : "v"(off), "s"(sb), "s"(dst)
                  : "memory");
   }
 }
@@ -431,7 +309,7 @@ __device__ __forceinline__ void dma_tile_x4(const uint8_t* pay, uint32_t ch0, ui
 template <int K, int SH>
 __device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArgs& a, uint8_t* tile, uint32_t* VP,
                                              uint8_t* out, uint32_t sh, uint32_t g, uint32_t lane, uint32_t ncols,
-                                             bool full, uint32_t cqb, uint32_t hb, const uint32_t (&ML)[16],
+                                             bool full, const uint32_t (&ML)[16],
                                              const uint32_t (&MH)[16], uint32_t (&PL)[8], uint32_t (&PH)[8],
                                              const uint8_t* dma_pay, uint32_t dma_ch0, uint64_t* dbg) {
   using G = Geo<K>;
@@ -439,7 +317,7 @@ __device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArg
   uint32_t XL[16], XH[16];
   const uint32_t* vp = VP + sh * G::kVPWords;  // the tables of every shift stay staged (kEncBuffers)
   constexpr int st0 = 7 + 4 * (SH - 1);  // stamp slots of this shift
-  if constexpr (NP_ENC_HIW_EARLY && kEncQx<K>) {
+  {
     // the quads of each level-4 group go to LDS as soon as they are final,
     // among the level's VALU work; the barrier that frees the tile (every
     // wave's previous cq read) moves before level 4
@@ -458,44 +336,15 @@ __device__ __forceinline__ void encode_shift(const DevTables& T, const EncodeArg
     stamp(dbg, st0);
     __syncthreads();
     cq_read_q(tile, g, lane, XL, XH);
-  } else if constexpr (kEncQx<K>) {
-    shift_hi<K, SH>(T, vp, index, ML, MH, XL, XH, PL, PH);
-    stamp(dbg, st0);
-    __syncthreads();  // the previous cq pass is done with the tile
-    hi_write_q<K>(tile, g, lane, XL, XH);
-    __syncthreads();
-    cq_read_q(tile, g, lane, XL, XH);
-  } else {
-    shift_hi<K, SH>(T, vp, index, ML, MH, XL, XH, PL, PH);
-    stamp(dbg, st0);
-    __syncthreads();  // the previous cq pass is done with the tile
-    hi_write_p<K>(tile, fresh_v(hb), XL, XH);
-    __syncthreads();
-    cq_read_p<K>(tile, fresh_v(cqb), XL, XH);
   }
   if (dma_pay) {
-    if constexpr (kEncDmaX4<K> && NP_ENC_DMA_WAVES < 16) {
-      constexpr uint32_t W = NP_ENC_DMA_WAVES;
-      __syncthreads();  // every wave has its cq registers: the tile is free
-      const uint32_t gi = NP_ENC_DMA_YOUNG ? g - (16u - W) : g;  // the youngest W waves instead
-      if (gi < W) {
-#pragma unroll
-        for (uint32_t r = 0; r < 16 / W; ++r) dma_tile_x4<K>(dma_pay, dma_ch0, tile, gi + W * r, lane);
-      }
-    } else if constexpr (kEncQx<K> && NP_ENC_DMA_NOBAR) {
-      // wave g's quad items and its share of the next payload tile are the
-      // same 8 KiB (cq_read_q, dma_tile): once its own reads are back, no
-      // other wave touches that region
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    } else {
-      __syncthreads();  // every wave has its cq registers: the tile is free
-    }
-    if constexpr ((kExp & 4) || (kEncDmaX4<K> && NP_ENC_DMA_WAVES < 16)) {
-    } else if constexpr (kEncDmaX4<K>) {
-      dma_tile_x4<K>(dma_pay, dma_ch0, tile, g, lane);
-    } else {
-      dma_tile<K>(dma_pay, dma_ch0, tile, g, lane);
-    }
+    // No workgroup barrier: wave g's quad items and its share of the next
+    // payload tile are the same 8 KiB (cq_read_q, dma_tile_x4), so once its
+    // own reads are back no other wave touches that region.  Measured: encode
+    // 1.646 / 1.648 -> 1.638 / 1.638 ms (-0.6 %, profiles/r04_ab.txt probe 13).
+    // Spreading the DMA pieces over the last cq pass measured +0.3 to +0.7 %.
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (!(kExp & 4)) dma_tile_x4<K>(dma_pay, dma_ch0, tile, g, lane);
   }
   stamp(dbg, st0 + 1);
   const uint32_t row0 = index + 16 * g;
@@ -587,23 +436,15 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
     tower_convert(T, CL, CH);  // transforms run in tower coordinates
     cq_levels<K, true, true, 0, false, kEncPrioCq>(T, VP, 0, g, CL, CH);
     stamp(dbg, 3);
-    if constexpr (kEncQx<K>) {
-      // the quad items overlay payload blocks that other waves read: wait for
-      // every wave's cq_read (cq_write_p writes back only the blocks it read)
-      __syncthreads();
-      cq_write_q(tile, g, lane, CL, CH);
-    } else {
-      cq_write_p<K>(tile, cqb, CL, CH);
-    }
+    // the quad items overlay payload blocks that other waves read: wait for
+    // every wave's cq_read
+    __syncthreads();
+    cq_write_q(tile, g, lane, CL, CH);
   }
   stamp(dbg, 4);
   __syncthreads();
-  const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
   uint32_t ML[16], MH[16];
-  if constexpr (kEncQx<K>)
-    hi_read_q<K>(tile, g, lane, ML, MH);
-  else
-    hi_read_p<K>(tile, hb, ML, MH);
+  hi_read_q<K>(tile, g, lane, ML, MH);
   stamp(dbg, 5);
   hi_levels<K, true, true, 0, 0, kEncPrio>(T, VP, 0, ML, MH);
 #pragma unroll
@@ -614,13 +455,13 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
   const uint8_t* dpay = dma ? pay : nullptr;
   const uint32_t dch0 = next_tl * kTile;
   if (last >= 1)
-    encode_shift<K, 1>(T, a, tile, VP, out, 1, g, lane, ncols, full, cqb, hb, ML, MH, PL, PH,
+    encode_shift<K, 1>(T, a, tile, VP, out, 1, g, lane, ncols, full, ML, MH, PL, PH,
                        last == 1 ? dpay : nullptr, dch0, dbg);
   if (last >= 2)
-    encode_shift<K, 2>(T, a, tile, VP, out, 2, g, lane, ncols, full, cqb, hb, ML, MH, PL, PH,
+    encode_shift<K, 2>(T, a, tile, VP, out, 2, g, lane, ncols, full, ML, MH, PL, PH,
                        last == 2 ? dpay : nullptr, dch0, dbg);
   if (last >= 3)
-    encode_shift<K, 3>(T, a, tile, VP, out, 3, g, lane, ncols, full, cqb, hb, ML, MH, PL, PH, dpay, dch0, dbg);
+    encode_shift<K, 3>(T, a, tile, VP, out, 3, g, lane, ncols, full, ML, MH, PL, PH, dpay, dch0, dbg);
   return dma;
 }
 
@@ -697,14 +538,8 @@ __device__ __forceinline__ uint32_t row_mask16(const uint8_t* pres, uint32_t row
 // and the merge's final read of the systematic rows -- and the default policy
 // for segment 0's systematic rows, which the merge reads again, so that the
 // parity rows do not push them (and the payload's row-table records, re-read
-// by every tile) out of L2.  NP_ROW_STREAM 0: every load default (all-nt
-// measured +0.5 % on the decode in round 1).
-#ifndef NP_ROW_LOAD_CPOL
-#define NP_ROW_LOAD_CPOL 0
-#endif
-#ifndef NP_ROW_STREAM
-#define NP_ROW_STREAM 1
-#endif
+// by every tile) out of L2.  (Every load with the default policy measured
+// +1.5 % on the decode, all-nt +0.5 % in round 1.)
 // Issues the loads of the lane's pieces of rows row0..row0+15; the data is
 // consumed later.  Full tiles: one buffer descriptor per row whose size is 0
 // for an absent row, so that load returns zeros with no HBM traffic and no
@@ -733,10 +568,10 @@ __device__ __forceinline__ void issue_rows_c(uint2 (&raw)[16], const uint8_t* sh
 __device__ __forceinline__ void issue_rows(uint2 (&raw)[16], const uint8_t* sh, size_t shard_len, uint32_t mask,
                                            uint32_t row0, const uint8_t* zeros, uint32_t lane, uint32_t ncols,
                                            bool full, bool reread = false) {
-  if (NP_ROW_STREAM && !reread)
+  if (!reread)
     issue_rows_c<2>(raw, sh, shard_len, mask, row0, zeros, lane, ncols, full);
   else
-    issue_rows_c<NP_ROW_LOAD_CPOL>(raw, sh, shard_len, mask, row0, zeros, lane, ncols, full);
+    issue_rows_c<0>(raw, sh, shard_len, mask, row0, zeros, lane, ncols, full);
 }
 
 // Copy-out straight from the cq registers: lane l holds columns 4l..4l+3 at
@@ -758,11 +593,10 @@ __device__ __forceinline__ void copy_out_cq(uint8_t* out_tile, uint32_t lane, ui
   }
 }
 
-// The merge's systematic rows (4- and 8-segment decodes) load: 0 at the
-// merge, 1 before the forward transform's cq pass, 2 before its high pass.
-#ifndef NP_MERGE_EARLY
-#define NP_MERGE_EARLY 1  // measured: decode 0 to -2 % at config 3 (box to box), -4 % at n/k = 8, k = 64; 2: -0.9 %
-#endif
+// The merge's systematic rows (4- and 8-segment decodes) load before the
+// forward transform's cq pass.  Measured: decode 0 to -2 % at config 3 (box to
+// box), -4 % at n/k = 8, k = 64, against loading them at the merge; before the
+// forward high pass instead: -0.9 %.
 
 // Row loads run one step ahead of their use where the registers allow it
 // (prefixes of up to 2 segments); the 4-segment decode, which keeps more
@@ -770,9 +604,6 @@ __device__ __forceinline__ void copy_out_cq(uint8_t* out_tile, uint32_t lane, ui
 template <int NQ>
 constexpr bool kRowPrefetch = NQ <= 2;
 
-#ifndef NP_REC_IDX0
-#define NP_REC_IDX0 1  // measured: reconstruct -1.1 % (config 3)
-#endif
 // The tables of all NQ segment transforms fit in LDS next to the tile (K = 256:
 // 128 KiB + 4 x 8 KiB of the 160 KiB): staged once per workgroup and kept for
 // all its tiles, instead of two buffers restaged per step.  Measured -1 % to
@@ -780,15 +611,12 @@ constexpr bool kRowPrefetch = NQ <= 2;
 // step's rows by LDS-DMA into a dummy LDS area measured +8 %: vector loads
 // complete in order, so the wait for a step's last row also waited for the
 // prefetch behind it.)
-#ifndef NP_REC_RESIDENT
-#define NP_REC_RESIDENT 1
-#endif
 // Only where it keeps the workgroups per CU (4K threads each, four waves per
 // SIMD): K = 64 / 128 with NQ = 8 would lose one of four / two (measured +24 %
 // / +65 % decode time).
 template <int K, int NQ>
 constexpr bool kRecResident =
-    NP_REC_RESIDENT && NQ > 1 &&
+    NQ > 1 &&
     Geo<K>::kTileBytes + NQ * 4u * Geo<K>::kVPWords <= 160u * 1024u * Geo<K>::kThreads / 1024u;
 // LDS buffer of segment q's tables at decode step `step`.
 template <int K, int NQ>
@@ -839,18 +667,15 @@ __device__ __forceinline__ uint32_t seg_mask(const uint32_t (&msk)[NQ], int step
 // systematic rows (for the merge) on exit.  A runtime loop keeps
 // the kernel small; at index 0 the t = 0 multipliers are the zero element,
 // whose table yields 0 (the reference's skipped multiply).
-// NP_REC_TILE_PREFETCH: the multi-tile decodes that load each step's rows
+// Tile prefetch: the multi-tile decodes that load each step's rows
 // where they use them (NQ >= 4) load the next tile's first-step rows during
 // this tile's copy-out (and the first tile's before the tables are staged), as
 // the 2-segment decode does: at the tile boundary only the rows and the output
 // registers are live.  Measured (profiles/r04_ab.txt): config-3 decode
 // 2.78 -> 2.73 ms (-1.6 %); the 8-segment decode (1200 validators) +0.5 %, so
 // 4 segments only.
-#ifndef NP_REC_TILE_PREFETCH
-#define NP_REC_TILE_PREFETCH 1
-#endif
 template <int K, int NQ>
-constexpr bool kTilePrefetch = NP_REC_TILE_PREFETCH && NQ == 4 && kMultiTile<K>;
+constexpr bool kTilePrefetch = NQ == 4 && kMultiTile<K>;
 
 // PRE0: step 0's rows are in `raw` on entry (kTilePrefetch).
 template <int K, int NQ, bool PRE0 = false>
@@ -929,7 +754,7 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
       issue_rows(raw, (kExp & 32) ? T.zeros : sh, (kExp & 32) ? 0 : shard_len, m, index + 16 * g, T.zeros, c.lane,
                  c.ncols, c.full, q == 0);
     stamp(c.dbg, 2 + 6 * step);
-    if constexpr (kRecPrioSpan) __builtin_amdgcn_s_setprio(NP_PRIO_PREMUL);
+    __builtin_amdgcn_s_setprio(kRecPrioPremul);
     pipelined_rec<16>(
         [&](auto pc) __attribute__((always_inline)) {
           return (cpool_t)(R) + (index + 16 * g + decltype(pc)::value) * kPoolWords;
@@ -987,7 +812,7 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
     // hi levels: gen_of(index) <= 4; segment 0 (index 0) skips the t = 0
     // groups, whose skew is the zero element (15 of the 32 quad multiplies)
     // (the 2-segment decode keeps its rows prefetch live here: no room for two instances)
-    if (NP_REC_IDX0 && NQ == 4 && q == 0)
+    if (NQ == 4 && q == 0)  // -1.1 % (config 3)
       hi_levels<K, true, true, 0, 0, kRecPrioHi>(T, vp, 0, XL, XH);
     else
       hi_levels<K, true, false, 0, 0, kRecPrioHi>(T, vp, index, XL, XH);
@@ -1048,7 +873,7 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
     hi_write<K>(tile, fresh_v(hb), AL, AH);
     __syncthreads();
     stamp(dbg, 28);
-    if constexpr (!kRowPrefetch<NQ> && NP_MERGE_EARLY == 1)  // the merge's rows load during the FFT's cq pass
+    if constexpr (!kRowPrefetch<NQ>)  // the merge's rows load during the FFT's cq pass
       issue_rows(raw, sh, a.shard_len, uniform(msk[NQ - 1]), 16 * g, T.zeros, lane, ncols, full);
     cq_read<K>(tile, fresh_v(cqb), XL, XH);
     cq_levels<K, false, true, 0, false, kRecPrioFwdCq>(T, vp0, 0, g, XL, XH, ~uniform(msk[NQ - 1]));  // erased rows only
@@ -1057,8 +882,6 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
   // ---- merge: received systematic rows, postmultiplied recovered ones
   const uint32_t cqbf = fresh_v(cqb);
   const uint32_t m0 = uniform(msk[NQ == 1 ? 0 : NQ - 1]);  // segment 0 = the last step's
-  if constexpr (!kRowPrefetch<NQ> && NP_MERGE_EARLY != 1)
-    issue_rows(raw, sh, a.shard_len, m0, 16 * g, T.zeros, lane, ncols, full);
   if constexpr (NQ == 1) {
 #pragma unroll
     for (int p = 0; p < 16; ++p) blk_to_quad(raw[p], XL[p], XH[p]);
@@ -1092,7 +915,7 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
   // ---- copy-out: column c of the tile is 2K contiguous bytes of the output
   {
     uint8_t* out = a.out + static_cast<size_t>(pb) * a.out_stride + static_cast<size_t>(col0) * 2 * K;
-    const bool al_o = NP_UNALIGNED || ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 7u) == 0;
+    const bool al_o = true;  // 8-byte stores at any address (rows_vec_ok)
     const uint32_t c0 = tid / G::Q, m0 = tid % G::Q;
     const uint32_t base = col_base<K>(c0) ^ (8u * m0);
 #pragma unroll
@@ -1183,11 +1006,9 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
     // row offsets, sizes and descriptors derived from them out of the tile loop
     // and keeps them live in (spilled) registers across it
     const uint32_t g = fresh(g0);
-#if NP_REC_TID_SPILL  // experiment: the round-4 form, whose tid0 stayed live across tiles (spilled)
-    const uint32_t tid = fresh_v(tid0), lane = tid & 63u;
-#else
+    // (a copy of threadIdx.x kept across the tile loop was the kernel's one
+    // spilled VGPR, and its reload waited with vmcnt(0) for every load in flight)
     const uint32_t lane = lane_fresh(), tid = 64u * g + lane;
-#endif
     const uint32_t cqb = col_base<K>(4 * lane) ^ (32u * g);
     const size_t shard_len = fresh(a.shard_len);
     uint32_t msk[NQ];
@@ -1220,15 +1041,13 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
       // ---- forward transform of size K at index 0
       const uint32_t* vp0 = VP + vp_slot<K, NQ>(0, NQ - 1) * G::kVPWords;  // segment 0's tables = FFT(K, 0)'s
       stamp(dbg, 26);
-      if constexpr (!kRowPrefetch<NQ> && NP_MERGE_EARLY == 2)  // the merge's rows load during the FFT
-        issue_rows(raw, sh, shard_len, uniform(msk[NQ - 1]), 16 * g, T.zeros, lane, ncols, full);
       hi_levels<K, false, true, 0, 0, kRecPrioFwdHi>(T, vp0, 0, AL, AH);
       stamp(dbg, 27);
       __syncthreads();
       hi_write<K>(tile, fresh_v(hb), AL, AH);
       __syncthreads();
       stamp(dbg, 28);
-      if constexpr (!kRowPrefetch<NQ> && NP_MERGE_EARLY == 1)  // the merge's rows load during the FFT's cq pass
+      if constexpr (!kRowPrefetch<NQ>)  // the merge's rows load during the FFT's cq pass
         issue_rows(raw, sh, shard_len, uniform(msk[NQ - 1]), 16 * g, T.zeros, lane, ncols, full);
       cq_read<K>(tile, fresh_v(cqb), XL, XH);
       cq_levels<K, false, true, 0, false, kRecPrioFwdCq>(T, vp0, 0, g, XL, XH, ~uniform(msk[NQ - 1]));  // erased rows only
@@ -1237,7 +1056,6 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
     // ---- merge: received systematic rows, postmultiplied recovered ones
     const uint32_t cqbf = fresh_v(cqb);
     const uint32_t m0 = uniform(msk[NQ == 1 ? 0 : NQ - 1]);  // segment 0 = the last step's
-    if constexpr (!kRowPrefetch<NQ> && !NP_MERGE_EARLY) issue_rows(raw, sh, shard_len, m0, 16 * g, T.zeros, lane, ncols, full);
     if constexpr (NQ == 1) {
 #pragma unroll
       for (int p = 0; p < 16; ++p) blk_to_quad(raw[p], XL[p], XH[p]);
@@ -1282,7 +1100,7 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
     // ---- copy-out: column c of the tile is 2K contiguous bytes of the output
     {
       uint8_t* out = a.out + static_cast<size_t>(pb) * a.out_stride + static_cast<size_t>(col0) * 2 * K;
-      const bool al_o = NP_UNALIGNED || ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 7u) == 0;
+      const bool al_o = true;  // 8-byte stores at any address (rows_vec_ok)
       const uint32_t c0 = tid / G::Q, q0 = tid % G::Q;
       const uint32_t base = col_base<K>(c0) ^ (8u * q0);
 #pragma unroll

@@ -45,12 +45,10 @@
 namespace np {
 namespace {
 
-// NP_PRIO_HUGE (experiment; bit 0 the encode, bit 1 the decode): progress-based
-// issue priority in the sub-transforms' passes (fast_common.hpp progress_prio).
-#ifndef NP_PRIO_HUGE
-#define NP_PRIO_HUGE 0
-#endif
-constexpr int kHugePrioEnc = NP_PRIO_HUGE & 1, kHugePrioDec = (NP_PRIO_HUGE >> 1) & 1;
+// Age order (no s_setprio) in the sub-transforms' passes: progress-based
+// priority (fast_common.hpp progress_prio) measured neutral at 10000
+// validators (profiles/r04_ab.txt probe 23).
+constexpr int kHugePrioEnc = 0, kHugePrioDec = 0;
 
 constexpr int kSK = 1024;                             // sub-transform size
 constexpr uint32_t kSlotBytes = 16u * 1024u * 8u;     // one sub-segment of a tile in thread order

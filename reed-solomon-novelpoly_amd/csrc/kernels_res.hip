@@ -6,22 +6,14 @@
 namespace np {
 namespace {
 
-// NP_PRIO_RES (bit 0 the encode, bit 1 the decode): progress-based issue
-// priority in every transform pass of the resident kernels (fast_common.hpp
-// progress_prio).  Measured (profiles/r04_ab.txt probe 23): config-4 encode
-// 2.545 / 2.550 -> 2.422 / 2.424 ms, reconstruct 4.376 / 4.381 -> 4.168 /
-// 4.166 ms (-4.8 % each); 2000 validators (k = 512) reconstruct -4.3 %,
-// encode unchanged.  (The huge kernels' sub-transforms, NP_PRIO_HUGE,
-// measured neutral at 10000 validators.)
-#ifndef NP_PRIO_RES
-#define NP_PRIO_RES 3
-#endif
-// Bit 2 (experiment): in the decode steps, one schedule over the span from the
-// row tables' barrier to the CQ write's: the premultiply at 3 then 2, the CQ
-// levels 1, 1, 0, 0.  Measured +2.4 % at config 4 (probe 24): not the default.
-constexpr bool kResPrioSpan = (NP_PRIO_RES & 4) != 0;
-constexpr int kResPrioEnc = NP_PRIO_RES & 1, kResPrioDec = (NP_PRIO_RES >> 1) & 1;
-constexpr int kResPrioDecCq = kResPrioSpan ? 3 : kResPrioDec;
+// Progress-based issue priority in every transform pass of the resident
+// kernels (fast_common.hpp progress_prio).  Measured (profiles/r04_ab.txt
+// probe 23): config-4 encode 2.545 / 2.550 -> 2.422 / 2.424 ms, reconstruct
+// 4.376 / 4.381 -> 4.168 / 4.166 ms (-4.8 % each); 2000 validators (k = 512)
+// reconstruct -4.3 %, encode unchanged.  (One schedule over each decode step's
+// span from the row tables' barrier to the CQ write, as the fast decode has,
+// measured +2.4 % at config 4, probe 24.)
+constexpr int kResPrioEnc = 1, kResPrioDec = 1, kResPrioDecCq = 1;
 
 // ---------------------------------------------------------------- encode ----
 // One workgroup: 64 chunks of one payload.  mod.rs:144-154 /
@@ -124,14 +116,11 @@ __device__ __forceinline__ void rstamp(uint64_t* dbg, int slot) {
 template <int K, int NQ>
 constexpr bool kRecDeltaST = !(K == 1024 && NQ == 8);
 
-// NP_RES_TABLE_DMA: a segment step's row tables arrive by LDS-DMA issued
-// during the previous step's HD levels and fold (dma_row_tables), instead of
-// by loads and LDS writes between two barriers at the start of the step.
-// Measured: config-4 decode 4.37 / 4.38 ms on, 4.37 / 4.36 off (noise,
-// profiles/r04_ab.txt); kept on, it leaves the step start to the row loads.
-#ifndef NP_RES_TABLE_DMA
-#define NP_RES_TABLE_DMA 1
-#endif
+// A segment step's row tables arrive by LDS-DMA issued during the previous
+// step's HD levels and fold (dma_row_tables), instead of by loads and LDS
+// writes between two barriers at the start of the step.  Measured: config-4
+// decode 4.37 / 4.38 ms with, 4.37 / 4.36 without (noise, profiles/r04_ab.txt);
+// kept, it leaves the step start to the row loads.
 
 template <int NQ>
 __host__ __device__ constexpr int res_seg(int step) {  // segments 2, 3, 1, 0 (NQ = 4); 1, 0 (NQ = 2); 7..0 (NQ = 8)
@@ -157,30 +146,17 @@ __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructAr
   {
     const uint32_t pm = lane_rows_present(pres, I, rr);
     uint2 raw[8];
-    if constexpr (NP_RES_TABLE_DMA) {
-      // this step's tables were issued by LDS-DMA during the previous step
-      // (res_decode_tile for step 0): wait for this wave's pieces before the
-      // row loads queue behind them, then for every wave's
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      load_lane_rows<8>(raw, sh, a.shard_len, I, pm, rr, ncols, full, T.zeros, 0);
-      __syncthreads();
-    } else {
-      load_lane_rows<8>(raw, sh, a.shard_len, I, pm, rr, ncols, full, T.zeros, 0);
-      __syncthreads();  // the previous step's HD read is done with the tile
-      stage_row_tables(tile, pools, pres, I, rr.tid, false);
-      __syncthreads();
-    }
+    // this step's tables were issued by LDS-DMA during the previous step
+    // (res_decode_tile for step 0): wait for this wave's pieces before the
+    // row loads queue behind them, then for every wave's
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    load_lane_rows<8>(raw, sh, a.shard_len, I, pm, rr, ncols, full, T.zeros, 0);
+    __syncthreads();
     rstamp(dbg, s0);
     // premultiply by the row multipliers (inc_reconstruct.rs:72-74; Cantor
     // in, tower out), in two halves of 8 rows (register pressure)
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
-      if constexpr (kResPrioSpan) {
-        if (half == 0)
-          __builtin_amdgcn_s_setprio(3);
-        else
-          __builtin_amdgcn_s_setprio(2);
-      }
       if (half == 1) load_lane_rows<8>(raw, sh, a.shard_len, I, pm, rr, ncols, full, T.zeros, 8);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -215,7 +191,7 @@ __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructAr
   rh_write<kHA>(tile, fresh_v(rr.hab), XL, XH);
   __syncthreads();
   rh_read<kHD>(tile, fresh_v(rr.hdb), XL, XH);
-  if constexpr (NP_RES_TABLE_DMA && STEP + 1 < NQ) {
+  if constexpr (STEP + 1 < NQ) {
     __syncthreads();  // every wave has read the tile: the next step's tables may land in it
     dma_row_tables(tile, pools, static_cast<uint32_t>(res_seg<NQ>(STEP + 1)) * K, K, rr.w, rr.l, K / 64);
   }
@@ -282,7 +258,7 @@ __device__ __forceinline__ void res_decode_tile(const DevTables& T, const Recons
   uint32_t* DL = reinterpret_cast<uint32_t*>(tile + RGeo<K>::kTileBytes);  // CQ delta tables
   uint32_t* VS = DL + kDeltaWords;                                      // RStage blocks 0..NQ-1
   rstamp(dbg, 0);
-  if constexpr (NP_RES_TABLE_DMA) {  // the first step's row tables (the tile is free at the start)
+  {  // the first step's row tables (the tile is free at the start)
     const Res r0 = res_coords<K>();
     dma_row_tables(tile, pools, static_cast<uint32_t>(res_seg<NQ>(0)) * K, K, r0.w, r0.l, K / 64);
   }
@@ -317,7 +293,7 @@ __device__ __forceinline__ void res_decode_tile(const DevTables& T, const Recons
   rh_write<kHA>(tile, fresh_v(r.hab), AL, AH);
   __syncthreads();
   rcq_read<K>(tile, fresh_v(r.cqb), AL, AH);
-  if constexpr (NP_RES_TABLE_DMA) {  // the merge's tables land during the FFT's CQ levels
+  {  // the merge's tables land during the FFT's CQ levels
     __syncthreads();  // every wave has read the tile
     dma_row_tables(tile, pools, 0, K, r.w, r.l, K / 64);
   }
@@ -328,16 +304,9 @@ __device__ __forceinline__ void res_decode_tile(const DevTables& T, const Recons
   // (inc_reconstruct.rs:46-50, :82-84; tower in, Cantor out)
   const uint32_t pm = lane_rows_present(pres, 0, r);
   uint2 raw[16];
-  if constexpr (NP_RES_TABLE_DMA) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's table pieces
-    load_lane_rows(raw, sh, a.shard_len, 0, pm, r, ncols, full, T.zeros);
-    __syncthreads();  // every wave's
-  } else {
-    load_lane_rows(raw, sh, a.shard_len, 0, pm, r, ncols, full, T.zeros);
-    __syncthreads();  // every wave has read the tile
-    stage_row_tables(tile, pools, pres, 0, r.tid, true);
-    __syncthreads();
-  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's table pieces
+  load_lane_rows(raw, sh, a.shard_len, 0, pm, r, ncols, full, T.zeros);
+  __syncthreads();  // every wave's
   rstamp(dbg, 45);
 #pragma unroll
   for (int i = 0; i < 16; ++i) {

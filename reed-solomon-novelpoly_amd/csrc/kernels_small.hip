@@ -148,7 +148,7 @@ __device__ __forceinline__ void store_rows_k(uint8_t* out, size_t shard_len, uin
       const uint2 v = cq_row(lo(Q[p]), hi(Q[p]));
       if (nt)
         __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, r, 8u * lane, static_cast<uint32_t>(p * shard_len),
-                                              NP_ROW_STORE_CPOL);
+                                              kRowStoreCpol);
       else
         __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, r, 8u * lane, static_cast<uint32_t>(p * shard_len), 0);
       __builtin_amdgcn_sched_barrier(0);  // one row at a time: no K rows of temporaries
@@ -435,7 +435,7 @@ __global__ __launch_bounds__(256) void k_reconstruct_small(DevTables T, Reconstr
   // ---- copy-out: column c of the tile is 2K contiguous output bytes
   uint8_t* out = a.out + static_cast<size_t>(pb) * a.out_stride + static_cast<size_t>(col0) * 2 * K;
   const bool al16 = full && out_vec_ok(a.out, a.out_stride);
-  const bool al8 = NP_UNALIGNED || ((reinterpret_cast<uintptr_t>(a.out) | a.out_stride) & 7u) == 0;
+  const bool al8 = true;  // 8-byte stores at any address (rows_vec_ok)
   if constexpr (K < 8) {  // k in {1, 2, 4}: 2K output bytes per column
     uint64_t Q4[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -520,19 +520,13 @@ hipError_t reconstruct_by_nq(const DevTables& T, const ReconstructArgs& a, hipSt
 
 }  // namespace
 
-// NP_SMALL_MINK (experiment builds only): the smallest k served here; below
-// it the generic kernels run (tools/records: the generic path's rate at 2-21
-// validators for comparison).
-#ifndef NP_SMALL_MINK
-#define NP_SMALL_MINK 1
-#endif
 bool small_encode_supported(uint32_t n, uint32_t k) {
-  return (k == 1 || k == 2 || k == 4 || k == 8 || k == 16 || k == 32) && k >= NP_SMALL_MINK && n >= 2 * k &&
+  return (k == 1 || k == 2 || k == 4 || k == 8 || k == 16 || k == 32) && n >= 2 * k &&
          n <= kSmallMaxSeg * k;
 }
 
 bool small_reconstruct_supported(uint32_t n, uint32_t k) {
-  return (k == 1 || k == 2 || k == 4 || k == 8 || k == 16 || k == 32) && k >= NP_SMALL_MINK &&
+  return (k == 1 || k == 2 || k == 4 || k == 8 || k == 16 || k == 32) &&
          (n == 2 * k || n == 4 * k || n == 8 * k);
 }
 

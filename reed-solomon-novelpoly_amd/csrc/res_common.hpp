@@ -699,7 +699,7 @@ __device__ __forceinline__ void rres_store_rows(uint8_t* out, size_t shard_len, 
       for (int i = 0; i < 16; ++i) {
         const uint2 v = cq_row(L[i], H[i]);
         __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, rs, vo, static_cast<uint32_t>(i * shard_len),
-                                              NP_ROW_STORE_CPOL);
+                                              kRowStoreCpol);
       }
     } else {
 #pragma unroll

@@ -27,6 +27,33 @@ e2e() {  # PCIe-inclusive host-pipeline rates, configs 3 and 4
   done
 }
 
+cfgs() {  # configs 2 and 4 bench lines
+  for c in 2 4; do
+    timeout -k 10 300 python bench.py --config $c --steps 5 --warmup 2 --no-cpu > gpurun_out/r05/bench_$1_cfg$c.log 2>&1 || exit $?
+    tail -1 gpurun_out/r05/bench_$1_cfg$c.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('cfg$c', d['value'], {k:(v['ms'],v['frac']) for k,v in d['kernels'].items()})"
+  done
+}
+
+p2() {  # experiment switches pruned (code objects unchanged but for dead code): suite, benches
+  suite p2 && bench p2 && bench p2b && cfgs p2
+}
+
+ab() {  # A/B of libraries on one box: ab TAG CONFIG LIB... (product = "prod"); two passes each
+  tag=$1; cfg=$2; shift 2
+  for pass in 1 2; do
+    for lib in "$@"; do
+      path=$PWD/reed-solomon-novelpoly_amd/lib/libnovelpoly_hip.so
+      [ "$lib" != prod ] && path=$PWD/tools/exp/lib_$lib.so
+      NP_LIB_PATH=$path timeout -k 10 300 python bench.py --config $cfg --steps 10 --warmup 3 --no-cpu > gpurun_out/r05/ab_${tag}_${lib}_$pass.log 2>&1 || exit $?
+      tail -1 gpurun_out/r05/ab_${tag}_${lib}_$pass.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$tag cfg$cfg $lib pass$pass', d['value'], {k:v['ms'] for k,v in d['kernels'].items()})"
+    done
+  done
+}
+
+p3() {  # pruned library against round 4's at configs 2, 3, 4
+  ab p3 2 prod r04 && ab p3 3 prod r04 && ab p3 4 prod r04
+}
+
 p1() {  # the host-pipeline fix: whole suite, smoke, bench, e2e
   suite p1 && bench p1 && e2e p1
 }
