@@ -54,6 +54,11 @@ p3() {  # pruned library against round 4's at configs 2, 3, 4
   ab p3 2 prod r04 && ab p3 3 prod r04 && ab p3 4 prod r04
 }
 
+micro() {  # bit-slicing microbenchmark
+  timeout -k 10 180 ./tools/microbench/bitslice > gpurun_out/r05/bitslice.txt 2>&1 || exit $?
+  cat gpurun_out/r05/bitslice.txt
+}
+
 p1() {  # the host-pipeline fix: whole suite, smoke, bench, e2e
   suite p1 && bench p1 && e2e p1
 }
