@@ -59,6 +59,35 @@ micro() {  # bit-slicing microbenchmark
   cat gpurun_out/r05/bitslice.txt
 }
 
+hugeprof() {  # kernel-trace stats of the sub-transform path at 20,000 / 40,000 / 65,536 validators
+  export TMPDIR=/tmp
+  for vc in ${VCS:-65536 40000 20000}; do
+    out=$PWD/gpurun_out/r05/prof_huge_$vc
+    mkdir -p $out
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out --output-format csv -- python3 bench.py --no-cpu --steps 3 --warmup 1 --batch 512 --n-wanted $vc --erase $(( (vc - 1) / 3 + 1 )) > $out/bench.log 2>&1 || exit $?
+    tail -1 $out/bench.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('vc$vc', d['value'], {k:v['ms'] for k,v in d['kernels'].items()})"
+    f=$(find $out -name "*kernel_stats.csv" | head -1)
+    python3 -c "
+import csv,sys
+rows=list(csv.DictReader(open('$f')))
+for r in sorted(rows, key=lambda r: -float(r['TotalDurationNs']))[:14]:
+    print('  %-70s calls %5s avg %9.1f us total %8.2f ms' % (r['Name'][:70], r['Calls'], float(r['AverageNs'])/1e3, float(r['TotalDurationNs'])/1e6))"
+  done
+}
+
+slices() {  # sub-transform path: batch slice size (NP_HUGE_SLICE_MB) against the Infinity Cache
+  for vc in ${VCS:-65536 40000 20000}; do
+    for mb in ${MBS:-2048 512 256 128 64}; do
+      NP_HUGE_SLICE_MB=$mb timeout -k 10 300 python bench.py --no-cpu --steps 3 --warmup 1 --batch 512 --n-wanted $vc --erase $(( (vc - 1) / 3 + 1 )) > gpurun_out/r05/slice_${vc}_$mb.log 2>&1 || exit $?
+      tail -1 gpurun_out/r05/slice_${vc}_$mb.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('vc$vc slice ${mb}MB', d['value'], {k:v['ms'] for k,v in d['kernels'].items()})"
+    done
+  done
+}
+
+p4() {  # sub-transform path: kernel profile, then the slice sweep
+  hugeprof && MBS="2048 256 128" slices
+}
+
 p1() {  # the host-pipeline fix: whole suite, smoke, bench, e2e
   suite p1 && bench p1 && e2e p1
 }
