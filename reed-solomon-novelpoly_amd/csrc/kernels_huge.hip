@@ -62,6 +62,9 @@ struct HugeArgs {
   const uint16_t* loc;  // reconstruct: locators, batch x n (log form)
   const uint8_t* mode;  // reconstruct: per payload kHugeSkip / kHugeCopy / kHugeDecode
   uint32_t tiles, slots, M, K, NQ;
+  // encode, payloads of at most 32 columns: a tile holds two payloads
+  // (columns 0-31 payload 2 pb, 32-63 payload 2 pb + 1; load_pay_tile_pair)
+  uint32_t pair;
   // this launch's sub-transforms: u0 .. u0 + (grid / per) - 1 (index 1024 u,
   // slot u; all of one res_gen), per = batch x tiles workgroups each
   uint32_t u0, per;
@@ -141,20 +144,42 @@ __device__ __forceinline__ void top_forward_h(const DevTables& T, uint2 (&y)[M],
 }
 
 // ---------------------------------------------------------------- encode ----
+// Shard rows I .. I + 1023 of the workgroup's tile from CQ registers: tile
+// (pb, columns ch0 ..), or the two payloads 2 pb, 2 pb + 1 of a paired tile.
+__device__ __forceinline__ void huge_store_rows(const EncodeArgs& a, const HugeArgs& h, uint32_t pb, uint32_t ch0,
+                                                uint32_t I, const uint32_t (&L)[16], const uint32_t (&H)[16],
+                                                const Res& r, uint32_t ncols, bool full, bool nt) {
+  if (h.pair) {
+    uint8_t* o0 = a.shards + static_cast<size_t>(2 * pb) * a.batch_stride;
+    uint8_t* o1 = 2 * pb + 1 < a.batch ? o0 + a.batch_stride : nullptr;
+    rres_store_rows_pair(o0, o1, a.shard_len, I, a.wanted_n, L, H, r, ncols);
+  } else {
+    rres_store_rows(a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(ch0), a.shard_len,
+                    I, a.wanted_n, L, H, r, ncols, full, nt);
+  }
+}
+
 template <int GEN>
 __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k_huge_enc_inv(
     DevTables T, EncodeArgs a, HugeArgs h, uint32_t nchunks) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
-  const SubRef sr = sub_of(h, blockIdx.x, a.batch);
+  const SubRef sr = sub_of(h, blockIdx.x, h.pair ? (a.batch + 1) / 2 : a.batch);
   const uint32_t pb = sr.pb, tl = sr.tl, ch0 = tl * kRC;
   const uint32_t ncols = min(static_cast<uint32_t>(kRC), nchunks - ch0);
   const uint32_t I = kSK * sr.u;  // sub-segment u of IFFT(k, 0)
   const Res r = res_coords<kSK>();
   const bool full = ncols == kRC && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
   const bool nt = rows_nt(a.shards, a.batch_stride, a.shard_len);
-  load_pay_tile<kSK>(tile, a.payloads + static_cast<size_t>(pb) * a.payload_stride, a.payload_len, ch0,
-                     2 * static_cast<size_t>(h.K), 2 * static_cast<size_t>(I), r.tid);
+  if (h.pair) {
+    const bool two = 2 * pb + 1 < a.batch;
+    load_pay_tile_pair<kSK>(tile, a.payloads + static_cast<size_t>(2 * pb) * a.payload_stride,
+                            two ? a.payloads + static_cast<size_t>(2 * pb + 1) * a.payload_stride : nullptr,
+                            a.payload_len, 2 * static_cast<size_t>(h.K), 2 * static_cast<size_t>(I), r.tid);
+  } else {
+    load_pay_tile<kSK>(tile, a.payloads + static_cast<size_t>(pb) * a.payload_stride, a.payload_len, ch0,
+                       2 * static_cast<size_t>(h.K), 2 * static_cast<size_t>(I), r.tid);
+  }
   uint32_t* DL = reinterpret_cast<uint32_t*>(smem + RGeo<kSK>::kTileBytes);
   uint32_t* VS = DL + kDeltaWords;
   stage_delta_tables(T, DL);
@@ -163,8 +188,7 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
   __syncthreads();
   uint32_t L[16], H[16];
   rcq_read_nat<kSK>(tile, r.cqb, L, H);
-  rres_store_rows(a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(ch0), a.shard_len, I,
-                  a.wanted_n, L, H, r, ncols, full, nt);
+  huge_store_rows(a, h, pb, ch0, I, L, H, r, ncols, full, nt);
   tower_convert(T, L, H);
   rcq_levels<true, GEN, true, kHugePrioEnc>(T, I, r, L, H, DL);
   __syncthreads();  // every wave has read its payload blocks
@@ -210,7 +234,7 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
     DevTables T, EncodeArgs a, HugeArgs h, uint32_t nchunks) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
-  const SubRef sr = sub_of(h, blockIdx.x, a.batch);
+  const SubRef sr = sub_of(h, blockIdx.x, h.pair ? (a.batch + 1) / 2 : a.batch);
   const uint32_t pb = sr.pb, tl = sr.tl, ch0 = tl * kRC;
   const uint32_t ncols = min(static_cast<uint32_t>(kRC), nchunks - ch0);
   const uint32_t I = kSK * sr.u;  // shift u / M, sub-segment u % M
@@ -236,8 +260,7 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
   qi_cq<false>(tile, qc, L, H);
   rcq_levels<false, GEN, true, kHugePrioEnc>(T, I, r, L, H, DL);
   tower_convert(T, L, H);  // back to Cantor coordinates for the shard rows
-  rres_store_rows(a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(ch0), a.shard_len, I,
-                  a.wanted_n, L, H, r, ncols, full, nt);
+  huge_store_rows(a, h, pb, ch0, I, L, H, r, ncols, full, nt);
 }
 
 // ----------------------------------------------------------- reconstruct ----
@@ -491,6 +514,15 @@ hipError_t with_nq(uint32_t NQ, F&& f) {
   }
 }
 
+// NP_HUGE_PAIR=0 (experiment knob, read once): one payload per tile always.
+bool huge_pair_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("NP_HUGE_PAIR");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 HugeArgs huge_args(uint8_t* scr, uint32_t n, uint32_t k, size_t tiles, uint32_t slots) {
   HugeArgs h{};
   h.scr = scr;
@@ -537,11 +569,14 @@ hipError_t launch_encode_huge(const DevTables& T, const EncodeArgs& a, uint8_t* 
   if (nchunks == 0 || a.batch == 0) return hipSuccess;
   if (nchunks > 0xffffffffu) return hipErrorInvalidValue;
   const size_t tiles = (nchunks + kRC - 1) / kRC;
-  const size_t per = a.batch * tiles;
+  // payloads of at most 32 columns (k = 16384 at 1 MiB): two per tile
+  const bool pair = huge_pair_enabled() && nchunks <= kRC / 2 && a.batch > 1;
+  const size_t per = pair ? (a.batch + 1) / 2 : a.batch * tiles;
   if (per * (a.n / kSK) > 0x7fffffffu) return hipErrorInvalidValue;
   const uint32_t nc = static_cast<uint32_t>(nchunks);
   HugeArgs h = huge_args(scratch, a.n, a.k, tiles, a.n / kSK);
   h.per = static_cast<uint32_t>(per);
+  h.pair = pair ? 1u : 0u;
   auto grid = [&](uint32_t u0, uint32_t u1) { return static_cast<uint32_t>(per * (u1 - u0)); };
   hipError_t e = for_gen_ranges(0, h.M, [&](auto g, uint32_t u0, uint32_t u1) {
     h.u0 = u0;

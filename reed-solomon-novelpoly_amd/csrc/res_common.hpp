@@ -680,6 +680,34 @@ __device__ __forceinline__ void load_pay_tile(uint8_t* tile, const uint8_t* pay,
   }
 }
 
+// Two payloads in one tile (kernels_huge.hip, payloads of at most 32 columns:
+// k = 16384 at 1 MiB): columns 0..31 are chunks 0..31 of pay0, columns
+// 32..63 chunks 0..31 of pay1 (nullptr: the batch ended, zeros).  Bytes past
+// payload_len, and chunks past the payload's last, are zeros as in
+// load_pay_tile.
+template <int K>
+__device__ __forceinline__ void load_pay_tile_pair(uint8_t* tile, const uint8_t* pay0, const uint8_t* pay1,
+                                                   size_t payload_len, size_t chunk_bytes, size_t off, uint32_t tid) {
+  const uint32_t m = tid % (K / 4), c0 = tid / (K / 4);
+#pragma unroll 1
+  for (uint32_t i = 0; i < 16; ++i) {
+    const uint32_t c = c0 + 4u * i;
+    const uint8_t* pay = c < 32u ? pay0 : pay1;
+    const size_t g0 = static_cast<size_t>(c & 31u) * chunk_bytes + off + 8u * m;
+    uint2 v = make_uint2(0, 0);
+    if (pay && g0 + 8 <= payload_len) {
+      v = load_once(pay + g0);
+    } else if (pay) {
+      uint32_t wv[2] = {0, 0};
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (g0 + e < payload_len) wv[e >> 2] |= static_cast<uint32_t>(pay[g0 + e]) << (8 * (e & 3));
+      v = make_uint2(wv[0], wv[1]);
+    }
+    *reinterpret_cast<uint2*>(tile + pq_addr<K>(c, m)) = v;
+  }
+}
+
 // ------------------------------------------------------------ shard rows ----
 
 // This lane's 8 bytes (columns 4 cq .. 4 cq + 3) of shard rows
@@ -714,6 +742,28 @@ __device__ __forceinline__ void rres_store_rows(uint8_t* out, size_t shard_len, 
   for (int i = 0; i < 16; ++i) {
     const uint32_t row = rb + 16u * r.u + i;
     if (row < wanted_n) store4(out + static_cast<size_t>(row) * shard_len, cq_row(L[i], H[i]), r.cq, ncols, full);
+  }
+}
+
+// The same for a tile of two payloads (load_pay_tile_pair): lane 16 u + cq
+// stores columns 4 (cq & 7) .. + 3 of payload cq >> 3 (out0 / out1 = row 0,
+// column 0 of each; nullptr: none), ncols columns each.
+__device__ __forceinline__ void rres_store_rows_pair(uint8_t* out0, uint8_t* out1, size_t shard_len, uint32_t row0,
+                                                     uint32_t wanted_n, const uint32_t (&L)[16], const uint32_t (&H)[16],
+                                                     const Res& r, uint32_t ncols) {
+  uint8_t* out = r.cq < 8u ? out0 : out1;
+  if (!out) return;
+  const uint32_t lc = r.cq & 7u, rb = row0 + 64u * r.w + 16u * r.u;
+  const bool whole = 4u * lc + 4u <= ncols;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if (rb + i >= wanted_n) break;
+    uint8_t* rowp = out + static_cast<size_t>(rb + i) * shard_len;
+    const uint2 v = cq_row(L[i], H[i]);
+    if (whole)
+      *reinterpret_cast<uint2*>(rowp + 8u * lc) = v;
+    else
+      store4(rowp, v, lc, ncols, false);
   }
 }
 

@@ -56,3 +56,36 @@ def test_huge_reconstruct(gpu, oracle, nw, kw, plen, erase):
     st, want = oracle.reconstruct(recv, n, k)
     assert st == 0 and got == want
     assert got[:plen] == pl
+
+
+# k = 16384 payloads of at most 32 columns: the sub-transform encode packs two
+# payloads into one 64-column tile (kernels_huge.hip HugeArgs::pair): odd and
+# even batches (the last tile half empty), whole and partial 32-column halves,
+# wanted_n < n; every payload against the oracle.
+PAIR = [(65536, 21846, 2 * 16384 * 32, 4), (65536, 21846, 2 * 16384 * 17 + 3, 3), (50000, 16667, 2 * 16384 * 5, 5)]
+
+
+@pytest.mark.parametrize("nw,kw,plen,batch", PAIR)
+def test_huge_encode_paired_batch(gpu, oracle, nw, kw, plen, batch):
+    import torch
+
+    p = npa.CodeParams.derive_parameters(nw, kw)
+    n, k = p.n(), p.k()
+    assert k == 16384
+    sl = p.make_encoder(gpu).shard_len(plen)
+    assert sl // 2 <= 32
+    pls = np.stack([np.frombuffer(synth.payload(nw + plen + b, plen), np.uint8) for b in range(batch)])
+    dp = torch.from_numpy(pls).cuda()
+    bstride = nw * sl + 6
+    ds = torch.full((batch, bstride), 0xA5, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    npa.encode_batch_dev(p, dp.data_ptr(), plen, plen, batch, ds.data_ptr(), bstride, ctx=gpu,
+                         stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    hs = ds.cpu().numpy()
+    for b in range(batch):
+        st, want = oracle.encode(pls[b].tobytes(), n, k, nw)
+        assert st == 0
+        bad = [v for v in range(nw) if hs[b, v * sl:(v + 1) * sl].tobytes() != want[v]]
+        assert not bad, (b, len(bad), bad[:5])
+        assert (hs[b, nw * sl:] == 0xA5).all()

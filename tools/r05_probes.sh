@@ -88,6 +88,18 @@ p4() {  # sub-transform path: kernel profile, then the slice sweep
   hugeprof && MBS="2048 256 128" slices
 }
 
+p5() {  # paired sub-transform encode: huge tests, then 65,536 / 50,000 validators with and without pairing
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_huge.py tests/test_gpu_noncodeword.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r05/pytest_huge_p5.log 2>&1; rc=$?
+  echo "huge tests: $(tail -1 gpurun_out/r05/pytest_huge_p5.log)"
+  [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r05/pytest_huge_p5.log | head -20; exit $rc; }
+  for vc in 65536 50000; do
+    for pr in 1 0; do
+      NP_HUGE_PAIR=$pr timeout -k 10 300 python bench.py --no-cpu --steps 3 --warmup 1 --batch 512 --n-wanted $vc --erase $(( (vc - 1) / 3 + 1 )) > gpurun_out/r05/pair_${vc}_$pr.log 2>&1 || exit $?
+      tail -1 gpurun_out/r05/pair_${vc}_$pr.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('vc$vc pair=$pr', d['value'], {k:v['ms'] for k,v in d['kernels'].items()}, d.get('roundtrip_ok'))"
+    done
+  done
+}
+
 p1() {  # the host-pipeline fix: whole suite, smoke, bench, e2e
   suite p1 && bench p1 && e2e p1
 }
