@@ -65,6 +65,7 @@ struct HugeArgs {
   // encode, payloads of at most 32 columns: a tile holds two payloads
   // (columns 0-31 payload 2 pb, 32-63 payload 2 pb + 1; load_pay_tile_pair)
   uint32_t pair;
+  uint32_t batch;  // payloads of the slice
   // this launch's sub-transforms: u0 .. u0 + (grid / per) - 1 (index 1024 u,
   // slot u; all of one res_gen), per = batch x tiles workgroups each
   uint32_t u0, per;
@@ -79,6 +80,19 @@ __device__ __forceinline__ SubRef sub_of(const HugeArgs& h, uint32_t b, size_t b
   return SubRef{u, tr.pb, tr.tl};
 }
 constexpr uint8_t kHugeSkip = 0, kHugeCopy = 1, kHugeDecode = 2;
+// Mode of tile pt's payload; a paired tile (HugeArgs::pair) runs the larger
+// of its two payloads' modes (decode > copy > skip).
+__device__ __forceinline__ uint32_t tile_mode(const HugeArgs& h, size_t pt) {
+  if (!h.pair) return h.mode[pt / h.tiles];
+  const uint32_t m0 = h.mode[2 * pt];
+  const uint32_t m1 = 2 * pt + 1 < h.batch ? h.mode[2 * pt + 1] : kHugeSkip;
+  return m0 > m1 ? m0 : m1;
+}
+// The units a launch's workgroups enumerate per sub-transform: tiles, or
+// pairs of payloads.
+__device__ __forceinline__ uint32_t unit_count(const HugeArgs& h, uint32_t batch) {
+  return h.pair ? (batch + 1) / 2 : batch;
+}
 
 __device__ __forceinline__ uint8_t* slot_at(const HugeArgs& h, uint32_t pb, uint32_t tl, uint32_t slot) {
   return h.scr + (static_cast<size_t>(pb) * h.tiles + tl) * h.slots * kSlotBytes + static_cast<size_t>(slot) * kSlotBytes;
@@ -164,7 +178,7 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
     DevTables T, EncodeArgs a, HugeArgs h, uint32_t nchunks) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
-  const SubRef sr = sub_of(h, blockIdx.x, h.pair ? (a.batch + 1) / 2 : a.batch);
+  const SubRef sr = sub_of(h, blockIdx.x, unit_count(h, a.batch));
   const uint32_t pb = sr.pb, tl = sr.tl, ch0 = tl * kRC;
   const uint32_t ncols = min(static_cast<uint32_t>(kRC), nchunks - ch0);
   const uint32_t I = kSK * sr.u;  // sub-segment u of IFFT(k, 0)
@@ -234,7 +248,7 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
     DevTables T, EncodeArgs a, HugeArgs h, uint32_t nchunks) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
-  const SubRef sr = sub_of(h, blockIdx.x, h.pair ? (a.batch + 1) / 2 : a.batch);
+  const SubRef sr = sub_of(h, blockIdx.x, unit_count(h, a.batch));
   const uint32_t pb = sr.pb, tl = sr.tl, ch0 = tl * kRC;
   const uint32_t ncols = min(static_cast<uint32_t>(kRC), nchunks - ch0);
   const uint32_t I = kSK * sr.u;  // shift u / M, sub-segment u % M
@@ -304,20 +318,54 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
     DevTables T, ReconstructArgs a, HugeArgs h, uint32_t nsyms) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
-  const SubRef sr = sub_of(h, blockIdx.x, a.batch);
-  const uint32_t pb = sr.pb, tl = sr.tl;
-  if (uniform(h.mode[pb]) != kHugeDecode) return;
+  const SubRef sr = sub_of(h, blockIdx.x, unit_count(h, a.batch));
+  const uint32_t pb = sr.pb, tl = sr.tl;  // pb: the pair of payloads 2 pb, 2 pb + 1 (HugeArgs::pair)
+  if (uniform(tile_mode(h, static_cast<size_t>(pb) * h.tiles + tl)) != kHugeDecode) return;
   const uint32_t col0 = tl * kRC, ncols = min(static_cast<uint32_t>(kRC), nsyms - col0);
   const uint32_t I = kSK * sr.u;  // rows I .. I + 1023: segment u / M, sub-segment u % M
-  const uint8_t* pres = a.present + static_cast<size_t>(pb) * a.n;
-  const uint16_t* loc = h.loc + static_cast<size_t>(pb) * a.n;
-  const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);
-  const bool full = ncols == kRC && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
   const Res r = res_coords<kSK>();
   uint32_t* DL = reinterpret_cast<uint32_t*>(smem + RGeo<kSK>::kTileBytes);
   uint32_t* VS = DL + kDeltaWords;
   uint32_t XL[16], XH[16];
-  {
+  if (h.pair) {
+    // lane 16 u + cq: payload 2 pb + (cq >> 3), columns 4 (cq & 7) ..; the two
+    // payloads' row tables in two halves of 8 rows per lane
+    const bool two = 2 * pb + 1 < a.batch;
+    const uint32_t sel = r.cq >> 3, pbl = 2 * pb + sel;
+    const bool valid = sel == 0 || two;
+    const size_t n = a.n;
+    const uint8_t* pres0 = a.present + static_cast<size_t>(2 * pb) * n;
+    const uint8_t* pres1 = two ? pres0 + n : nullptr;
+    const uint16_t* loc0 = h.loc + static_cast<size_t>(2 * pb) * n;
+    const uint16_t* loc1 = two ? loc0 + n : nullptr;
+    const uint32_t pm = valid ? lane_rows_present(a.present + static_cast<size_t>(pbl) * n, I, r) : 0u;
+    const uint8_t* sh = a.shards + static_cast<size_t>(valid ? pbl : 2 * pb) * a.batch_stride;
+    Res rl = r;
+    rl.cq = r.cq & 7u;
+    uint2 raw[8];
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      load_lane_rows<8>(raw, sh, a.shard_len, I, pm, rl, ncols, false, T.zeros, 8 * hf);
+      if (hf == 1) __syncthreads();  // every wave is done with half 0's tables
+      stage_row_tables_pair(tile, T, loc0, pres0, loc1, pres1, I, hf, r.tid, false);
+      if (hf == 0) {
+        stage_delta_tables(T, DL);
+        stage_rh_tables<kSK>(T, VS, 1, I);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        uint32_t l, hh;
+        blk_to_quad(raw[i], l, hh);
+        const FullT m = row_table_at(tile, pair_row_slot(sel, 4u * r.w + r.u, i));
+        qmul_set_vv(XL[8 * hf + i], XH[8 * hf + i], l, hh, m);
+      }
+    }
+  } else {
+    const uint8_t* pres = a.present + static_cast<size_t>(pb) * a.n;
+    const uint16_t* loc = h.loc + static_cast<size_t>(pb) * a.n;
+    const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);
+    const bool full = ncols == kRC && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
     const uint32_t pm = lane_rows_present(pres, I, r);
     uint2 raw[8];
     load_lane_rows<8>(raw, sh, a.shard_len, I, pm, r, ncols, full, T.zeros, 0);
@@ -373,7 +421,7 @@ __global__ __launch_bounds__(256) void k_huge_rec_top(DevTables T, HugeArgs h, s
   const size_t gid = static_cast<size_t>(blockIdx.x) * 256u + threadIdx.x;
   if (gid >= units) return;
   const size_t pt = gid >> 14;  // tile of the slice
-  if (uniform(h.mode[pt / h.tiles]) != kHugeDecode) return;
+  if (uniform(tile_mode(h, pt)) != kHugeDecode) return;
   uint8_t* base = h.scr + pt * h.slots * kSlotBytes + (gid & 16383u) * 8u;
   auto at = [&](uint32_t slot) __attribute__((always_inline)) { return base + static_cast<size_t>(slot) * kSlotBytes; };
   uint2 d[M], x[M];
@@ -422,15 +470,12 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
     DevTables T, ReconstructArgs a, HugeArgs h, uint32_t nsyms) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
-  const SubRef sr = sub_of(h, blockIdx.x, a.batch);
-  const uint32_t pb = sr.pb, tl = sr.tl;
-  const uint32_t mode = uniform(h.mode[pb]);
+  const SubRef sr = sub_of(h, blockIdx.x, unit_count(h, a.batch));
+  const uint32_t pb = sr.pb, tl = sr.tl;  // pb: the pair 2 pb, 2 pb + 1 (HugeArgs::pair)
+  const uint32_t mode = uniform(tile_mode(h, static_cast<size_t>(pb) * h.tiles + tl));
   if (mode == kHugeSkip) return;
   const uint32_t col0 = tl * kRC, ncols = min(static_cast<uint32_t>(kRC), nsyms - col0);
   const uint32_t I = kSK * sr.u;  // output rows I .. I + 1023
-  const uint8_t* pres = a.present + static_cast<size_t>(pb) * a.n;
-  const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);
-  const bool full = ncols == kRC && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
   const bool out16 = out_vec_ok(a.out, a.out_stride);
   const Res r = res_coords<kSK>();
   uint32_t AL[16], AH[16];
@@ -457,6 +502,54 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
   }
   // merge: received systematic rows, postmultiplied recovered ones
   // (inc_reconstruct.rs:46-50, :82-84; tower in, Cantor out)
+  if (h.pair) {
+    // lane 16 u + cq: payload 2 pb + (cq >> 3), whose own mode decides
+    // whether it writes (a copy-mode payload has every systematic row
+    // present, so the merge takes them all; a skipped one writes nothing)
+    const bool two = 2 * pb + 1 < a.batch;
+    const uint32_t sel = r.cq >> 3, pbl = 2 * pb + sel;
+    const bool valid = sel == 0 || two;
+    const size_t n = a.n;
+    const uint8_t* pres0 = a.present + static_cast<size_t>(2 * pb) * n;
+    const uint8_t* pres1 = two ? pres0 + n : nullptr;
+    const uint16_t* loc0 = h.loc + static_cast<size_t>(2 * pb) * n;
+    const uint16_t* loc1 = two ? loc0 + n : nullptr;
+    const bool writes = valid && h.mode[pbl] != kHugeSkip;
+    const uint32_t pm = valid ? lane_rows_present(a.present + static_cast<size_t>(pbl) * n, I, r) : 0u;
+    Res rl = r;
+    rl.cq = r.cq & 7u;
+    uint2 raw[16];
+    load_lane_rows(raw, a.shards + static_cast<size_t>(valid ? pbl : 2 * pb) * a.batch_stride, a.shard_len, I, pm, rl,
+                   ncols, false, T.zeros);
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      if (mode == kHugeDecode) {
+        __syncthreads();  // every wave has read the tile (hf = 0) / half 0's tables (hf = 1)
+        stage_row_tables_pair(tile, T, loc0, pres0, loc1, pres1, I, hf, r.tid, true);
+        __syncthreads();
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int x = 8 * hf + i;
+        uint32_t l, hh;
+        if ((pm >> x) & 1u) {
+          blk_to_quad(raw[x], l, hh);
+        } else {
+          const FullT m = row_table_at(tile, pair_row_slot(sel, 4u * r.w + r.u, i));
+          qmul_set_vv(l, hh, AL[x], AH[x], m);
+        }
+        AL[x] = l;
+        AH[x] = hh;
+      }
+    }
+    if (writes)
+      res_copy_out<kSK>(a.out + static_cast<size_t>(pbl) * a.out_stride + 2 * I, AL, AH, rl, ncols, out16,
+                        2 * static_cast<size_t>(h.K));
+    return;
+  }
+  const uint8_t* pres = a.present + static_cast<size_t>(pb) * a.n;
+  const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);
+  const bool full = ncols == kRC && rows_vec_ok(a.shards, a.batch_stride, a.shard_len);
   const uint32_t pm = lane_rows_present(pres, I, r);
   uint2 raw[16];
   load_lane_rows(raw, sh, a.shard_len, I, pm, r, ncols, full, T.zeros);
@@ -615,13 +708,17 @@ hipError_t launch_reconstruct_huge(const DevTables& T, const ReconstructArgs& a,
     loc = locators;
   }
   const size_t tiles = (nsyms + kRC - 1) / kRC;
-  const size_t per = a.batch * tiles;
+  // payloads of at most 32 columns: two per tile, as the encode
+  const bool pair = huge_pair_enabled() && nsyms <= kRC / 2 && a.batch > 1;
+  const size_t per = pair ? (a.batch + 1) / 2 : a.batch * tiles;
   if (per * (a.n / kSK) > 0x7fffffffu) return hipErrorInvalidValue;
   const uint32_t ns = static_cast<uint32_t>(nsyms);
   HugeArgs h = huge_args(scratch, a.n, a.k, tiles, (a.n + a.k) / kSK);
   h.loc = loc;
   h.mode = mode;
   h.per = static_cast<uint32_t>(per);
+  h.pair = pair ? 1u : 0u;
+  h.batch = static_cast<uint32_t>(a.batch);
   auto grid = [&](uint32_t u0, uint32_t u1) { return static_cast<uint32_t>(per * (u1 - u0)); };
   if (e == hipSuccess)
     e = for_gen_ranges(0, a.n / kSK, [&](auto g, uint32_t u0, uint32_t u1) {

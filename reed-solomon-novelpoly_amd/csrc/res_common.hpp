@@ -867,6 +867,56 @@ __device__ __forceinline__ FullT row_table(const uint8_t* tile, uint32_t r) {
   return m;
 }
 
+// Two payloads in one tile (kernels_huge.hip, HugeArgs::pair): the tables of
+// both payloads' rows do not fit the tile at once (2 x 1024 x 80 bytes), so
+// they are staged in two halves.  Half hf holds rows row0 + 16 g + 8 hf + i
+// (g < 64, i < 8) of payload sel at slot sel * 512 + 8 g + i, in the 16-row
+// groups of row_slot (83 KiB).  A CQ lane (wave w, u, cq) reads its row i of
+// the half at pair_row_slot(cq >> 3, 4 w + u, i).
+__host__ __device__ constexpr uint32_t pair_row_slot(uint32_t sel, uint32_t g, uint32_t i) {
+  return row_slot(512u * sel + 8u * g + i);
+}
+static_assert(pair_row_slot(1, 63, 7) + kRowSlot <= RGeo<1024>::kTileBytes, "pair row tables fit the tile");
+
+// Thread t stages half hf's table of payload t >> 9 (loc / pres of payload 0
+// and 1; payload 1 may be absent: pres1 == nullptr, zero tables), as
+// stage_row_tables_loc.
+__device__ __forceinline__ void stage_row_tables_pair(uint8_t* tile, const DevTables& T, const uint16_t* loc0,
+                                                      const uint8_t* pres0, const uint16_t* loc1,
+                                                      const uint8_t* pres1, uint32_t row0, uint32_t hf, uint32_t tid,
+                                                      bool erased_only) {
+  const uint32_t sel = tid >> 9, g = (tid >> 3) & 63u, i = tid & 7u;
+  const uint32_t row = row0 + 16u * g + 8u * hf + i;
+  const uint8_t* pres = sel ? pres1 : pres0;
+  const uint16_t* loc = sel ? loc1 : loc0;
+  uint4 v[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) v[k] = make_uint4(0, 0, 0, 0);
+  if (pres) {
+    const bool p = pres[row] != 0;
+    if (erased_only ? !p : p) {
+      const uint32_t e = T.exp[loc[row]];
+      const uint4* src = reinterpret_cast<const uint4*>((p ? T.in_pools : T.out_pools) + static_cast<size_t>(e) * kPoolWords);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) v[k] = src[k];
+    }
+  }
+  uint4* dst = reinterpret_cast<uint4*>(tile + pair_row_slot(sel, g, i));
+#pragma unroll
+  for (int k = 0; k < 5; ++k) dst[k] = v[k];
+}
+
+__device__ __forceinline__ FullT row_table_at(const uint8_t* tile, uint32_t addr) {
+  FullT m;
+  const uint4* src = reinterpret_cast<const uint4*>(tile + addr);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const uint4 v = src[i];
+    m.p[4 * i] = v.x, m.p[4 * i + 1] = v.y, m.p[4 * i + 2] = v.z, m.p[4 * i + 3] = v.w;
+  }
+  return m;
+}
+
 // Presence bits of this lane's 16 rows row0 + 64 w + 16 u + i (bit i).
 __device__ __forceinline__ uint32_t lane_rows_present(const uint8_t* pres, uint32_t row0, const Res& r) {
   const uint8_t* p = pres + row0 + 64u * r.w + 16u * r.u;

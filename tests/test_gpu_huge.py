@@ -89,3 +89,70 @@ def test_huge_encode_paired_batch(gpu, oracle, nw, kw, plen, batch):
         bad = [v for v in range(nw) if hs[b, v * sl:(v + 1) * sl].tobytes() != want[v]]
         assert not bad, (b, len(bad), bad[:5])
         assert (hs[b, nw * sl:] == 0xA5).all()
+
+
+# The same pairing in the sub-transform decode: a tile runs the larger of its
+# two payloads' modes, each lane half merges and writes for its own payload.
+# Mixed modes per pair: random erasures (decode), only parity lost (copy),
+# every systematic shard lost, fewer than k shards (NeedMoreShards: status
+# set, output untouched), and a non-codeword (a corrupted present shard).
+PAIR_REC = [(65536, 21846, 2 * 16384 * 32, ["rand", "copy", "nosys", "rand"]),
+            (65536, 21846, 2 * 16384 * 17 + 3, ["copy", "rand", "few", "corrupt", "rand"]),
+            (50000, 16667, 2 * 16384 * 5, ["few", "rand", "rand"])]
+
+
+@pytest.mark.parametrize("nw,kw,plen,kinds", PAIR_REC)
+def test_huge_reconstruct_paired_batch(gpu, oracle, nw, kw, plen, kinds):
+    import torch
+
+    p = npa.CodeParams.derive_parameters(nw, kw)
+    n, k = p.n(), p.k()
+    assert k == 16384
+    sl = p.make_encoder(gpu).shard_len(plen)
+    assert sl // 2 <= 32
+    batch = len(kinds)
+    pls = np.stack([np.frombuffer(synth.payload(2 * nw + plen + b, plen), np.uint8) for b in range(batch)])
+    dp = torch.from_numpy(pls).cuda()
+    ds = torch.zeros((batch, n * sl), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    npa.encode_batch_dev(p, dp.data_ptr(), plen, plen, batch, ds.data_ptr(), n * sl, ctx=gpu,
+                         stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    hs = ds.cpu().numpy()
+    rng = np.random.default_rng(plen + batch)
+    pres = np.zeros((batch, n), np.uint8)
+    for b, kind in enumerate(kinds):
+        pres[b, :nw] = 1
+        if kind in ("rand", "corrupt"):
+            pres[b, rng.choice(nw, nw - k, replace=False)] = 0
+        elif kind == "copy":
+            pres[b, k + rng.choice(nw - k, (nw - k) // 2, replace=False)] = 0
+        elif kind == "nosys":
+            pres[b, :k] = 0
+        elif kind == "few":
+            pres[b, rng.choice(nw, nw - k + 1, replace=False)] = 0
+        if kind == "corrupt":
+            v = int(rng.choice(np.flatnonzero(pres[b])))
+            hs[b, v * sl:(v + 1) * sl] ^= 0x3C
+    ds = torch.from_numpy(hs).cuda()
+    dpres = torch.from_numpy(pres).cuda()
+    olen = (sl // 2) * 2 * k
+    dout = torch.full((batch, olen), 0x77, dtype=torch.uint8, device="cuda")
+    dst = torch.full((batch, 2), -1, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    npa.reconstruct_batch_dev2(p, ds.data_ptr(), sl, n * sl, dpres.data_ptr(), 0, batch, dout.data_ptr(), olen,
+                               ctx=gpu, stream=torch.cuda.current_stream().cuda_stream, d_status=dst.data_ptr())
+    torch.cuda.synchronize()
+    o, stat = dout.cpu().numpy(), dst.cpu().numpy()
+    for b, kind in enumerate(kinds):
+        have = int(pres[b].sum())
+        if kind == "few":
+            assert have < k and stat[b, 0] != 0 and stat[b, 1] == have, (b, stat[b])
+            assert (o[b] == 0x77).all(), b  # a NeedMoreShards payload's output is left untouched
+            continue
+        assert tuple(stat[b]) == (0, have), (b, stat[b])
+        recv = [hs[b, i * sl:(i + 1) * sl].tobytes() if pres[b, i] else None for i in range(n)]
+        st, want = oracle.reconstruct(recv, n, k)
+        assert st == 0 and o[b].tobytes() == want, (b, kind)
+        if kind != "corrupt":
+            assert want[:plen] == pls[b].tobytes()

@@ -88,6 +88,10 @@ p4() {  # sub-transform path: kernel profile, then the slice sweep
   hugeprof && MBS="2048 256 128" slices
 }
 
+p6() {  # paired sub-transform decode: huge tests, then 65,536 / 50,000 validators with and without pairing
+  p5
+}
+
 p5() {  # paired sub-transform encode: huge tests, then 65,536 / 50,000 validators with and without pairing
   timeout -k 10 600 python -u -m pytest tests/test_gpu_huge.py tests/test_gpu_noncodeword.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r05/pytest_huge_p5.log 2>&1; rc=$?
   echo "huge tests: $(tail -1 gpurun_out/r05/pytest_huge_p5.log)"
