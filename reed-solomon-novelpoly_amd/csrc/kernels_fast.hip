@@ -505,6 +505,7 @@ struct RecCtx {
   bool full;
   uint32_t cqb, hb;
   uint64_t* dbg;  // experiment builds only (stamp)
+  uint32_t occ;   // bit q: segment q holds a present row (k_prefix_locator, record byte 1)
 };
 
 // Segment q of the sweep at step `step` (segments 2, 3, 1, 0 for NQ = 4; 1, 0
@@ -678,6 +679,9 @@ template <int K, int NQ>
 constexpr bool kTilePrefetch = NQ == 4 && kMultiTile<K>;
 
 // PRE0: step 0's rows are in `raw` on entry (kTilePrefetch).
+template <int NQ>
+constexpr bool kSkipEmpty = NQ == 8;
+
 template <int K, int NQ, bool PRE0 = false>
 __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&msk)[NQ], uint2 (&raw)[16],
                                              uint32_t (&AL)[16], uint32_t (&AH)[16], bool after_tile) {
@@ -742,81 +746,101 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
 #pragma unroll 1
   for (int step = 0; step < NQ; ++step) {
     const int q = seg_of<NQ>(step);
-    const uint32_t index = uniform(static_cast<uint32_t>(q) * K);
-    __builtin_amdgcn_sched_barrier(0);
-    const uint32_t g = fresh(c.g);
-    const uint8_t* sh = fresh(c.sh);
-    const uint32_t* R = fresh(c.R);
-    const size_t shard_len = fresh(c.shard_len);
-    const uint32_t cqb = fresh_v(c.cqb), hb = fresh_v(c.hb);
-    uint32_t m = uniform(seg_mask<NQ>(msk, step));
-    if (!kRowPrefetch<NQ> && !(PRE0 && step == 0))
-      issue_rows(raw, (kExp & 32) ? T.zeros : sh, (kExp & 32) ? 0 : shard_len, m, index + 16 * g, T.zeros, c.lane,
-                 c.ncols, c.full, q == 0);
-    stamp(c.dbg, 2 + 6 * step);
-    __builtin_amdgcn_s_setprio(kRecPrioPremul);
-    pipelined_rec<16>(
-        [&](auto pc) __attribute__((always_inline)) {
-          return (cpool_t)(R) + (index + 16 * g + decltype(pc)::value) * kPoolWords;
-        },
-        [&](auto pc) __attribute__((always_inline)) { return ((m >> decltype(pc)::value) & 1u) != 0; },  // present
-        [&](auto pc, const Mult& pool) __attribute__((always_inline)) {
-          constexpr int x = decltype(pc)::value;
-          XL[x] = 0;  // absent rows contribute zero
-          XH[x] = 0;
-          if ((m >> x) & 1u) {
-            uint32_t l, h;
-            blk_to_quad(raw[x], l, h);
-            if constexpr (kExp & 16) {  // experiment: no premultiply
-              XL[x] = l;
-              XH[x] = h;
-            } else {
-              qmul_set(XL[x], XH[x], l, h, pool);
-            }
-          }
-        });
-    const uint32_t* vp = c.VP + vp_slot<K, NQ>(q, step) * Geo<K>::kVPWords;
-    stamp(c.dbg, 3 + 6 * step);
-    // absent rows are zero; segment q's transform has gen_of(qK) <= kRecMaxGen
-    with_gen<0, kRecMaxGen<K, NQ>, false>(index, [&](auto gc) __attribute__((always_inline)) {
-      cq_levels<K, true, false, decltype(gc)::value, false, kRecPrioCq>(T, vp, index, g, XL, XH, m);
-    });
-    stamp(c.dbg, 4 + 6 * step);
-    if (step > 0 || after_tile) {
-      __syncthreads();  // the previous high pass (or tile's copy-out) is done with the tile and the other table buffer
-      if (!kRecResident<K, NQ> && step + 1 < NQ) {
-        const int qn = seg_of<NQ>(step + 1);
-        stage_vpools<K, Geo<K>::kThreads>(T, static_cast<uint32_t>(qn) * K, c.VP + ((step + 1) & 1) * Geo<K>::kVPWords, true);
-      }
-    }
-    cq_write_p<K>(c.tile, cqb, XL, XH);
-    // next step's rows (the systematic rows after the last step) load during
-    // this step's high pass
-    if constexpr (kRowPrefetch<NQ>) {
-      uint32_t mn = msk[0];
-      uint32_t qn = 0;
+    // A segment without a present row contributes x_q = 0 (absent rows are
+    // zeros): no loads, premultiply, transform or exchange, only the fold.
+    // The 8-segment decodes only (n = 8k, e.g. 300, 700 and 1,200
+    // validators: the segments above wanted_n are empty); the others are
+    // compiled without the branch.  The next step's tables are still staged
+    // here when they are not resident (in the other buffer, which the
+    // previous step's high pass read).
+    if (kSkipEmpty<NQ> && !((c.occ >> q) & 1u)) {
 #pragma unroll
-      for (int i = 1; i < NQ; ++i) {
-        if (step + 1 == i) {
-          mn = msk[i];
-          qn = static_cast<uint32_t>(seg_of<NQ>(i));
+      for (int j = 0; j < 16; ++j) XL[j] = XH[j] = 0;
+      if constexpr (!kRecResident<K, NQ>) {
+        if (step > 0 && step + 1 < NQ) {
+          __syncthreads();
+          stage_vpools<K, Geo<K>::kThreads>(T, static_cast<uint32_t>(seg_of<NQ>(step + 1)) * K,
+                                            c.VP + ((step + 1) & 1) * Geo<K>::kVPWords, true);
+          __syncthreads();
         }
       }
-      if (step + 1 == NQ) mn = msk[NQ - 1], qn = 0;  // segment 0 is the last step's
-      issue_rows(raw, (kExp & 32) ? T.zeros : sh, (kExp & 32) ? 0 : shard_len, uniform(mn), uniform(qn) * K + 16 * g,
-                 T.zeros, c.lane, c.ncols, c.full, qn == 0 && step + 1 < NQ);
+    } else {
+      const uint32_t index = uniform(static_cast<uint32_t>(q) * K);
+      __builtin_amdgcn_sched_barrier(0);
+      const uint32_t g = fresh(c.g);
+      const uint8_t* sh = fresh(c.sh);
+      const uint32_t* R = fresh(c.R);
+      const size_t shard_len = fresh(c.shard_len);
+      const uint32_t cqb = fresh_v(c.cqb), hb = fresh_v(c.hb);
+      uint32_t m = uniform(seg_mask<NQ>(msk, step));
+      if (!kRowPrefetch<NQ> && !(PRE0 && step == 0))
+        issue_rows(raw, (kExp & 32) ? T.zeros : sh, (kExp & 32) ? 0 : shard_len, m, index + 16 * g, T.zeros, c.lane,
+                   c.ncols, c.full, q == 0);
+      stamp(c.dbg, 2 + 6 * step);
+      __builtin_amdgcn_s_setprio(kRecPrioPremul);
+      pipelined_rec<16>(
+          [&](auto pc) __attribute__((always_inline)) {
+            return (cpool_t)(R) + (index + 16 * g + decltype(pc)::value) * kPoolWords;
+          },
+          [&](auto pc) __attribute__((always_inline)) { return ((m >> decltype(pc)::value) & 1u) != 0; },  // present
+          [&](auto pc, const Mult& pool) __attribute__((always_inline)) {
+            constexpr int x = decltype(pc)::value;
+            XL[x] = 0;  // absent rows contribute zero
+            XH[x] = 0;
+            if ((m >> x) & 1u) {
+              uint32_t l, h;
+              blk_to_quad(raw[x], l, h);
+              if constexpr (kExp & 16) {  // experiment: no premultiply
+                XL[x] = l;
+                XH[x] = h;
+              } else {
+                qmul_set(XL[x], XH[x], l, h, pool);
+              }
+            }
+          });
+      const uint32_t* vp = c.VP + vp_slot<K, NQ>(q, step) * Geo<K>::kVPWords;
+      stamp(c.dbg, 3 + 6 * step);
+      // absent rows are zero; segment q's transform has gen_of(qK) <= kRecMaxGen
+      with_gen<0, kRecMaxGen<K, NQ>, false>(index, [&](auto gc) __attribute__((always_inline)) {
+        cq_levels<K, true, false, decltype(gc)::value, false, kRecPrioCq>(T, vp, index, g, XL, XH, m);
+      });
+      stamp(c.dbg, 4 + 6 * step);
+      if (step > 0 || after_tile) {
+        __syncthreads();  // the previous high pass (or tile's copy-out) is done with the tile and the other table buffer
+        if (!kRecResident<K, NQ> && step + 1 < NQ) {
+          const int qn = seg_of<NQ>(step + 1);
+          stage_vpools<K, Geo<K>::kThreads>(T, static_cast<uint32_t>(qn) * K, c.VP + ((step + 1) & 1) * Geo<K>::kVPWords, true);
+        }
+      }
+      cq_write_p<K>(c.tile, cqb, XL, XH);
+      // next step's rows (the systematic rows after the last step) load during
+      // this step's high pass
+      if constexpr (kRowPrefetch<NQ>) {
+        uint32_t mn = msk[0];
+        uint32_t qn = 0;
+  #pragma unroll
+        for (int i = 1; i < NQ; ++i) {
+          if (step + 1 == i) {
+            mn = msk[i];
+            qn = static_cast<uint32_t>(seg_of<NQ>(i));
+          }
+        }
+        if (step + 1 == NQ) mn = msk[NQ - 1], qn = 0;  // segment 0 is the last step's
+        issue_rows(raw, (kExp & 32) ? T.zeros : sh, (kExp & 32) ? 0 : shard_len, uniform(mn), uniform(qn) * K + 16 * g,
+                   T.zeros, c.lane, c.ncols, c.full, qn == 0 && step + 1 < NQ);
+      }
+      __syncthreads();
+      stamp(c.dbg, 5 + 6 * step);
+      hi_read_p<K>(c.tile, hb, XL, XH);
+      // hi levels: gen_of(index) <= 4; segment 0 (index 0) skips the t = 0
+      // groups, whose skew is the zero element (15 of the 32 quad multiplies)
+      // (the 2-segment decode keeps its rows prefetch live here: no room for two instances)
+      if (NQ == 4 && q == 0)  // -1.1 % (config 3)
+        hi_levels<K, true, true, 0, 0, kRecPrioHi>(T, vp, 0, XL, XH);
+      else
+        hi_levels<K, true, false, 0, 0, kRecPrioHi>(T, vp, index, XL, XH);
+      stamp(c.dbg, 6 + 6 * step);
     }
-    __syncthreads();
-    stamp(c.dbg, 5 + 6 * step);
-    hi_read_p<K>(c.tile, hb, XL, XH);
-    // hi levels: gen_of(index) <= 4; segment 0 (index 0) skips the t = 0
-    // groups, whose skew is the zero element (15 of the 32 quad multiplies)
-    // (the 2-segment decode keeps its rows prefetch live here: no room for two instances)
-    if (NQ == 4 && q == 0)  // -1.1 % (config 3)
-      hi_levels<K, true, true, 0, 0, kRecPrioHi>(T, vp, 0, XL, XH);
-    else
-      hi_levels<K, true, false, 0, 0, kRecPrioHi>(T, vp, index, XL, XH);
-    stamp(c.dbg, 6 + 6 * step);
     __builtin_amdgcn_sched_barrier(0);
     fold(step, q);
     __builtin_amdgcn_sched_barrier(0);
@@ -834,7 +858,8 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
 template <int K, int NQ>
 __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructArgs& a, const uint8_t* sh,
                                          const uint8_t* pres, const uint32_t* rows, uint8_t* smem,
-                                         uint32_t pb, uint32_t col0, uint32_t ncols, bool full, uint64_t* dbg) {
+                                         uint32_t pb, uint32_t col0, uint32_t ncols, bool full, uint64_t* dbg,
+                                         uint32_t occ) {
   using G = Geo<K>;
   uint8_t* tile = smem;
   uint32_t* VP = reinterpret_cast<uint32_t*>(smem + G::kTileBytes);  // 2 staged transforms
@@ -862,7 +887,7 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
 
     const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
     uint32_t AL[16], AH[16];
-    RecCtx c{T, a.shard_len, tile, rows, sh, VP, g, lane, tid, ncols, full, cqb, hb, dbg};
+    RecCtx c{T, a.shard_len, tile, rows, sh, VP, g, lane, tid, ncols, full, cqb, hb, dbg, occ};
     rec_segments<K, NQ>(c, msk, raw, AL, AH, false);
     // ---- forward transform of size K at index 0
     const uint32_t* vp0 = VP + vp_slot<K, NQ>(0, NQ - 1) * G::kVPWords;  // segment 0's tables = FFT(K, 0)'s
@@ -960,7 +985,7 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
 template <int K, int NQ>
 __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructArgs& a, const uint8_t* pres,
                                           const uint32_t* rows, uint8_t* smem, uint32_t pb,
-                                          uint32_t tl0, uint32_t ntl, uint32_t nsyms) {
+                                          uint32_t tl0, uint32_t ntl, uint32_t nsyms, uint32_t occ) {
   using G = Geo<K>;
   uint8_t* tile = smem;
   uint32_t* VP = reinterpret_cast<uint32_t*>(smem + G::kTileBytes);  // 2 staged transforms
@@ -1034,7 +1059,7 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
     if constexpr (NQ > 1) {
       const uint32_t hb = col_base<K>(tid / G::R) ^ (8u * (tid % G::R));
       uint32_t AL[16], AH[16];
-      RecCtx c{T, shard_len, tile, rows, sh, VP, g, lane, tid, ncols, full, cqb, hb, dbg};
+      RecCtx c{T, shard_len, tile, rows, sh, VP, g, lane, tid, ncols, full, cqb, hb, dbg, occ};
       // t > 0: step 0 waits for the previous tile's last LDS reads (its FFT's
       // cq_read, the copy-out) before writing the tile
       rec_segments<K, NQ, kTilePrefetch<K, NQ>>(c, msk, raw, AL, AH, t > 0 && (NQ == 2 || kRecResident<K, NQ>));
@@ -1147,14 +1172,15 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
   // k_locator_records for caller locators)
   const uint8_t* rec = a.prefix + static_cast<size_t>(pb) * prefix_stride_c(N, K);
   const int nq = uniform(rec[0]);
+  const uint32_t occ = uniform(rec[1]);  // segments with a present row
   const uint32_t* rows = reinterpret_cast<const uint32_t*>(rec + prefix_pools_offset(N));
   if constexpr (kMultiTile<K>) {
     if constexpr (SERVE >= 4) {
-      if (nq == SERVE) rec_tiles<K, SERVE>(T, a, pres, rows, smem, pb, tl0, ntl, nsyms);
+      if (nq == SERVE) rec_tiles<K, SERVE>(T, a, pres, rows, smem, pb, tl0, ntl, nsyms, occ);
     } else if (nq == 1) {
-      rec_tiles<K, 1>(T, a, pres, rows, smem, pb, tl0, ntl, nsyms);
+      rec_tiles<K, 1>(T, a, pres, rows, smem, pb, tl0, ntl, nsyms, occ);
     } else if (NQ <= 4 && nq == 2) {
-      rec_tiles<K, 2>(T, a, pres, rows, smem, pb, tl0, ntl, nsyms);
+      rec_tiles<K, 2>(T, a, pres, rows, smem, pb, tl0, ntl, nsyms, occ);
     }
   } else {  // tpw == 1
     const uint32_t col0 = tl0 * kTile;
@@ -1166,11 +1192,11 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
                                                                static_cast<size_t>(nsyms) * 2 * K + ((kExp & 128) ? 4096u : 256u) * tl0)
                                  : nullptr;
     if constexpr (SERVE >= 4) {
-      if (nq == SERVE) rec_tile<K, SERVE>(T, a, sh, pres, rows, smem, pb, col0, ncols, full, dbg);
+      if (nq == SERVE) rec_tile<K, SERVE>(T, a, sh, pres, rows, smem, pb, col0, ncols, full, dbg, occ);
     } else if (nq == 1) {
-      rec_tile<K, 1>(T, a, sh, pres, rows, smem, pb, col0, ncols, full, dbg);
+      rec_tile<K, 1>(T, a, sh, pres, rows, smem, pb, col0, ncols, full, dbg, occ);
     } else if (NQ <= 4 && nq == 2) {
-      rec_tile<K, 2>(T, a, sh, pres, rows, smem, pb, col0, ncols, full, dbg);
+      rec_tile<K, 2>(T, a, sh, pres, rows, smem, pb, col0, ncols, full, dbg, occ);
     }
   }
 }
@@ -1211,6 +1237,20 @@ __device__ __forceinline__ void count_present(const uint8_t* pres, int& have1, i
   }
 }
 
+// Bit q: segment q (rows [qK, (q+1)K)) holds a present row (record byte 1:
+// the decodes skip the transforms of empty segments).
+template <int K, int N>
+__device__ __forceinline__ uint32_t segment_occupancy(const uint8_t* pres) {
+  uint32_t occ = 0;
+#pragma unroll 1
+  for (int q = 0; q < N / K; ++q) {
+    int any = 0;
+    for (int v = static_cast<int>(threadIdx.x); v < K; v += 256) any |= pres[q * K + v] != 0;
+    if (__syncthreads_or(any)) occ |= 1u << q;
+  }
+  return occ;
+}
+
 // Status of payload pb (launchers.hpp ReconstructArgs::status); true if it
 // decodes.
 __device__ __forceinline__ bool write_status(const ReconstructArgs& a, uint32_t pb, int have) {
@@ -1239,7 +1279,8 @@ __global__ __launch_bounds__(256) void k_prefix_locator(DevTables T, Reconstruct
   // Otherwise the full decode from every present row, as the reference
   // (inc_reconstruct.rs:61-85); the 2K-row prefix only for trusted codewords.
   const int nq = !write_status(a, pb, have) ? 0 : have1 == K ? 1 : (a.trusted && NQ == 4 && have2 >= K) ? 2 : NQ;
-  if (tid == 0) rec[0] = static_cast<uint8_t>(nq);
+  const uint32_t occ = segment_occupancy<K, N>(pres);
+  if (tid == 0) rec[0] = static_cast<uint8_t>(nq), rec[1] = static_cast<uint8_t>(occ);
   if (nq <= 1) return;
   if (NQ == 4 && nq == 2) {
     fused_locator<2 * K, 256>(T, pres, W, E, PR);
@@ -1262,7 +1303,8 @@ __global__ __launch_bounds__(256) void k_locator_records(DevTables T, Reconstruc
   int have1, have2, have;
   count_present<K, N>(a.present + static_cast<size_t>(pb) * N, have1, have2, have);
   const bool ok = write_status(a, pb, have);
-  if (tid == 0) rec[0] = static_cast<uint8_t>(ok ? NQ : 0);
+  const uint32_t occ = segment_occupancy<K, N>(a.present + static_cast<size_t>(pb) * N);
+  if (tid == 0) rec[0] = static_cast<uint8_t>(ok ? NQ : 0), rec[1] = static_cast<uint8_t>(occ);
   if (!ok) return;
   // mul(x, log m) == x * EXP[m] (inc_log_mul.rs:42-49)
   for (uint32_t v = tid; v < static_cast<uint32_t>(N); v += 256) E[v] = T.exp[loc[v]];

@@ -522,6 +522,57 @@ def test_reconstruct_prefix_modes(gpu, oracle, nw, kw, plen):
         assert want[:plen] == pls[b].tobytes()
 
 
+@pytest.mark.parametrize("nw,kw,plen", [(300, 100, 64 * 256), (300, 100, 64 * 37 + 5), (700, 234, 128 * 256 + 3),
+                                        (1200, 400, 256 * 257), (512, 64, 64 * 64)])
+def test_reconstruct_empty_segments(gpu, oracle, nw, kw, plen):
+    """n = 8k fast reconstruct skips the transforms of k-row segments without a
+    present row (record byte 1, kernels_fast.hip segment_occupancy): whole
+    segments erased inside wanted_n (alone, several, all but one) and the
+    segments past wanted_n, with caller locators and with the fused locator,
+    give the oracle's bytes."""
+    import torch
+
+    p = npa.CodeParams.derive_parameters(nw, kw)
+    n, k, wn = p.n(), p.k(), p.wanted_n
+    assert n == 8 * k
+    nseg = (wn + k - 1) // k
+    rng = np.random.default_rng(nw + plen)
+    pats = []
+    for gone in ([1], [0, 2], [0] + list(range(2, nseg)), list(range(1, nseg)), [nseg - 1], []):
+        pres = np.zeros(n, np.uint8)
+        pres[:wn] = 1
+        for q in gone:
+            pres[q * k:(q + 1) * k] = 0
+        if pres.sum() > k + 8:  # a few random erasures in what is left
+            idx = np.flatnonzero(pres)
+            pres[rng.choice(idx, min(len(idx) - k, 5), replace=False)] = 0
+        if pres.sum() >= k:
+            pats.append(pres)
+    batch = len(pats)
+    sl = p.make_encoder(gpu).shard_len(plen)
+    pls = np.stack([np.frombuffer(synth.payload(5000 + b, plen), dtype=np.uint8) for b in range(batch)])
+    dp = dev(pls)
+    ds = torch.empty((batch, n, sl), dtype=torch.uint8, device="cuda")
+    npa.encode_batch_dev(p, dp.data_ptr(), plen, plen, batch, ds.data_ptr(), n * sl, ctx=gpu, stream=stream())
+    pres = np.stack(pats)
+    dpres = dev(pres)
+    loc = torch.empty((batch, n), dtype=torch.int16, device="cuda")
+    npa.error_locator_dev(n, dpres.data_ptr(), batch, loc.data_ptr(), ctx=gpu, stream=stream())
+    olen = (sl // 2) * 2 * k
+    hs = host(ds)
+    for lp in (loc.data_ptr(), 0):
+        out = torch.empty((batch, olen), dtype=torch.uint8, device="cuda")
+        npa.reconstruct_batch_dev2(p, ds.data_ptr(), sl, n * sl, dpres.data_ptr(), lp, batch, out.data_ptr(), olen,
+                                   ctx=gpu, stream=stream())
+        o = host(out)
+        for b in range(batch):
+            recv = [hs[b, i].tobytes() if pres[b, i] else None for i in range(n)]
+            st, want = oracle.reconstruct(recv, n, k)
+            assert st == 0
+            assert o[b].tobytes() == want, (b, bool(lp))
+            assert want[:plen] == pls[b].tobytes()
+
+
 @pytest.mark.parametrize("nw,tpw,batch,stride_pad", [(1024, 2, 8, 0), (1024, 3, 8, 0), (1024, 4, 5, 0),
                                                      (700, 4, 8, 0), (1024, 4, 8, 1), (2048, 3, 3, 0)])
 def test_encode_multi_tile_workgroups(gpu, oracle, monkeypatch, nw, tpw, batch, stride_pad):
