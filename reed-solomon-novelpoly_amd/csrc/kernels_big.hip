@@ -405,10 +405,11 @@ __host__ __device__ constexpr bool kappa_bit_used(int b) {
 template <int KB, int NQ>
 constexpr int kRecBigMaxGen = static_cast<int>(gen_of(256u * (KB / kS * NQ - 1)));
 
-// Per-payload record of the big reconstruct (k_big_records): a mode word, then
-// the row multipliers E[0..n) (u16: EXP[loc] of present rows, EXP[-loc] of
-// erased ones) and the present flags PR[0..n) (bytes), as the kernel's LDS
-// holds them.
+// Per-payload record of the big reconstruct (k_big_records): a mode word, at
+// byte 8 the occupancy of the 256-row sub-segments (bit i: rows [256 i,
+// 256 i + 256) hold a present row; n <= 16384), then the row multipliers
+// E[0..n) (u16: EXP[loc] of present rows, EXP[-loc] of erased ones) and the
+// present flags PR[0..n) (bytes), as the kernel's LDS holds them.
 constexpr uint32_t kBigSkip = 0;  // fewer than k present rows (NeedMoreShards)
 constexpr uint32_t kBigCopy = 1;  // all k systematic rows present: a copy
 constexpr uint32_t kBigDecode = 2;
@@ -535,6 +536,12 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   const uint8_t* rec = a.prefix + static_cast<size_t>(pb) * big_rec_stride(N);
   const uint32_t mode = uniform(*reinterpret_cast<const uint32_t*>(rec));
   if (mode == kBigSkip) return;  // fewer than k present rows: status NeedMoreShards
+  // sub-segments with a present row; the others are zero (absent rows are)
+  const uint64_t occ = (static_cast<uint64_t>(uniform(reinterpret_cast<const uint32_t*>(rec)[3])) << 32) |
+                       uniform(reinterpret_cast<const uint32_t*>(rec)[2]);
+  auto seg_live = [&](int q) __attribute__((always_inline)) {
+    return ((occ >> (SUBS * q)) & ((1ull << SUBS) - 1u)) != 0;
+  };
   const uint32_t col0 = tl * kTile;
   const uint32_t ncols = min(static_cast<uint32_t>(kTile), nsyms - col0);
   const uint8_t* sh = a.shards + static_cast<size_t>(pb) * a.batch_stride + 2 * static_cast<size_t>(col0);
@@ -567,6 +574,17 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
     const uint32_t index = 256u * qs;  // = KB q + 256 s
     const uint32_t gg = fresh(g);
     const uint32_t tid = fresh_v(threadIdx.x), lane = tid & 63u;  // opaque: not hoisted and spilled
+    if (!((occ >> qs) & 1u)) {  // no present row: y_qs = 0 without loads, tables or transform
+      uint32_t ZL[16] = {0}, ZH[16] = {0};
+      if (qs + 1 < static_cast<uint32_t>(SUBS * NQ)) {
+        scr_store<true>(scrY + qs * kSegScr, tid, ZL, ZH);
+      } else {
+        __syncthreads();  // every wave has read the tile
+        scr_store<false>(tile, tid, ZL, ZH);
+      }
+      if (qs < static_cast<uint32_t>(SUBS)) scr_store<true>(scrD + qs * kSegScr, tid, ZL, ZH);
+      continue;
+    }
     // the sub-segment's present rows load while the tables are staged
     uint2 rows[2][8];
 #pragma unroll
@@ -663,7 +681,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       if constexpr (kq != 0) {
         if constexpr (q == 0) {
           accumulate(x0, kq);
-        } else {
+        } else if (seg_live(q)) {
           top_inverse<SUBS>(yq[q - 1], static_cast<uint32_t>(q), top_mults<SUBS>(T, static_cast<uint32_t>(q)));
           accumulate(yq[q - 1], kq);
         }
@@ -712,7 +730,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       for_each_q(std::make_integer_sequence<int, NQ>{}, [&](auto qc) __attribute__((always_inline)) {
         constexpr int q = decltype(qc)::value;
         constexpr uint32_t kq = big_kappa<NQ>(q);
-        if constexpr (q > 0 && kq != 0) {
+        if (q > 0 && kq != 0 && seg_live(q)) {
           __builtin_amdgcn_sched_barrier(0);
           const DevTables Tq = fresh_tables(T);
           uint2 y[SUBS];
@@ -751,11 +769,12 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
         z[u][s] = scr_q<true>(scrD + s * kSegScr, j0 + u, tid);
       }
 #pragma unroll
-      for (int q = 1; q < NQ; ++q)
+      for (int q = 1; q < NQ; ++q) {  // (zeros for empty segments: skipping them here spills at k = 1024)
 #pragma unroll
         for (int s = 0; s < SUBS; ++s)
           yq[u][q - 1][s] = (q == NQ - 1 && s == SUBS - 1) ? scr_q<false>(tile, j0 + u, tid)  // this thread's own
                                                            : scr_q<true>(scrY + (SUBS * q + s) * kSegScr, j0 + u, tid);
+      }
     }
 #pragma unroll
     for (int u = 0; u < JB; ++u) fold(j0 + u, x0[u], z[u], yq[u]);
@@ -835,10 +854,13 @@ __global__ __launch_bounds__(256) void k_big_records(DevTables T, ReconstructArg
   uint16_t* E = RG ? reinterpret_cast<uint16_t*>(rec + kBigRecHeader) : El;
   uint8_t* PR = RG ? rec + kBigRecHeader + 2u * N : PRl;
   int have1 = 0, have = 0;  // present rows in [0, K) and [0, N)
+  uint64_t occ = 0;          // 256-row sub-segments with a present row
   for (int r = 0; r < N; r += 256) {
     const bool p = pres[r + static_cast<int>(tid)] != 0;
     if (r < K) have1 += __syncthreads_count(p);
-    have += __syncthreads_count(p);
+    const int c = __syncthreads_count(p);
+    have += c;
+    if (c) occ |= 1ull << (r / 256);
   }
   const bool ok = have >= K;
   if (tid == 0 && a.status) {
@@ -846,7 +868,11 @@ __global__ __launch_bounds__(256) void k_big_records(DevTables T, ReconstructArg
     a.status[2 * pb + 1] = static_cast<uint32_t>(have);
   }
   const uint32_t mode = !ok ? kBigSkip : have1 == K ? kBigCopy : kBigDecode;
-  if (tid == 0) *reinterpret_cast<uint32_t*>(rec) = mode;
+  if (tid == 0) {
+    reinterpret_cast<uint32_t*>(rec)[0] = mode;
+    reinterpret_cast<uint32_t*>(rec)[2] = static_cast<uint32_t>(occ);
+    reinterpret_cast<uint32_t*>(rec)[3] = static_cast<uint32_t>(occ >> 32);
+  }
   if (mode != kBigDecode) return;
   if (a.locators) {  // mul(x, log m) == x * EXP[m] (inc_log_mul.rs:42-49)
     const uint16_t* loc = a.locators + static_cast<size_t>(pb) * N;
@@ -872,6 +898,7 @@ constexpr size_t rec_big_lds(uint32_t n) {  // tile, tables, E (2 n bytes), PR (
 }
 // Dynamic LDS of every instance fits the CU's 160 KiB (n = 8192 exactly fills it).
 static_assert(enc_big_lds() <= 160u * 1024u, "encode LDS");
+static_assert(16384 / 256 <= 64, "sub-segment occupancy is one u64");
 static_assert(rec_big_lds(8192) <= 160u * 1024u, "largest reconstruct instance (k = 1024 / 2048, n = 8192) LDS");
 
 // Calls f(reconstruct kernel, record kernel) for the instances of (n, k);

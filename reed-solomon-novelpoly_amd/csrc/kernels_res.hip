@@ -136,13 +136,26 @@ template <int K, int NQ, int STEP>
 __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructArgs& a, uint8_t* tile,
                                          const uint8_t* pools, const uint8_t* pres, const uint8_t* sh,
                                          uint8_t* out_tile, uint32_t ncols, bool full, bool out16, uint32_t (&AL)[16],
-                                         uint32_t (&AH)[16], uint64_t* dbg) {
+                                         uint32_t (&AH)[16], uint64_t* dbg, uint32_t occ) {
   constexpr int q = res_seg<NQ>(STEP);
   constexpr int s0 = 2 + 8 * STEP;
   constexpr uint32_t I = static_cast<uint32_t>(q) * K;
   constexpr uint32_t kHD = RGeo<K>::kHD;
   const Res rr = res_coords<K>();  // opaque per step: lane-derived values are not hoisted across steps
   uint32_t XL[16], XH[16];
+  // 8 segments: a segment without a present row gives x_q = 0 (record byte 1,
+  // kernels_fast.hip segment_occupancy; e.g. the rows past wanted_n at 2,500,
+  // 3,000 and 5,000 validators): no loads, transform or exchanges, only the
+  // next step's row tables and the fold.
+  if (NQ == 8 && !((occ >> q) & 1u)) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) XL[j] = XH[j] = 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this step's table pieces (LDS-DMA into the tile)
+    if constexpr (STEP + 1 < NQ) {
+      __syncthreads();  // every wave's
+      dma_row_tables(tile, pools, static_cast<uint32_t>(res_seg<NQ>(STEP + 1)) * K, K, rr.w, rr.l, K / 64);
+    }
+  } else {
   {
     const uint32_t pm = lane_rows_present(pres, I, rr);
     uint2 raw[8];
@@ -198,6 +211,7 @@ __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructAr
   rstamp(dbg, s0 + 5);
   hd_levels_st<K, true, kResPrioDec>(T, I, XL, XH, vs);
   rstamp(dbg, s0 + 6);
+  }
   // fold x_q into d (kernels_fast.hip rec_segments)
   if constexpr (NQ == 8 && q != 0 && rec8_kappa_res(q) != 1u) {  // d ^= kappa_q x_q, kappa_q in GF(16)
     uint32_t kp[20];
@@ -242,9 +256,9 @@ template <int K, int NQ, int... STEP>
 __device__ __forceinline__ bool res_sweep(const DevTables& T, const ReconstructArgs& a, uint8_t* tile,
                                           const uint8_t* pools, const uint8_t* pres, const uint8_t* sh,
                                           uint8_t* out_tile, uint32_t ncols, bool full, bool out16,
-                                          uint32_t (&AL)[16], uint32_t (&AH)[16], uint64_t* dbg,
+                                          uint32_t (&AL)[16], uint32_t (&AH)[16], uint64_t* dbg, uint32_t occ,
                                           std::integer_sequence<int, STEP...>) {
-  return (res_step<K, NQ, STEP>(T, a, tile, pools, pres, sh, out_tile, ncols, full, out16, AL, AH, dbg) && ...);
+  return (res_step<K, NQ, STEP>(T, a, tile, pools, pres, sh, out_tile, ncols, full, out16, AL, AH, dbg, occ) && ...);
 }
 
 // One tile; NQ segments of K rows (a.n = NQ * K, or a trusted 2-segment
@@ -253,7 +267,7 @@ template <int K, int NQ>
 __device__ __forceinline__ void res_decode_tile(const DevTables& T, const ReconstructArgs& a, uint8_t* tile,
                                                 const uint8_t* pools, const uint8_t* pres, const uint8_t* sh,
                                                 uint8_t* out_tile, uint32_t ncols, bool full, bool out16,
-                                                uint64_t* dbg) {
+                                                uint64_t* dbg, uint32_t occ) {
   uint32_t AL[16], AH[16];
   uint32_t* DL = reinterpret_cast<uint32_t*>(tile + RGeo<K>::kTileBytes);  // CQ delta tables
   uint32_t* VS = DL + kDeltaWords;                                      // RStage blocks 0..NQ-1
@@ -265,7 +279,7 @@ __device__ __forceinline__ void res_decode_tile(const DevTables& T, const Recons
   stage_delta_tables(T, DL);  // the first step's barriers order both
   stage_rh_tables<K>(T, VS, NQ);
   rstamp(dbg, 1);
-  if (!res_sweep<K, NQ>(T, a, tile, pools, pres, sh, out_tile, ncols, full, out16, AL, AH, dbg,
+  if (!res_sweep<K, NQ>(T, a, tile, pools, pres, sh, out_tile, ncols, full, out16, AL, AH, dbg, occ,
                      std::make_integer_sequence<int, NQ>{}))
     return;
   constexpr uint32_t kHD = RGeo<K>::kHD, lpc = RGeo<K>::kLPC;
@@ -369,7 +383,7 @@ __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4))) void k_r
   if constexpr (SERVE == 1)
     res_copy_tile<K>(a, sh, out_tile, ncols, full, out16, T);
   else
-    res_decode_tile<K, SERVE>(T, a, smem, pools, pres, sh, out_tile, ncols, full, out16, dbg);
+    res_decode_tile<K, SERVE>(T, a, smem, pools, pres, sh, out_tile, ncols, full, out16, dbg, uniform(rec[1]));
 }
 
 }  // namespace

@@ -523,26 +523,34 @@ def test_reconstruct_prefix_modes(gpu, oracle, nw, kw, plen):
 
 
 @pytest.mark.parametrize("nw,kw,plen", [(300, 100, 64 * 256), (300, 100, 64 * 37 + 5), (700, 234, 128 * 256 + 3),
-                                        (1200, 400, 256 * 257), (512, 64, 64 * 64)])
+                                        (1200, 400, 256 * 257), (512, 64, 64 * 64), (2500, 834, 512 * 100 + 1),
+                                        (5000, 1667, 1024 * 64 + 3), (10000, 3334, 2048 * 9 + 1),
+                                        (2000, 667, 1024 * 33)])
 def test_reconstruct_empty_segments(gpu, oracle, nw, kw, plen):
-    """n = 8k fast reconstruct skips the transforms of k-row segments without a
-    present row (record byte 1, kernels_fast.hip segment_occupancy): whole
-    segments erased inside wanted_n (alone, several, all but one) and the
-    segments past wanted_n, with caller locators and with the fused locator,
-    give the oracle's bytes."""
+    """Reconstruct skips the transforms of row blocks without a present row:
+    n = 8k fast path, k-row segments (record byte 1, kernels_fast.hip
+    segment_occupancy); k >= 512, 256-row sub-segments (kernels_big.hip
+    k_big_records occupancy) and whole segments in the fold.  Whole segments
+    erased inside wanted_n (alone, several, all but one), single 256-row blocks
+    and the blocks past wanted_n, with caller locators and with the fused
+    locator, give the oracle's bytes."""
     import torch
 
     p = npa.CodeParams.derive_parameters(nw, kw)
     n, k, wn = p.n(), p.k(), p.wanted_n
-    assert n == 8 * k
+    assert n in (4 * k, 8 * k) or k >= 512
     nseg = (wn + k - 1) // k
     rng = np.random.default_rng(nw + plen)
+    blocks = [[(q * k, (q + 1) * k) for q in gone]
+              for gone in ([1], [0, 2], [0] + list(range(2, nseg)), list(range(1, nseg)), [nseg - 1], [])]
+    if k >= 512:
+        blocks += [[(256, 512)], [(0, 256), (k + 512, k + 768)], [(k - 256, k), (2 * k, 2 * k + 256)]]
     pats = []
-    for gone in ([1], [0, 2], [0] + list(range(2, nseg)), list(range(1, nseg)), [nseg - 1], []):
+    for bl in blocks:
         pres = np.zeros(n, np.uint8)
         pres[:wn] = 1
-        for q in gone:
-            pres[q * k:(q + 1) * k] = 0
+        for r0, r1 in bl:
+            pres[r0:r1] = 0
         if pres.sum() > k + 8:  # a few random erasures in what is left
             idx = np.flatnonzero(pres)
             pres[rng.choice(idx, min(len(idx) - k, 5), replace=False)] = 0

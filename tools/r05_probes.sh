@@ -108,14 +108,22 @@ p7() {  # empty-segment skip (n = 8k fast reconstruct): parity tests, then 300 /
   timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fuzz.py tests/test_gpu_noncodeword.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r05/pytest_p7.log 2>&1; rc=$?
   echo "tests: $(tail -1 gpurun_out/r05/pytest_p7.log)"
   [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r05/pytest_p7.log | head -20; exit $rc; }
-  for vc in 300 700 1200 5000; do
-    for lib in prod base; do
+  for vc in ${VCS:-300 700 1200 5000}; do
+    for lib in ${LIBS:-prod base}; do
       path=$PWD/reed-solomon-novelpoly_amd/lib/libnovelpoly_hip.so
-      [ $lib = base ] && path=$PWD/tools/exp/lib_base.so
+      [ $lib != prod ] && path=$PWD/tools/exp/lib_$lib.so
       NP_LIB_PATH=$path timeout -k 10 300 python bench.py --no-cpu --steps 10 --warmup 3 --n-wanted $vc --erase $(( (vc - 1) / 3 + 1 )) > gpurun_out/r05/seg_${vc}_$lib.log 2>&1 || exit $?
       tail -1 gpurun_out/r05/seg_${vc}_$lib.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('vc$vc $lib', d['value'], d['config'].get('batch'), {k:v['ms'] for k,v in d['kernels'].items()})"
     done
   done
+}
+
+p8() {  # empty sub-segment skip, k >= 512 (kernels_big.hip)
+  VCS="2500 3000 5000 10000 2000" p7
+}
+
+p9() {  # empty-segment skip in the resident decodes (k = 512 / 1024, n = 8k)
+  VCS="2500 3000 5000" LIBS="prod k1024 base" p7
 }
 
 p1() {  # the host-pipeline fix: whole suite, smoke, bench, e2e
