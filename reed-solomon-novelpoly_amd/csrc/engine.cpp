@@ -336,8 +336,9 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
   }
   const size_t huge_per = np::huge_reconstruct_scratch_per_payload(a.shard_len, a.n, a.k);
   if (path == RecPath::Huge) {
-    // per payload: tile slots, mode byte, locators (unless the caller's), status
-    const size_t side = 16 + (a.locators ? 0 : 2 * static_cast<size_t>(a.n)) + own_status;
+    // per payload: tile slots, mode byte and occupancy word, locators (unless
+    // the caller's), status
+    const size_t side = 32 + (a.locators ? 0 : 2 * static_cast<size_t>(a.n)) + own_status;
     const size_t per = std::max<size_t>(1, kBigScratchCap / (huge_per + side));
     for (size_t b0 = 0; b0 < a.batch; b0 += per) {
       np::ReconstructArgs sub = slice(a, b0, std::min(per, a.batch - b0));
@@ -347,7 +348,7 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
       uint8_t* side0 = scr + sub.batch * huge_per;  // huge_per is a multiple of 128 KiB
       uint16_t* loc = reinterpret_cast<uint16_t*>(side0);
       uint8_t* mode = side0 + (a.locators ? 0 : 2 * static_cast<size_t>(a.n) * sub.batch);
-      if (!a.status) sub.status = reinterpret_cast<uint32_t*>(mode + (sub.batch + 15) / 16 * 16);
+      if (!a.status) sub.status = reinterpret_cast<uint32_t*>(mode + np::huge_side_bytes(sub.batch));
       if (e == hipSuccess) e = HIP(np::launch_reconstruct_huge(c->T, sub, scr, mode, loc, s));
       e = big_done(c, s, e);
       if (e != hipSuccess) return e;

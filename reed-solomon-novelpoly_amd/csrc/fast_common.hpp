@@ -356,6 +356,9 @@ __device__ __forceinline__ void spool_of(const DevTables& T, uint32_t c, uint32_
 }
 
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+  return (static_cast<uint64_t>(uniform(static_cast<uint32_t>(v >> 32))) << 32) | uniform(static_cast<uint32_t>(v));
+}
 
 // A wave-uniform value the compiler must treat as new here: stops common
 // subexpressions (row offsets, table indices) of different phases from being

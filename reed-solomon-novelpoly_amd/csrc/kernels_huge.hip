@@ -29,11 +29,13 @@
 //                   rows sk + 1024 m ...
 // Reconstruct (inc_reconstruct.rs:1-113, mod.rs:162-239; the fold of
 // kernels_fast.hip / DESIGN.md §4.3 with n = NQ k):
-//   k_huge_records  status and mode per payload (skip / copy / decode);
+//   k_huge_records  status and mode per payload (skip / copy / decode), and
+//                   which 1024-row blocks hold a present row;
 //   locators        the generic 65536-point Walsh kernel (or the caller's);
 //   k_huge_rec_inv  per (q, m): premultiplied rows q k + 1024 m ..,
 //                   IFFT(1024, q k + 1024 m) -> slot q M + m; q = 0 also
-//                   D_1024 of it -> slot NQ M + m;
+//                   D_1024 of it -> slot NQ M + m; nothing for a block
+//                   without a present row (zero: the rows past wanted_n);
 //   k_huge_rec_top  per (j, t): x_q = Top^-1_{qk}, d = D_k(x_0) ^ sum kappa_q
 //                   x_q with D_k = (D_1024 lifted) ^ the high single-bit
 //                   terms x_0[m | 2^L] (kernels_big.hip's argument), then
@@ -61,6 +63,7 @@ struct HugeArgs {
   uint8_t* scr;         // tile slots of the slice: tile (pb, tl) at (pb tiles + tl) slots kSlotBytes
   const uint16_t* loc;  // reconstruct: locators, batch x n (log form)
   const uint8_t* mode;  // reconstruct: per payload kHugeSkip / kHugeCopy / kHugeDecode
+  const uint64_t* occ;  // reconstruct: per payload, bit u: rows 1024 u .. + 1023 hold a present row
   uint32_t tiles, slots, M, K, NQ;
   // encode, payloads of at most 32 columns: a tile holds two payloads
   // (columns 0-31 payload 2 pb, 32-63 payload 2 pb + 1; load_pay_tile_pair)
@@ -87,6 +90,12 @@ __device__ __forceinline__ uint32_t tile_mode(const HugeArgs& h, size_t pt) {
   const uint32_t m0 = h.mode[2 * pt];
   const uint32_t m1 = 2 * pt + 1 < h.batch ? h.mode[2 * pt + 1] : kHugeSkip;
   return m0 > m1 ? m0 : m1;
+}
+// Blocks of tile pt's payload(s) with a present row (a paired tile: either
+// payload's); the slots of the others are zero and never written.
+__device__ __forceinline__ uint64_t tile_occ(const HugeArgs& h, size_t pt) {
+  if (!h.pair) return h.occ[pt / h.tiles];
+  return h.occ[2 * pt] | (2 * pt + 1 < h.batch ? h.occ[2 * pt + 1] : 0ull);
 }
 // The units a launch's workgroups enumerate per sub-transform: tiles, or
 // pairs of payloads.
@@ -283,16 +292,19 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
 // else the full decode from every present row.
 // Thread t counts the present flags of rows 4 (t + 256 i) .. + 3 (one dword
 // each; n is a multiple of 1024), then one block sum.
-__global__ __launch_bounds__(256) void k_huge_records(ReconstructArgs a, uint8_t* mode) {
+// Iteration i covers block i (rows 1024 i .. + 1023): its occupancy bit.
+__global__ __launch_bounds__(256) void k_huge_records(ReconstructArgs a, uint8_t* mode, uint64_t* occ) {
   __shared__ int part[2][4];
   const uint32_t pb = blockIdx.x;
   const uint8_t* pres = a.present + static_cast<size_t>(pb) * a.n;
   int c1 = 0, c = 0;
-  for (uint32_t v = 4u * threadIdx.x; v < a.n; v += 1024u) {
+  uint64_t oc = 0;
+  for (uint32_t v = 4u * threadIdx.x, i = 0; v < a.n; v += 1024u, ++i) {
     const uint32_t w = *reinterpret_cast<const uint32_t*>(pres + v);  // the flags are 0 / 1 bytes
     const int cnt = ((w & 0xffu) != 0) + ((w & 0xff00u) != 0) + ((w & 0xff0000u) != 0) + ((w >> 24) != 0);
     c += cnt;
     if (v < a.k) c1 += cnt;
+    if (__syncthreads_or(cnt)) oc |= 1ull << i;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -310,6 +322,7 @@ __global__ __launch_bounds__(256) void k_huge_records(ReconstructArgs a, uint8_t
       a.status[2 * pb + 1] = static_cast<uint32_t>(have);
     }
     mode[pb] = !ok ? kHugeSkip : have1 == static_cast<int>(a.k) ? kHugeCopy : kHugeDecode;
+    occ[pb] = oc;
   }
 }
 
@@ -321,6 +334,8 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
   const SubRef sr = sub_of(h, blockIdx.x, unit_count(h, a.batch));
   const uint32_t pb = sr.pb, tl = sr.tl;  // pb: the pair of payloads 2 pb, 2 pb + 1 (HugeArgs::pair)
   if (uniform(tile_mode(h, static_cast<size_t>(pb) * h.tiles + tl)) != kHugeDecode) return;
+  // no present row: the slot is zero (k_huge_rec_top reads none)
+  if (!((uniform64(tile_occ(h, static_cast<size_t>(pb) * h.tiles + tl)) >> sr.u) & 1u)) return;
   const uint32_t col0 = tl * kRC, ncols = min(static_cast<uint32_t>(kRC), nsyms - col0);
   const uint32_t I = kSK * sr.u;  // rows I .. I + 1023: segment u / M, sub-segment u % M
   const Res r = res_coords<kSK>();
@@ -424,12 +439,17 @@ __global__ __launch_bounds__(256) void k_huge_rec_top(DevTables T, HugeArgs h, s
   if (uniform(tile_mode(h, pt)) != kHugeDecode) return;
   uint8_t* base = h.scr + pt * h.slots * kSlotBytes + (gid & 16383u) * 8u;
   auto at = [&](uint32_t slot) __attribute__((always_inline)) { return base + static_cast<size_t>(slot) * kSlotBytes; };
+  // blocks without a present row: zero slots that k_huge_rec_inv skipped
+  const uint64_t oc = uniform64(tile_occ(h, pt));
+  auto ld = [&](uint32_t u, uint32_t slot) __attribute__((always_inline)) {
+    return ((oc >> u) & 1u) ? *reinterpret_cast<const uint2*>(at(slot)) : make_uint2(0u, 0u);
+  };
   uint2 d[M], x[M];
   // x_0 and the lifted D_1024(y_0)
 #pragma unroll
   for (int m = 0; m < M; ++m) {
-    x[m] = *reinterpret_cast<const uint2*>(at(m));
-    d[m] = *reinterpret_cast<const uint2*>(at(NQ * M + m));
+    x[m] = ld(m, m);
+    d[m] = ld(m, NQ * M + m);
   }
   top_inverse_h<M>(T, x, 0u);
   top_inverse_h<M>(T, d, 0u);
@@ -448,8 +468,9 @@ __global__ __launch_bounds__(256) void k_huge_rec_top(DevTables T, HugeArgs h, s
   }
 #pragma unroll
   for (int q = 1; q < NQ; ++q) {
+    if (!((oc >> (q * M)) & ((1ull << M) - 1u))) continue;  // x_q = 0
 #pragma unroll
-    for (int m = 0; m < M; ++m) x[m] = *reinterpret_cast<const uint2*>(at(q * M + m));
+    for (int m = 0; m < M; ++m) x[m] = ld(q * M + m, q * M + m);
     top_inverse_h<M>(T, x, uniform(q * h.K));
     const uint32_t kq = huge_kappa<NQ>(q);
     if (kq == 1u) {
@@ -699,7 +720,8 @@ hipError_t launch_reconstruct_huge(const DevTables& T, const ReconstructArgs& a,
   const size_t nsyms = a.shard_len / 2;
   if (a.batch == 0) return hipSuccess;
   if (a.batch > 0x7fffffffu || nsyms > 0xffffffffu) return hipErrorInvalidValue;
-  k_huge_records<<<static_cast<uint32_t>(a.batch), 256, 0, s>>>(a, mode);
+  uint64_t* occ = reinterpret_cast<uint64_t*>(mode + (a.batch + 15) / 16 * 16);
+  k_huge_records<<<static_cast<uint32_t>(a.batch), 256, 0, s>>>(a, mode, occ);
   hipError_t e = hipGetLastError();
   if (nsyms == 0 || e != hipSuccess) return e;
   const uint16_t* loc = a.locators;
@@ -716,6 +738,7 @@ hipError_t launch_reconstruct_huge(const DevTables& T, const ReconstructArgs& a,
   HugeArgs h = huge_args(scratch, a.n, a.k, tiles, (a.n + a.k) / kSK);
   h.loc = loc;
   h.mode = mode;
+  h.occ = occ;
   h.per = static_cast<uint32_t>(per);
   h.pair = pair ? 1u : 0u;
   h.batch = static_cast<uint32_t>(a.batch);

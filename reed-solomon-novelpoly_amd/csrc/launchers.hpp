@@ -143,7 +143,9 @@ bool huge_reconstruct_supported(uint32_t n, uint32_t k);  // n / k in {2, 4, 8}
 size_t huge_encode_scratch_per_payload(size_t shard_len, uint32_t n, uint32_t k);
 size_t huge_reconstruct_scratch_per_payload(size_t shard_len, uint32_t n, uint32_t k);
 hipError_t launch_encode_huge(const DevTables& T, const EncodeArgs& a, uint8_t* scratch, hipStream_t s);
-// mode: batch bytes; locators: batch x n u16 (unused when a.locators is set)
+// side: huge_side_bytes(batch) (per-payload mode bytes, then the 1024-row
+// block occupancy words); locators: batch x n u16 (unused when a.locators is set)
+constexpr size_t huge_side_bytes(size_t batch) { return (batch + 15) / 16 * 16 + 8 * batch; }
 hipError_t launch_reconstruct_huge(const DevTables& T, const ReconstructArgs& a, uint8_t* scratch, uint8_t* mode,
                                    uint16_t* locators, hipStream_t s);
 hipError_t configure_huge_kernels();

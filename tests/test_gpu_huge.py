@@ -32,8 +32,11 @@ def test_huge_encode(gpu, oracle, nw, kw, plen):
     assert not bad, f"{len(bad)} shards differ, first {bad[:5]}"
 
 
-# erase: number of random erasures; -1: every systematic shard lost; 0: none (copy)
-REC = [(16384, 5462, 2 * 4096 * 64, 8000), (16384, 5462, 2 * 4096 * 70 + 3, -1), (20000, 6667, 2 * 4096 * 65, 13333),
+# erase: number of random erasures; -1: every systematic shard lost; 0: none (copy);
+# -2: whole 1024-row blocks (0, 3 and the second k-row segment: k_huge_rec_inv
+# skips blocks without a present row, k_huge_rec_top reads them as zero)
+REC = [(20000, 6667, 2 * 4096 * 65, -2), (40000, 13334, 2 * 8192 * 66 + 1, -2), (16384, 5462, 2 * 4096 * 64, -2),
+       (16384, 5462, 2 * 4096 * 64, 8000), (16384, 5462, 2 * 4096 * 70 + 3, -1), (20000, 6667, 2 * 4096 * 65, 13333),
        (20000, 6667, 2 * 4096 * 2, 0), (30000, 10000, 2 * 8192 * 64 + 5, 20000), (30000, 10000, 2 * 8192 * 3, -1),
        (40000, 13334, 2 * 8192 * 66, 26666), (65536, 21846, 2 * 16384 * 65 + 7, 43690),
        (65536, 21846, 2 * 16384 * 2, -1)]
@@ -48,6 +51,8 @@ def test_huge_reconstruct(gpu, oracle, nw, kw, plen, erase):
     shards = p.make_encoder(gpu).encode(pl)
     if erase == -1:
         gone = set(range(k))
+    elif erase == -2:
+        gone = set(range(1024)) | set(range(3072, 4096)) | set(range(k, 2 * k))
     else:
         gone = set(synth.erasure_indices(plen + erase, nw, min(erase, nw - k)).tolist())
     recv = [None if i in gone else s for i, s in enumerate(shards[:nw])]
@@ -95,8 +100,11 @@ def test_huge_encode_paired_batch(gpu, oracle, nw, kw, plen, batch):
 # two payloads' modes, each lane half merges and writes for its own payload.
 # Mixed modes per pair: random erasures (decode), only parity lost (copy),
 # every systematic shard lost, fewer than k shards (NeedMoreShards: status
-# set, output untouched), and a non-codeword (a corrupted present shard).
+# set, output untouched), a non-codeword (a corrupted present shard), and
+# whole 1024-row blocks erased (a pair's blocks are skipped where neither
+# payload has a present row).
 PAIR_REC = [(65536, 21846, 2 * 16384 * 32, ["rand", "copy", "nosys", "rand"]),
+            (65536, 21846, 2 * 16384 * 9, ["blocks", "blocks2", "blocks", "rand", "blocks2"]),
             (65536, 21846, 2 * 16384 * 17 + 3, ["copy", "rand", "few", "corrupt", "rand"]),
             (50000, 16667, 2 * 16384 * 5, ["few", "rand", "rand"])]
 
@@ -131,6 +139,13 @@ def test_huge_reconstruct_paired_batch(gpu, oracle, nw, kw, plen, kinds):
             pres[b, :k] = 0
         elif kind == "few":
             pres[b, rng.choice(nw, nw - k + 1, replace=False)] = 0
+        elif kind == "blocks":  # blocks 0, 5, 17-20 and 40-63
+            for u in [0, 5, 17, 18, 19, 20] + list(range(40, n // 1024)):
+                pres[b, 1024 * u:1024 * (u + 1)] = 0
+        elif kind == "blocks2":  # blocks 5, 6 and 33-63, and random rows
+            for u in [5, 6] + list(range(33, n // 1024)):
+                pres[b, 1024 * u:1024 * (u + 1)] = 0
+            pres[b, rng.choice(1024 * 30, 5000, replace=False)] = 0
         if kind == "corrupt":
             v = int(rng.choice(np.flatnonzero(pres[b])))
             hs[b, v * sl:(v + 1) * sl] ^= 0x3C

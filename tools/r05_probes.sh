@@ -126,6 +126,20 @@ p9() {  # empty-segment skip in the resident decodes (k = 512 / 1024, n = 8k)
   VCS="2500 3000 5000" LIBS="prod k1024 base" p7
 }
 
+p10() {  # empty 1024-row blocks in the sub-transform decode: huge tests, then 20,000 .. 65,536 validators
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_huge.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r05/pytest_huge_p10.log 2>&1; rc=$?
+  echo "huge tests: $(tail -1 gpurun_out/r05/pytest_huge_p10.log)"
+  [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r05/pytest_huge_p10.log | head -20; exit $rc; }
+  for vc in 20000 40000 50000 65536; do
+    for lib in prod base; do
+      path=$PWD/reed-solomon-novelpoly_amd/lib/libnovelpoly_hip.so
+      [ $lib != prod ] && path=$PWD/tools/exp/lib_$lib.so
+      NP_LIB_PATH=$path timeout -k 10 300 python bench.py --no-cpu --steps 3 --warmup 1 --batch 512 --n-wanted $vc --erase $(( (vc - 1) / 3 + 1 )) > gpurun_out/r05/blk_${vc}_$lib.log 2>&1 || exit $?
+      tail -1 gpurun_out/r05/blk_${vc}_$lib.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('vc$vc $lib', d['value'], {k:v['ms'] for k,v in d['kernels'].items()}, d.get('roundtrip_ok'))"
+    done
+  done
+}
+
 p1() {  # the host-pipeline fix: whole suite, smoke, bench, e2e
   suite p1 && bench p1 && e2e p1
 }
