@@ -192,20 +192,134 @@ __device__ void lds_walsh(uint16_t* v, uint32_t size) {
   }
 }
 
+// The locator of one payload in registers: position i of the 65536-point
+// Walsh transforms lives in thread t, register r of one of three layouts,
+// each holding a different 6 (or 4) bits of i in r, so each pass of levels
+// runs in registers and the passes meet through the LDS (four exchanges
+// instead of one barrier per level):
+//   A  i = 64 t + r                      levels 0-5   (r = bits 0-5)
+//   B  i = 4096 w + 64 r + lane          levels 6-11  (t = 64 w + lane)
+//   C  i = 1024 r + t                    levels 12-15 (r bits 2-5)
+// The first transform (of 0 / 1 erasure flags) is exact in integers, so its
+// levels run in any order (C, B, A) and one reduction mod 65535 follows
+// (only its residue enters the product, inc_reconstruct.rs:103-106).  The
+// second keeps the reference's per-level end-around-carry form and its level
+// order 0..15 (inc_log_mul.rs:92-114), which decides whether a zero residue
+// reads 0 or 65535.
+// LDS slot of position i: i + 2 (i >> 6), one dword of padding per 64
+// positions, so A's 64-position stride falls on distinct banks and every
+// layout's address is a per-thread base plus a constant (65536 + 2048 u16 =
+// 132 KiB).
+constexpr uint32_t kLocLdsBytes = 2u * (65536u + 2048u);
+
+template <int B0, int NB>
+__device__ __forceinline__ void walsh_exact(int32_t (&v)[64]) {
+#pragma unroll
+  for (int b = B0; b < B0 + NB; ++b)
+#pragma unroll
+    for (int r = 0; r < 64; ++r)
+      if (!(r & (1 << b))) {
+        const int32_t x = v[r], y = v[r | (1 << b)];
+        v[r] = x + y;
+        v[r | (1 << b)] = x - y;
+      }
+}
+template <int B0, int NB>
+__device__ __forceinline__ void walsh_fold(uint32_t (&v)[64]) {
+#pragma unroll
+  for (int b = B0; b < B0 + NB; ++b)
+#pragma unroll
+    for (int r = 0; r < 64; ++r)
+      if (!(r & (1 << b))) {
+        const uint32_t x = v[r], y = v[r | (1 << b)];
+        const uint32_t s = x + y, d = x + kQ - y;
+        v[r] = static_cast<uint16_t>(s + (s >> 16));  // (s & 0xffff) + (s >> 16), at most 65535
+        v[r | (1 << b)] = static_cast<uint16_t>(d + (d >> 16));
+      }
+}
+
+// BLK: n is a multiple of 1024, so rows 1024 r + t < n for r < n / 1024 (a
+// wave-uniform test); otherwise the test is per row.
+template <bool BLK>
 __global__ __launch_bounds__(1024) void k_error_locator(DevTables T, uint32_t n, const uint8_t* present,
                                                         uint16_t* locators) {
   extern __shared__ uint16_t lw[];
   const size_t b = blockIdx.x;
   const uint8_t* pres = present + b * n;
-  for (uint32_t i = threadIdx.x; i < 65536u; i += blockDim.x) lw[i] = (i < n && !pres[i]) ? 1 : 0;
+  const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
+  const uint32_t nr = BLK ? __builtin_amdgcn_readfirstlane(n >> 10) : (n > t ? (n - t + 1023u) >> 10 : 0u);
+  auto in_n = [&](int r) { return static_cast<uint32_t>(r) < nr; };  // row 1024 r + t < n
+  // LDS slots i + 2 (i >> 6) of the three layouts as a per-thread base (opaque,
+  // so no phase keeps another's 64 addresses live) plus a constant per r
+  auto base = [](uint32_t v) {
+    asm volatile("" : "+v"(v));
+    return v;
+  };
+  auto sa = [&](int r) { return base(66u * t) + r; };                 // A: i = 64 t + r
+  auto sb = [&](int r) { return base(4224u * w + lane) + 66u * r; };  // B: i = 4096 w + 64 r + lane
+  auto sc = [&](int r) { return base(t + 2u * w) + 1056u * r; };      // C: i = 1024 r + t
+  // ---- Walsh of the erasure flags (i < n), exact: levels 12-15 in C, then B, A
+  int32_t e[64];
+  uint32_t er[2] = {0u, 0u};  // bit r: row 1024 r + t erased (kept for the output)
+#pragma unroll
+  for (int r = 0; r < 64; ++r) {
+    e[r] = in_n(r) ? (pres[t + 1024u * r] == 0) : 0;
+    er[r >> 5] |= static_cast<uint32_t>(e[r]) << (r & 31);
+    if ((r & 15) == 15) __builtin_amdgcn_sched_barrier(0);  // 16 loads in flight, not 64 addresses live
+  }
+  asm volatile("" : "+v"(er[0]), "+v"(er[1]));  // the mask now, not 64 flags kept to the end
+  walsh_exact<2, 4>(e);  // C: i bits 12-15 are r bits 2-5
+#pragma unroll
+  for (int r = 0; r < 64; ++r) lw[sc(r)] = static_cast<uint16_t>(e[r]);  // |e| <= 16
   __syncthreads();
-  lds_walsh(lw, 65536u);
-  for (uint32_t i = threadIdx.x; i < 65536u; i += blockDim.x)
-    lw[i] = static_cast<uint16_t>((static_cast<uint32_t>(lw[i]) * T.log_walsh[i]) % kQ);
+#pragma unroll
+  for (int r = 0; r < 64; ++r) e[r] = static_cast<int16_t>(lw[sb(r)]);
+  walsh_exact<0, 6>(e);  // B: levels 6-11
   __syncthreads();
-  lds_walsh(lw, 65536u);
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
-    locators[b * n + i] = pres[i] ? lw[i] : static_cast<uint16_t>(kQ - lw[i]);
+#pragma unroll
+  for (int r = 0; r < 64; ++r) lw[sb(r)] = static_cast<uint16_t>(e[r]);  // |e| <= 1024
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 64; ++r) e[r] = static_cast<int16_t>(lw[sa(r)]);
+  walsh_exact<0, 6>(e);  // A: levels 0-5; |e| <= 65536
+  // ---- times LOG_WALSH mod 65535 (inc_reconstruct.rs:103-106), in A
+  uint32_t v[64];
+  const uint4* lwt = reinterpret_cast<const uint4*>(T.log_walsh + 64u * t);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const uint4 m = lwt[q];
+    const uint32_t mm[4] = {m.x, m.y, m.z, m.w};
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+      const int r = 8 * q + h;
+      const int32_t c = e[r] % static_cast<int32_t>(kQ);
+      const uint32_t res = static_cast<uint32_t>(c < 0 ? c + static_cast<int32_t>(kQ) : c);
+      v[r] = (res * ((mm[h >> 1] >> (16 * (h & 1))) & 0xffffu)) % kQ;
+    }
+  }
+  // ---- second Walsh, the reference's form and order: A (0-5), B (6-11), C (12-15)
+  walsh_fold<0, 6>(v);
+  __syncthreads();  // every wave has read the first transform's A values
+#pragma unroll
+  for (int r = 0; r < 64; ++r) lw[sa(r)] = static_cast<uint16_t>(v[r]);
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 64; ++r) v[r] = lw[sb(r)];
+  walsh_fold<0, 6>(v);
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 64; ++r) lw[sb(r)] = static_cast<uint16_t>(v[r]);
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 64; ++r) v[r] = lw[sc(r)];
+  walsh_fold<2, 4>(v);
+  // erased rows: ONEMASK - value (inc_reconstruct.rs:108-112)
+#pragma unroll
+  for (int r = 0; r < 64; ++r) {
+    if (in_n(r))
+      locators[b * n + t + 1024u * r] = static_cast<uint16_t>(((er[r >> 5] >> (r & 31)) & 1u) ? kQ - v[r] : v[r]);
+    if ((r & 15) == 15) __builtin_amdgcn_sched_barrier(0);
+  }
 }
 
 // mod.rs:171-180: a payload with fewer than k present rows is NeedMoreShards
@@ -312,7 +426,8 @@ hipError_t configure_generic_kernels() {
   };
   set(reinterpret_cast<const void*>(&k_encode_generic));
   set(reinterpret_cast<const void*>(&k_reconstruct_generic));
-  set(reinterpret_cast<const void*>(&k_error_locator));
+  set(reinterpret_cast<const void*>(&k_error_locator<true>));
+  set(reinterpret_cast<const void*>(&k_error_locator<false>));
   set(reinterpret_cast<const void*>(&k_afft_cols<true>));
   set(reinterpret_cast<const void*>(&k_afft_cols<false>));
   set(reinterpret_cast<const void*>(&k_walsh));
@@ -344,7 +459,10 @@ hipError_t launch_reconstruct_generic(const DevTables& T, const ReconstructArgs&
 hipError_t launch_error_locator(const DevTables& T, uint32_t n, const uint8_t* present, size_t batch,
                                 uint16_t* locators, hipStream_t s) {
   if (batch == 0) return hipSuccess;
-  k_error_locator<<<static_cast<uint32_t>(batch), 1024, 65536 * sizeof(uint16_t), s>>>(T, n, present, locators);
+  if (n % 1024u == 0)
+    k_error_locator<true><<<static_cast<uint32_t>(batch), 1024, kLocLdsBytes, s>>>(T, n, present, locators);
+  else
+    k_error_locator<false><<<static_cast<uint32_t>(batch), 1024, kLocLdsBytes, s>>>(T, n, present, locators);
   return hipGetLastError();
 }
 

@@ -118,6 +118,34 @@ def test_encode_low_and_decode_main_dev_golden(gpu, golden_vectors, oracle):
         assert np.array_equal(from_dev_u16(ct), g[key + "_decoded"]), key
 
 
+@pytest.mark.parametrize("n", [2, 16, 256, 1024, 4096, 16384, 32768, 65536])
+def test_error_locator_dev_vs_oracle(gpu, oracle, n):
+    """np_error_locator_dev (kernels_generic.hip k_error_locator: the two
+    65536-point Walsh transforms in registers, three layouts) against the
+    oracle's eval_error_polynomial (inc_reconstruct.rs:90-113), including the
+    patterns whose zero residues read 65535 (no erasure, every row erased)."""
+    import torch
+
+    rng = np.random.default_rng(n)
+    pats = [np.ones(n, np.uint8), np.zeros(n, np.uint8)]
+    for frac in (0.5, 0.1, 0.9):
+        pats.append((rng.random(n) >= frac).astype(np.uint8))
+    one = np.ones(n, np.uint8)
+    one[n // 2] = 0
+    pats.append(one)
+    half = np.ones(n, np.uint8)
+    half[: n // 2] = 0
+    pats.append(half)
+    pres = np.stack(pats)
+    dpres = dev(pres)
+    loc = torch.empty((len(pats), n), dtype=torch.int16, device="cuda")
+    npa.error_locator_dev(n, dpres.data_ptr(), len(pats), loc.data_ptr(), ctx=gpu, stream=stream())
+    got = host(loc).view(np.uint16)
+    for b, p in enumerate(pats):
+        want = oracle.eval_error_polynomial(1 - p)[:n]
+        assert np.array_equal(got[b], want), (b, np.flatnonzero(got[b] != want)[:5])
+
+
 # ---------------------------------------------------------- crate surface ----
 def test_api_cases_golden(gpu, golden_json):
     for case in golden_json("api_cases.json"):

@@ -140,6 +140,36 @@ p10() {  # empty 1024-row blocks in the sub-transform decode: huge tests, then 2
   done
 }
 
+p11() {  # register-resident error locator: locator + parity + huge tests, then huge benches against HEAD's library
+  if [ -z "$BENCH_ONLY" ]; then
+    timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_huge.py tests/test_gpu_noncodeword.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r05/pytest_p11.log 2>&1; rc=$?
+    echo "tests: $(tail -1 gpurun_out/r05/pytest_p11.log)"
+    [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r05/pytest_p11.log | head -20; exit $rc; }
+  fi
+  for vc in 65536 40000 20000; do
+    for lib in prod base; do
+      path=$PWD/reed-solomon-novelpoly_amd/lib/libnovelpoly_hip.so
+      [ $lib != prod ] && path=$PWD/tools/exp/lib_$lib.so
+      NP_LIB_PATH=$path timeout -k 10 300 python bench.py --no-cpu --steps 3 --warmup 1 --batch 512 --n-wanted $vc --erase $(( (vc - 1) / 3 + 1 )) > gpurun_out/r05/loc_${vc}_$lib.log 2>&1 || exit $?
+      tail -1 gpurun_out/r05/loc_${vc}_$lib.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('vc$vc $lib', d['value'], {k:v['ms'] for k,v in d['kernels'].items()}, d.get('roundtrip_ok'))"
+    done
+  done
+  export TMPDIR=/tmp
+  out=$PWD/gpurun_out/r05/prof_loc_65536
+  mkdir -p $out
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out --output-format csv -- python3 bench.py --no-cpu --steps 3 --warmup 1 --batch 512 --n-wanted 65536 --erase 21846 > $out/bench.log 2>&1 || exit $?
+  f=$(find $out -name "*kernel_stats.csv" | head -1)
+  python3 -c "
+import csv
+rows=list(csv.DictReader(open('$f')))
+for r in sorted(rows, key=lambda r: -float(r['TotalDurationNs']))[:12]:
+    print('  %-60s calls %5s avg %9.1f us total %8.2f ms' % (r['Name'][:60], r['Calls'], float(r['AverageNs'])/1e3, float(r['TotalDurationNs'])/1e6))"
+}
+
+p12() {  # the register-resident locator: whole GPU suite and smoke, then p11's benches and profile
+  suite p12 && BENCH_ONLY=1 p11
+}
+
 p1() {  # the host-pipeline fix: whole suite, smoke, bench, e2e
   suite p1 && bench p1 && e2e p1
 }
