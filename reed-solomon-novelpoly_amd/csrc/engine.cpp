@@ -677,14 +677,17 @@ int np_encode_batch_dev(np_ctx* c, const np_code_params* p, const uint8_t* d_pay
 //  - pinned by the caller (hipHostMalloc, torch pin_memory, hipHostRegister;
 //    mapped_host_range finds it): DMA, or the present-row gather kernel,
 //    straight from / to it;
-//  - pinned in place for the call through the process-wide PinRegistry
-//    (pageable spans of at least kPinMinBytes): the same;
+//  - with NP_PAGEABLE=pin (opt-in), pinned in place for the call through the
+//    process-wide PinRegistry (pageable spans of at least kPinMinBytes): the
+//    same;
 //  - staged: host threads copy it into / out of the context's pinned staging
 //    slots, and the DMA or the gather runs from / to those.
 // Round 4 still let the runtime copy pageable spans whose rows were not
 // 4-byte aligned (hipMemcpy2DAsync from a numpy array, right after the same
 // pages had been registered and unregistered), and one GPU run faulted in
-// that call.
+// that call.  Round 5 saw one more illegal address in a
+// process that had pinned numpy buffers in place earlier (in device-only
+// calls, not traced to any kernel), so pinning in place is opt-in.
 namespace {
 
 constexpr size_t kPipeSlotBytes = size_t(64) << 20;
@@ -816,11 +819,12 @@ const uint8_t* mapped_host_range(const uint8_t* p, size_t bytes) {
   return d0;
 }
 
-// Pageable buffers are pinned in place (default) or, with NP_PAGEABLE=stage,
-// always staged through pinned memory by host threads (read per call).
+// Pageable buffers are staged through pinned memory by host threads
+// (default), or with NP_PAGEABLE=pin pinned in place for the call (read per
+// call).
 bool pageable_pin() {
   const char* m = std::getenv("NP_PAGEABLE");
-  return !m || (std::strcmp(m, "stage") != 0 && std::strcmp(m, "gather") != 0);
+  return m && std::strcmp(m, "pin") == 0;
 }
 
 // A host span for the length of a call: its device address when the caller

@@ -14,6 +14,18 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
+    config.addinivalue_line("markers", "pin_in_place: NP_PAGEABLE=pin cases, run in a child process "
+                            "(test_gpu_pin_isolated.py) so that the rest of the suite never shares a "
+                            "process with buffers the engine registered in place")
+
+
+def pytest_collection_modifyitems(config, items):
+    if os.environ.get("NP_PIN_CHILD"):
+        return
+    skip = pytest.mark.skip(reason="NP_PAGEABLE=pin case: runs in the child process of test_gpu_pin_isolated.py")
+    for it in items:
+        if it.get_closest_marker("pin_in_place"):
+            it.add_marker(skip)
 
 
 @pytest.fixture(scope="session")

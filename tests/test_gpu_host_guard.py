@@ -4,8 +4,9 @@ encode then reconstruct on the SAME buffer -- the sequence of
 test_host_pipeline_all_systematic[12289-4097-73728-3-pageable], where the
 encode pinned and unpinned the numpy buffer and the reconstruct then handed it
 to the runtime's pageable 2-D copies.  The engine now never passes a pageable
-pointer to a HIP copy (engine.cpp, host-memory pipeline: pinned in place
-through the process-wide registry, or staged by host threads).
+pointer to a HIP copy (engine.cpp, host-memory pipeline: staged by host
+threads, or with NP_PAGEABLE=pin pinned in place through the process-wide
+registry; those cases run in a child process, test_gpu_pin_isolated.py).
 
 Every host and device buffer sits between guard bytes, checked after every
 call: the engine must neither write outside the caller's ranges nor read
@@ -54,7 +55,7 @@ def _erasures(p, batch, how, seed):
     return pres
 
 
-@pytest.mark.parametrize("mode", ["pin", "stage"])
+@pytest.mark.parametrize("mode", [pytest.param("pin", marks=pytest.mark.pin_in_place), "stage"])
 @pytest.mark.parametrize("how", ["parity", "any"])
 @pytest.mark.parametrize("batch", [3, 5])
 @pytest.mark.parametrize("nw,kw,plen", _CASES)

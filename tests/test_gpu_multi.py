@@ -80,15 +80,17 @@ def test_host_batch_multi(gpu, oracle):
         assert out[b, :plen].tobytes() == pay[b].tobytes()
 
 
+@pytest.mark.parametrize("mode", [pytest.param("pin", marks=pytest.mark.pin_in_place), "stage"])
 @pytest.mark.parametrize("nctx", [2, 3])
-def test_host_batch_multi_pageable_unaligned_split(gpu, oracle, nctx):
+def test_host_batch_multi_pageable_unaligned_split(gpu, oracle, monkeypatch, nctx, mode):
     """the ranges of a host multi call are adjacent slices of one
     pageable caller buffer, and with a row stride that is no multiple of the
-    page size neighbouring ranges share a page.  The engine pins the whole
-    spans once before the worker threads start (engine.cpp
-    np_*_batch_host_multi, PinRegistry), so no worker registers or
-    unregisters a page under another's copies.  Guard bytes around every
-    buffer; every payload against the oracle."""
+    page size neighbouring ranges share a page.  Staged (the default), or with
+    NP_PAGEABLE=pin the engine pins the whole spans once before the worker
+    threads start (engine.cpp np_*_batch_host_multi, PinRegistry), so no
+    worker registers or unregisters a page under another's copies.  Guard
+    bytes around every buffer; every payload against the oracle."""
+    monkeypatch.setenv("NP_PAGEABLE", mode)
     ctxs = [npa.Context(0) for _ in range(nctx)]
     p = npa.CodeParams.derive_parameters(1024, 342)
     n, k = p.n(), p.k()

@@ -759,8 +759,9 @@ def _host_array(shape, fill, pinned, offset=0):
     return t.numpy()[offset:].reshape(shape)  # the view's base keeps the pinned tensor alive
 
 
-@pytest.mark.parametrize("pinned,mode", [(False, "pin"), (False, "gather"), (True, "pin")],
-                         ids=["pageable", "pageable-gather", "pinned"])
+@pytest.mark.parametrize("pinned,mode", [pytest.param(False, "pin", marks=pytest.mark.pin_in_place), (False, "stage"),
+                                        (True, "stage")],
+                         ids=["pageable-pin", "pageable", "pinned"])
 @pytest.mark.parametrize("nw,kw,plen,batch,offset", [(1024, 342, 512 * 256, 9, 0), (256, 86, 128 * 99 + 1, 7, 0),
                                                      (300, 100, 5000, 3, 2), (4096, 1366, 2048 * 40, 2, 0),
                                                      (1024, 342, 512 * 256, 3, 6)])
@@ -769,9 +770,9 @@ def test_host_batch_pipeline(gpu, oracle, nw, kw, plen, batch, offset, pinned, m
     sub-batches over several streams) give the oracle's shards and payloads;
     strided host layouts, unaligned starts, pinned host memory (present rows
     gathered over PCIe by a kernel) and garbage in the absent rows included.
-    Pageable buffers go pinned in place for the call (NP_PAGEABLE=pin, the
-    default) or through host-thread staging (NP_PAGEABLE=gather; engine.cpp
-    reads the variable per call)."""
+    Pageable buffers go through host-thread staging (the default) or, with
+    NP_PAGEABLE=pin, pinned in place for the call (engine.cpp reads the
+    variable per call; those cases run in a child process)."""
     monkeypatch.setenv("NP_PAGEABLE", mode)
     p = npa.CodeParams.derive_parameters(nw, kw)
     n, k = p.n(), p.k()

@@ -69,10 +69,10 @@ ok = torch.equal(h_out[:, :plen], h_pay)
 # reads (engine.cpp rows_needed: the k systematic rows when every payload of the
 # batch has them all, else all n rows), of those only the present ones on the
 # gather path, (+ flags) in, and 2k*sl/2 out.
-# Pageable shards and output (numpy).  Default (NP_PAGEABLE=pin): the engine
-# pins them in place for the call (PinRegistry) and goes as from pinned
-# memory; NP_PAGEABLE=stage: host threads copy the present rows into pinned
-# staging and the outputs back out of it (engine.cpp, host-memory pipeline).
+# Pageable shards and output (numpy).  Default: host threads copy the present
+# rows into pinned staging and the outputs back out of it (engine.cpp,
+# host-memory pipeline); NP_PAGEABLE=pin (opt-in): the engine pins them in
+# place for the call (PinRegistry) and goes as from pinned memory.
 pg_sh = h_sh.numpy().copy()
 pg_out = np.zeros((B, olen), dtype=np.uint8)
 pg_pay = h_pay.numpy().copy()
@@ -89,16 +89,16 @@ def enc_pageable():
 
 
 wb = p.wanted_n * sl  # the rows encode writes
+os.environ["NP_PAGEABLE"] = "pin"
 t_enc_pg = timed(enc_pageable)
 ok_pg = bool((pg_enc[:, :wb] == h_sh.numpy().reshape(B, -1)[:, :wb]).all())
 t_pg = timed(rec_pageable)
 ok_pg = ok_pg and bool((pg_out[:, :plen] == h_pay.numpy()).all())
 pg_out[:] = 0
 pg_enc[:] = 0
-os.environ["NP_PAGEABLE"] = "stage"
+del os.environ["NP_PAGEABLE"]  # the default: staged
 t_pg_st = timed(rec_pageable)
 t_enc_st = timed(enc_pageable)
-del os.environ["NP_PAGEABLE"]
 ok_pg = ok_pg and bool((pg_out[:, :plen] == h_pay.numpy()).all())
 ok_pg = ok_pg and bool((pg_enc[:, :wb] == h_sh.numpy().reshape(B, -1)[:, :wb]).all())
 ok = ok and ok_pg

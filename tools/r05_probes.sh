@@ -170,6 +170,10 @@ p12() {  # the register-resident locator: whole GPU suite and smoke, then p11's 
   suite p12 && BENCH_ONLY=1 p11
 }
 
+p13() {  # pinning in place opt-in (pin cases in a child process): whole suite, smoke, e2e
+  suite p13 && e2e p13
+}
+
 p1() {  # the host-pipeline fix: whole suite, smoke, bench, e2e
   suite p1 && bench p1 && e2e p1
 }
