@@ -174,6 +174,22 @@ p13() {  # pinning in place opt-in (pin cases in a child process): whole suite, 
   suite p13 && e2e p13
 }
 
+hugeab() {  # huge tests, then VCS benches prod vs base (tools/exp/lib_base.so), two passes
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_huge.py tests/test_gpu_noncodeword.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r05/pytest_huge_$1.log 2>&1; rc=$?
+  echo "huge tests: $(tail -1 gpurun_out/r05/pytest_huge_$1.log)"
+  [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r05/pytest_huge_$1.log | head -20; exit $rc; }
+  for pass in 1 2; do
+  for vc in ${VCS:-65536 50000 40000}; do
+    for lib in prod base; do
+      path=$PWD/reed-solomon-novelpoly_amd/lib/libnovelpoly_hip.so
+      [ $lib != prod ] && path=$PWD/tools/exp/lib_$lib.so
+      NP_LIB_PATH=$path timeout -k 10 300 python bench.py --no-cpu --steps 3 --warmup 1 --batch 512 --n-wanted $vc --erase $(( (vc - 1) / 3 + 1 )) > gpurun_out/r05/$1_${vc}_${lib}_$pass.log 2>&1 || exit $?
+      tail -1 gpurun_out/r05/$1_${vc}_${lib}_$pass.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('vc$vc $lib p$pass', d['value'], {k:v['ms'] for k,v in d['kernels'].items()}, d.get('roundtrip_ok'))"
+    done
+  done
+  done
+}
+
 p1() {  # the host-pipeline fix: whole suite, smoke, bench, e2e
   suite p1 && bench p1 && e2e p1
 }
