@@ -190,6 +190,11 @@ hugeab() {  # huge tests, then VCS benches prod vs base (tools/exp/lib_base.so),
   done
 }
 
+stamps() {  # HEAD wave-stamp table of the config-3 decode (NP_EXP=192 build; tools/wave_stamps.py)
+  NP_LIB_PATH=$PWD/tools/exp/lib_192.so timeout -k 10 300 python tools/wave_stamps.py > gpurun_out/r05/decode_wave_stamps.txt 2>&1 || exit $?
+  cat gpurun_out/r05/decode_wave_stamps.txt
+}
+
 p1() {  # the host-pipeline fix: whole suite, smoke, bench, e2e
   suite p1 && bench p1 && e2e p1
 }
