@@ -1,14 +1,14 @@
 #!/bin/bash
-# Round-4 closing run on the GPU box: the GPU test suite, the records
+# Round-5 closing run on the GPU box: the GPU test suite, the records
 # (tools/records.sh: BASELINE lines with CPU baselines, config-1 CPU record,
 # shapes), the config-3 kernel trace and PMC passes (tools/profile_round.sh),
 # and the PCIe-inclusive rates (tools/e2e_bench.py).  Usage:
-#   bash tools/r04_final.sh [RECORDS_TAG [PROFILE_TAG [PART]]]   (defaults r04f, r04,
+#   bash tools/r05_final.sh [RECORDS_TAG [PROFILE_TAG [PART]]]   (defaults r05f, r05,
 #   all; PART a = tests and records, b = profiles and PCIe rates)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-RT=${1:-r04f}
-PT=${2:-r04}
+RT=${1:-r05f}
+PT=${2:-r05}
 PART=${3:-ab}
 D=gpurun_out/$RT
 mkdir -p $D
@@ -21,6 +21,7 @@ fi
 [[ $PART == *b* ]] || { echo final part a done; exit 0; }
 bash tools/profile_round.sh $PT 3 > gpurun_out/prof_$PT.log 2>&1 || { tail -20 gpurun_out/prof_$PT.log; exit 1; }
 bash tools/profile_round.sh ${PT}_cfg4 4 > gpurun_out/prof_${PT}_cfg4.log 2>&1 || { tail -20 gpurun_out/prof_${PT}_cfg4.log; exit 1; }
+bash tools/profile_round.sh ${PT}_cfg2 2 > gpurun_out/prof_${PT}_cfg2.log 2>&1 || { tail -20 gpurun_out/prof_${PT}_cfg2.log; exit 1; }
 for c in 3 4; do
   timeout -k 10 300 python tools/e2e_bench.py --config $c --batch $([ $c = 3 ] && echo 256 || echo 64) > $D/e2e_cfg$c.json 2> $D/e2e_cfg$c.err || { tail -5 $D/e2e_cfg$c.err; exit 1; }
   cat $D/e2e_cfg$c.json

@@ -23,7 +23,7 @@ run() { tag=$1; shift
 import json; d=json.load(open('$D/$tag.json'))
 c=d['config']; print('$tag', 'n', c['n'], 'k', c['k'], 'GiB/s', d['value'], {k:(v['ms'], v['frac']) for k,v in d['kernels'].items()}, 'ok', d['roundtrip_ok'])"
 }
-for vc in ${VCS:-2 3 6 10 20 40 100 300 700 1200 1600 2000 2500 3000 5000 7000 10000}; do
+for vc in ${VCS:-2 3 6 10 20 40 100 300 700 1200 1600 2000 2500 3000 5000 7000 10000 16384 20000 30000 40000 50000 65536}; do
   b=1024; [ $vc -gt 2048 ] && b=512
   run shapes_vc$vc --n-wanted $vc --batch $b --erase $(( (vc - 1) / 3 + 1 )) || exit 1
 done
