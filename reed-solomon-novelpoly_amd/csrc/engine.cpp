@@ -203,7 +203,17 @@ np::EncodeArgs enc_args(const np_code_params* p, const uint8_t* payloads, size_t
   return a;
 }
 
-constexpr size_t kBigScratchCap = size_t(2) << 30;  // bytes of big-kernel scratch per context (k = 2048 decode: 256 slots of 4.9 MiB)
+// Bytes of big-kernel scratch per context (k = 2048 decode: 256 slots of
+// 4.9 MiB; the sub-transform path: 512 paired 1 MiB payloads at 65,536
+// validators in one slice, 2.5 GiB of slots).
+constexpr size_t kBigScratchCap = size_t(4) << 30;
+
+// Payloads per slice of the sub-transform path when one payload costs
+// `two / 2` bytes of slots plus `side`: even, so that pairs stay whole.
+size_t huge_slice(size_t two, size_t side) {
+  const size_t per = kBigScratchCap / std::max<size_t>(1, (two + 1) / 2 + side);
+  return per >= 2 ? per & ~size_t(1) : 1;
+}
 
 // Big-kernel scratch of `want` bytes (capped), ordered after every earlier
 // big launch of this context on any stream.  Caller holds the context lock.
@@ -265,7 +275,7 @@ hipError_t launch_encode(np_ctx* c, const np::EncodeArgs& a, hipStream_t s) {
   const size_t huge_per = np::huge_encode_scratch_per_payload(a.shard_len, a.n, a.k);
   if (np::huge_encode_supported(a.n, a.k) && huge_on(a.k) && huge_per <= kBigScratchCap) {
     // slices of the batch whose tile slots fit the context scratch
-    const size_t per = std::max<size_t>(1, kBigScratchCap / std::max<size_t>(1, huge_per));
+    const size_t per = huge_slice(np::huge_encode_scratch(2, a.payload_len, a.n, a.k), 0);
     for (size_t b0 = 0; b0 < a.batch; b0 += per) {
       np::EncodeArgs sub = a;
       sub.batch = std::min(per, a.batch - b0);
@@ -273,7 +283,7 @@ hipError_t launch_encode(np_ctx* c, const np::EncodeArgs& a, hipStream_t s) {
       sub.shards = a.shards + b0 * a.batch_stride;
       uint8_t* scr = nullptr;
       size_t bytes = 0;
-      hipError_t e = big_scratch(c, sub.batch * huge_per, s, &scr, &bytes);
+      hipError_t e = big_scratch(c, np::huge_encode_scratch(sub.batch, sub.payload_len, sub.n, sub.k), s, &scr, &bytes);
       if (e == hipSuccess) e = HIP(np::launch_encode_huge(c->T, sub, scr, s));
       e = big_done(c, s, e);
       if (e != hipSuccess) return e;
@@ -334,18 +344,18 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
     }
     return hipSuccess;
   }
-  const size_t huge_per = np::huge_reconstruct_scratch_per_payload(a.shard_len, a.n, a.k);
   if (path == RecPath::Huge) {
     // per payload: tile slots, mode byte and occupancy word, locators (unless
     // the caller's), status
     const size_t side = 32 + (a.locators ? 0 : 2 * static_cast<size_t>(a.n)) + own_status;
-    const size_t per = std::max<size_t>(1, kBigScratchCap / (huge_per + side));
+    const size_t per = huge_slice(np::huge_reconstruct_scratch(2, a.shard_len, a.n, a.k), side);
     for (size_t b0 = 0; b0 < a.batch; b0 += per) {
       np::ReconstructArgs sub = slice(a, b0, std::min(per, a.batch - b0));
       uint8_t* scr = nullptr;
       size_t bytes = 0;
-      hipError_t e = big_scratch(c, sub.batch * (huge_per + side), s, &scr, &bytes);
-      uint8_t* side0 = scr + sub.batch * huge_per;  // huge_per is a multiple of 128 KiB
+      const size_t slots = np::huge_reconstruct_scratch(sub.batch, sub.shard_len, sub.n, sub.k);
+      hipError_t e = big_scratch(c, slots + sub.batch * side, s, &scr, &bytes);
+      uint8_t* side0 = scr + slots;  // a multiple of 128 KiB
       uint16_t* loc = reinterpret_cast<uint16_t*>(side0);
       uint8_t* mode = side0 + (a.locators ? 0 : 2 * static_cast<size_t>(a.n) * sub.batch);
       if (!a.status) sub.status = reinterpret_cast<uint32_t*>(mode + np::huge_side_bytes(sub.batch));

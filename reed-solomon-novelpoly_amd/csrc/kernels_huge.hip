@@ -659,6 +659,18 @@ size_t huge_encode_scratch_per_payload(size_t shard_len, uint32_t n, uint32_t k)
   const size_t tiles = (shard_len / 2 + kRC - 1) / kRC;
   return tiles * (n / kSK) * static_cast<size_t>(kSlotBytes);
 }
+// Tile slots of a slice of `batch` payloads of `cols` columns each, as the
+// launchers lay them out: two payloads per tile when they pair them.
+size_t huge_slice_units(size_t batch, size_t cols) {
+  const bool pair = huge_pair_enabled() && cols <= kRC / 2 && batch > 1;
+  return pair ? (batch + 1) / 2 : batch * ((cols + kRC - 1) / kRC);
+}
+size_t huge_encode_scratch(size_t batch, size_t payload_len, uint32_t n, uint32_t k) {
+  return huge_slice_units(batch, (payload_len + 2 * k - 1) / (2 * k)) * (n / kSK) * static_cast<size_t>(kSlotBytes);
+}
+size_t huge_reconstruct_scratch(size_t batch, size_t shard_len, uint32_t n, uint32_t k) {
+  return huge_slice_units(batch, shard_len / 2) * ((n + k) / kSK) * static_cast<size_t>(kSlotBytes);
+}
 size_t huge_reconstruct_scratch_per_payload(size_t shard_len, uint32_t n, uint32_t k) {
   const size_t tiles = (shard_len / 2 + kRC - 1) / kRC;
   return tiles * ((n + k) / kSK) * static_cast<size_t>(kSlotBytes);

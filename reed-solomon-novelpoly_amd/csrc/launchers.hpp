@@ -142,6 +142,10 @@ bool huge_encode_supported(uint32_t n, uint32_t k);       // n >= 2k, n <= 65536
 bool huge_reconstruct_supported(uint32_t n, uint32_t k);  // n / k in {2, 4, 8}
 size_t huge_encode_scratch_per_payload(size_t shard_len, uint32_t n, uint32_t k);
 size_t huge_reconstruct_scratch_per_payload(size_t shard_len, uint32_t n, uint32_t k);
+// Slots of a slice of `batch` payloads, two payloads per tile where the launch
+// pairs them (32 columns or fewer): multiples of 128 KiB.
+size_t huge_encode_scratch(size_t batch, size_t payload_len, uint32_t n, uint32_t k);
+size_t huge_reconstruct_scratch(size_t batch, size_t shard_len, uint32_t n, uint32_t k);
 hipError_t launch_encode_huge(const DevTables& T, const EncodeArgs& a, uint8_t* scratch, hipStream_t s);
 // side: huge_side_bytes(batch) (per-payload mode bytes, then the 1024-row
 // block occupancy words); locators: batch x n u16 (unused when a.locators is set)

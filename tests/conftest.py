@@ -72,3 +72,21 @@ def gpu():
     torch.cuda.init()
     ctx = npa.default_context(0)
     return ctx
+
+
+@pytest.fixture(autouse=True)
+def _own_stream(request):
+    """GPU tests run on a non-default torch stream, and the tests hand that
+    stream to the library: torch's fills and copies and our kernels are then
+    ordered on one queue.  (A NULL stream means the context's own
+    non-blocking stream, which does not wait for work on torch's default,
+    legacy null stream.)"""
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    import torch
+
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        yield
+    torch.cuda.synchronize()

@@ -13,18 +13,6 @@ from novelpoly_amd import synth
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True)
-def _own_stream():
-    """Run every test on a non-default torch stream and hand that stream to
-    the library, so torch copies and our kernels are ordered on one queue."""
-    import torch
-
-    s = torch.cuda.Stream()
-    with torch.cuda.stream(s):
-        yield
-    torch.cuda.synchronize()
-
-
 def dev(a):
     import torch
 

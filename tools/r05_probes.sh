@@ -175,7 +175,7 @@ p13() {  # pinning in place opt-in (pin cases in a child process): whole suite, 
 }
 
 hugeab() {  # huge tests, then VCS benches prod vs base (tools/exp/lib_base.so), two passes
-  timeout -k 10 600 python -u -m pytest tests/test_gpu_huge.py tests/test_gpu_noncodeword.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r05/pytest_huge_$1.log 2>&1; rc=$?
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_huge.py tests/test_gpu_noncodeword.py ${TESTS_EXTRA} -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r05/pytest_huge_$1.log 2>&1; rc=$?
   echo "huge tests: $(tail -1 gpurun_out/r05/pytest_huge_$1.log)"
   [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r05/pytest_huge_$1.log | head -20; exit $rc; }
   for pass in 1 2; do
