@@ -204,9 +204,11 @@ np::EncodeArgs enc_args(const np_code_params* p, const uint8_t* payloads, size_t
 }
 
 // Bytes of big-kernel scratch per context (k = 2048 decode: 256 slots of
-// 4.9 MiB; the sub-transform path: 512 paired 1 MiB payloads at 65,536
-// validators in one slice, 2.5 GiB of slots).
-constexpr size_t kBigScratchCap = size_t(4) << 30;
+// 4.9 MiB; the sub-transform path: 512 x 1 MiB payloads in one slice at
+// every validator count, 4.5 GiB of slots at 40,000 validators).  8 GiB
+// against 4 measured 4-5 % faster at 20,000 and 40,000 validators
+// (profiles/r05/huge/slices_ab.txt), 2.8 % of the 288 GB.
+constexpr size_t kBigScratchCap = size_t(8) << 30;
 
 // Payloads per slice of the sub-transform path when one payload costs
 // `two / 2` bytes of slots plus `side`: even, so that pairs stay whole.

@@ -18,9 +18,9 @@ pytestmark = pytest.mark.gpu
 
 
 # (n_wanted, k_wanted, batch, present rate): the batch exceeds one slice of the
-# 4 GiB scratch (fast: ~25k payloads of n = 1024; k = 512: ~86k of n = 2048;
-# k = 1024: ~43k of n = 4096)
-CASES = [(1024, 342, 52000, 0.27), (2000, 667, 90000, 0.272), (4096, 1366, 45000, 0.262)]
+# 8 GiB scratch (fast: ~51k payloads of n = 1024; k = 512: ~172k of n = 2048;
+# k = 1024: ~86k of n = 4096)
+CASES = [(1024, 342, 104000, 0.27), (2000, 667, 180000, 0.272), (4096, 1366, 90000, 0.262)]
 
 
 @pytest.mark.parametrize("nw,kw,batch,rate", CASES)
@@ -67,10 +67,10 @@ def test_reconstruct_record_slices(gpu, oracle, nw, kw, batch, rate):
 
 
 # 65,536 validators, 1 MiB payloads (32 columns: two per tile): the encode's
-# slots take 4 MiB per payload (2 slices of the 4 GiB scratch for 1,801
-# payloads), the decode's 5 MiB + 128 KiB (3 slices); slices hold whole pairs,
+# slots take 4 MiB per payload (2 slices of the 8 GiB scratch for 2,501
+# payloads), the decode's 5 MiB + 128 KiB (2 slices); slices hold whole pairs,
 # and the odd last payload has a tile of its own.
-@pytest.mark.parametrize("batch", [1801])
+@pytest.mark.parametrize("batch", [2501])
 def test_huge_paired_slices_round_trip(gpu, batch):
     import torch
 
