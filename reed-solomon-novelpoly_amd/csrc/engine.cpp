@@ -75,7 +75,7 @@ struct DevBuf {
     p = nullptr;
     cap = 0;
     // exactly the size asked for (the context scratch is capped by its callers:
-    // engine.cpp big_scratch, kBigScratchCap)
+    // engine.cpp big_scratch, np_ctx::big_cap)
     hipError_t e = hipMalloc(&p, bytes);
     if (e == hipSuccess)
       cap = bytes;
@@ -137,6 +137,7 @@ struct np_ctx {
   // Per-workgroup scratch of the k = 1024 kernels (kernels_big.hip).  Launches
   // on different streams are ordered through big_done so they never share it.
   DevBuf d_big;
+  size_t big_cap = size_t(2) << 30;  // scratch_cap_for: set at creation
   hipEvent_t big_done = nullptr;
   bool big_used = false;
   // Host-memory batch pipeline (np_*_batch_host): per slot a stream and
@@ -203,24 +204,35 @@ np::EncodeArgs enc_args(const np_code_params* p, const uint8_t* payloads, size_t
   return a;
 }
 
-// Bytes of big-kernel scratch per context (k = 2048 decode: 256 slots of
-// 4.9 MiB; the sub-transform path: 512 x 1 MiB payloads in one slice at
-// every validator count, 4.5 GiB of slots at 40,000 validators).  8 GiB
-// against 4 measured 4-5 % faster at 20,000 and 40,000 validators
-// (profiles/r05/huge/slices_ab.txt), 2.8 % of the 288 GB.
-constexpr size_t kBigScratchCap = size_t(8) << 30;
+// Bytes of big-kernel scratch per context (k = 2048 decode at n = 16384:
+// 256 slots of 9.1 MiB; the sub-transform path: 512 x 1 MiB payloads in one
+// slice at every validator count, 4.5 GiB of slots at 40,000 validators).
+// 8 GiB against 4 measured 4-5 % faster at 20,000 and 40,000 validators
+// (profiles/r05/huge/slices_ab.txt), 2.8 % of the 288 GB; an eighth of the
+// memory free when the context is created, if that is less, but never below
+// kBigScratchMin, the size the path choice (rec_path) assumes.
+constexpr size_t kBigScratchMax = size_t(8) << 30;
+constexpr size_t kBigScratchMin = size_t(2) << 30;
+size_t scratch_cap_for(int device) {
+  size_t free_b = 0, total_b = 0;
+  if (hipSetDevice(device) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+    (void)hipGetLastError();
+    return kBigScratchMin;
+  }
+  return std::min(kBigScratchMax, std::max(kBigScratchMin, free_b / 8));
+}
 
 // Payloads per slice of the sub-transform path when one payload costs
 // `two / 2` bytes of slots plus `side`: even, so that pairs stay whole.
-size_t huge_slice(size_t two, size_t side) {
-  const size_t per = kBigScratchCap / std::max<size_t>(1, (two + 1) / 2 + side);
+size_t huge_slice(const np_ctx* c, size_t two, size_t side) {
+  const size_t per = c->big_cap / std::max<size_t>(1, (two + 1) / 2 + side);
   return per >= 2 ? per & ~size_t(1) : 1;
 }
 
 // Big-kernel scratch of `want` bytes (capped), ordered after every earlier
 // big launch of this context on any stream.  Caller holds the context lock.
 hipError_t big_scratch(np_ctx* c, size_t want, hipStream_t s, uint8_t** out, size_t* bytes) {
-  want = std::min(want, kBigScratchCap);
+  want = std::min(want, c->big_cap);
   hipError_t e = hipSuccess;
   if (!c->big_done) e = HIP(hipEventCreateWithFlags(&c->big_done, hipEventDisableTiming));
   if (e == hipSuccess && c->big_used) {
@@ -264,7 +276,7 @@ RecPath rec_path(uint32_t n, uint32_t k, size_t shard_len) {
   if (np::fast_reconstruct_supported(n, k) || (np::res_reconstruct_supported(n, k) && np::res_enabled()))
     return RecPath::FastRes;
   if (np::huge_reconstruct_supported(n, k) && huge_on(k) &&
-      np::huge_reconstruct_scratch_per_payload(shard_len, n, k) <= kBigScratchCap / 2)
+      np::huge_reconstruct_scratch_per_payload(shard_len, n, k) <= kBigScratchMin / 2)
     return RecPath::Huge;
   if (np::big_reconstruct_supported(n, k)) return RecPath::Big;
   return RecPath::Generic;
@@ -275,9 +287,9 @@ hipError_t launch_encode(np_ctx* c, const np::EncodeArgs& a, hipStream_t s) {
   if (np::fast_encode_supported(a.n, a.k)) return HIP(np::launch_encode_fast(c->T, a, s));
   if (np::res_encode_supported(a.n, a.k) && np::res_enabled()) return HIP(np::launch_encode_res(c->T, a, s));
   const size_t huge_per = np::huge_encode_scratch_per_payload(a.shard_len, a.n, a.k);
-  if (np::huge_encode_supported(a.n, a.k) && huge_on(a.k) && huge_per <= kBigScratchCap) {
+  if (np::huge_encode_supported(a.n, a.k) && huge_on(a.k) && huge_per <= c->big_cap) {
     // slices of the batch whose tile slots fit the context scratch
-    const size_t per = huge_slice(np::huge_encode_scratch(2, a.payload_len, a.n, a.k), 0);
+    const size_t per = huge_slice(c, np::huge_encode_scratch(2, a.payload_len, a.n, a.k), 0);
     for (size_t b0 = 0; b0 < a.batch; b0 += per) {
       np::EncodeArgs sub = a;
       sub.batch = std::min(per, a.batch - b0);
@@ -331,7 +343,7 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
     // per-payload decode rows + row multipliers and their tables (from the
     // caller's locators when given) and the status, then the decode
     const size_t stride = np::prefix_stride(a.n, a.k);
-    const size_t per = std::max<size_t>(1, kBigScratchCap / (stride + own_status));
+    const size_t per = std::max<size_t>(1, c->big_cap / (stride + own_status));
     for (size_t b0 = 0; b0 < a.batch; b0 += per) {
       np::ReconstructArgs sub = slice(a, b0, std::min(per, a.batch - b0));
       uint8_t* scr = nullptr;
@@ -350,7 +362,7 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
     // per payload: tile slots, mode byte and occupancy word, locators (unless
     // the caller's), status
     const size_t side = 32 + (a.locators ? 0 : 2 * static_cast<size_t>(a.n)) + own_status;
-    const size_t per = huge_slice(np::huge_reconstruct_scratch(2, a.shard_len, a.n, a.k), side);
+    const size_t per = huge_slice(c, np::huge_reconstruct_scratch(2, a.shard_len, a.n, a.k), side);
     for (size_t b0 = 0; b0 < a.batch; b0 += per) {
       np::ReconstructArgs sub = slice(a, b0, std::min(per, a.batch - b0));
       uint8_t* scr = nullptr;
@@ -373,7 +385,7 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
     const size_t tiles = (a.shard_len / 2 + 255) / 256;
     const size_t per_tile = np::big_reconstruct_scratch_per_tile(a.n, a.k);
     const size_t rstride = np::big_record_stride(a.n) + own_status;
-    const size_t per = std::max<size_t>(1, kBigScratchCap / 4 / rstride);
+    const size_t per = std::max<size_t>(1, c->big_cap / 4 / rstride);
     for (size_t b0 = 0; b0 < a.batch; b0 += per) {
       np::ReconstructArgs sub = slice(a, b0, std::min(per, a.batch - b0));
       const size_t rec_bytes = (sub.batch * rstride + 255) / 256 * 256;
@@ -393,7 +405,7 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
   // generic path: the status, and the locators unless the caller gave them,
   // into the ordered context scratch
   const size_t loc_bytes = a.locators ? 0 : a.n * sizeof(uint16_t);
-  const size_t per = std::max<size_t>(1, kBigScratchCap / (loc_bytes + own_status + 1));
+  const size_t per = std::max<size_t>(1, c->big_cap / (loc_bytes + own_status + 1));
   for (size_t b0 = 0; b0 < a.batch; b0 += per) {
     np::ReconstructArgs b = slice(a, b0, std::min(per, a.batch - b0));
     uint8_t* scr = nullptr;
@@ -557,6 +569,7 @@ int np_ctx_create(int device, np_ctx** out) {
   np_ctx* c = new (std::nothrow) np_ctx();
   if (!c) return fail(NP_ERR_ALLOC);
   c->device = device;
+  c->big_cap = scratch_cap_for(device);
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   const np::HostTables& t = np::host_tables();
   if (e == hipSuccess) e = upload(c, t.log, &c->T.log);
