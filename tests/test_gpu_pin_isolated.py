@@ -15,6 +15,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 
 
+@pytest.mark.timeout(900)  # the child's own cases are limited to 120 s each
 def test_pin_in_place_cases_in_child_process():
     env = dict(os.environ, NP_PIN_CHILD="1")
     files = ["tests/test_gpu_host_guard.py", "tests/test_gpu_parity.py", "tests/test_gpu_multi.py"]
