@@ -183,7 +183,7 @@ __device__ __forceinline__ void huge_store_rows(const EncodeArgs& a, const HugeA
 }
 
 template <int GEN>
-__global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k_huge_enc_inv(
+__device__ __forceinline__ void huge_enc_inv_body(
     DevTables T, EncodeArgs a, HugeArgs h, uint32_t nchunks) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
@@ -253,7 +253,7 @@ __global__ __launch_bounds__(256) void k_huge_enc_top(DevTables T, HugeArgs h, u
 }
 
 template <int GEN>
-__global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k_huge_enc_fwd(
+__device__ __forceinline__ void huge_enc_fwd_body(
     DevTables T, EncodeArgs a, HugeArgs h, uint32_t nchunks) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
@@ -327,7 +327,7 @@ __global__ __launch_bounds__(256) void k_huge_records(ReconstructArgs a, uint8_t
 }
 
 template <int GEN>
-__global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k_huge_rec_inv(
+__device__ __forceinline__ void huge_rec_inv_body(
     DevTables T, ReconstructArgs a, HugeArgs h, uint32_t nsyms) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
@@ -487,7 +487,7 @@ __global__ __launch_bounds__(256) void k_huge_rec_top(DevTables T, HugeArgs h, s
 }
 
 template <int GEN>
-__global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k_huge_rec_fwd(
+__device__ __forceinline__ void huge_rec_fwd_body(
     DevTables T, ReconstructArgs a, HugeArgs h, uint32_t nsyms) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
@@ -593,21 +593,32 @@ __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k
                     r, ncols, out16, 2 * static_cast<size_t>(h.K));
 }
 
-// ------------------------------------------------------------ dispatch ----
-// f(Int<GEN>) for GEN = res_gen<1024>(I) of a sub-transform index I < 65536.
+// One launch per phase: workgroup b's sub-transform u picks its GEN
+// (res_gen<1024>(1024 u)) at run time; the bodies are the same code as one
+// launch per GEN range had run, without the launches' ramps and tails.
 template <typename F>
-hipError_t with_sub_gen(uint32_t I, F&& f) {
-  switch (res_gen<kSK>(I)) {
-    case 2: return f(Int<2>{});
-    case 3: return f(Int<3>{});
-    case 4: return f(Int<4>{});
-    case 5: return f(Int<5>{});
-    case 6: return f(Int<6>{});
-    case 7: return f(Int<7>{});
-    case 8: return f(Int<8>{});
-    default: return hipErrorInvalidValue;
+__device__ __forceinline__ void with_gen_dev(uint32_t u, F&& f) {
+  switch (res_gen<kSK>(kSK * u)) {
+    case 2: f(Int<2>{}); break;
+    case 3: f(Int<3>{}); break;
+    case 4: f(Int<4>{}); break;
+    case 5: f(Int<5>{}); break;
+    case 6: f(Int<6>{}); break;
+    case 7: f(Int<7>{}); break;
+    default: f(Int<8>{}); break;
   }
 }
+#define NP_HUGE_PHASE(NAME, ARGS, CALL)                                                                              \
+  __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k_##NAME ARGS {                     \
+    with_gen_dev(uniform(h.u0 + blockIdx.x / h.per), [&](auto g) { NAME##_body<decltype(g)::value> CALL; });       \
+  }
+NP_HUGE_PHASE(huge_enc_inv, (DevTables T, EncodeArgs a, HugeArgs h, uint32_t nchunks), (T, a, h, nchunks))
+NP_HUGE_PHASE(huge_enc_fwd, (DevTables T, EncodeArgs a, HugeArgs h, uint32_t nchunks), (T, a, h, nchunks))
+NP_HUGE_PHASE(huge_rec_inv, (DevTables T, ReconstructArgs a, HugeArgs h, uint32_t nsyms), (T, a, h, nsyms))
+NP_HUGE_PHASE(huge_rec_fwd, (DevTables T, ReconstructArgs a, HugeArgs h, uint32_t nsyms), (T, a, h, nsyms))
+#undef NP_HUGE_PHASE
+
+// ------------------------------------------------------------ dispatch ----
 template <typename F>
 hipError_t with_m(uint32_t M, F&& f) {
   switch (M) {
@@ -676,19 +687,6 @@ size_t huge_reconstruct_scratch_per_payload(size_t shard_len, uint32_t n, uint32
   return tiles * ((n + k) / kSK) * static_cast<size_t>(kSlotBytes);
 }
 
-// Sub-transforms u in [u0, u1) in launches of one res_gen each: res_gen(1024 u)
-// is 2 for u = 0 and g for u in [2^(g-3), 2^(g-2)).
-template <typename F>
-hipError_t for_gen_ranges(uint32_t u0, uint32_t u1, F&& f) {
-  hipError_t e = hipSuccess;
-  while (u0 < u1 && e == hipSuccess) {
-    const uint32_t end = u0 == 0 ? 1u : std::min(u1, 2u * (1u << (31 - __builtin_clz(u0))));
-    e = with_sub_gen(kSK * u0, [&](auto g) { return f(g, u0, std::min(end, u1)); });
-    u0 = std::min(end, u1);
-  }
-  return e;
-}
-
 hipError_t launch_encode_huge(const DevTables& T, const EncodeArgs& a, uint8_t* scratch, hipStream_t s) {
   if (!huge_encode_supported(a.n, a.k)) return hipErrorInvalidValue;
   const size_t nchunks = (a.payload_len + 2 * a.k - 1) / (2 * a.k);
@@ -704,11 +702,9 @@ hipError_t launch_encode_huge(const DevTables& T, const EncodeArgs& a, uint8_t* 
   h.per = static_cast<uint32_t>(per);
   h.pair = pair ? 1u : 0u;
   auto grid = [&](uint32_t u0, uint32_t u1) { return static_cast<uint32_t>(per * (u1 - u0)); };
-  hipError_t e = for_gen_ranges(0, h.M, [&](auto g, uint32_t u0, uint32_t u1) {
-    h.u0 = u0;
-    k_huge_enc_inv<decltype(g)::value><<<grid(u0, u1), kSK, kHugeLds, s>>>(T, a, h, nc);
-    return hipGetLastError();
-  });
+  h.u0 = 0;
+  k_huge_enc_inv<<<grid(0, h.M), kSK, kHugeLds, s>>>(T, a, h, nc);
+  hipError_t e = hipGetLastError();
   const size_t units = per * 16 * kSK;
   if (e == hipSuccess)
     e = with_m(h.M, [&](auto mc) {
@@ -717,12 +713,11 @@ hipError_t launch_encode_huge(const DevTables& T, const EncodeArgs& a, uint8_t* 
     });
   // parity sub-segments holding wanted rows: u in [M, ceil(wanted_n / 1024))
   const uint32_t u_end = std::min(a.n, a.wanted_n + kSK - 1) / kSK;
-  if (e == hipSuccess)
-    e = for_gen_ranges(h.M, u_end, [&](auto g, uint32_t u0, uint32_t u1) {
-      h.u0 = u0;
-      k_huge_enc_fwd<decltype(g)::value><<<grid(u0, u1), kSK, kHugeLds, s>>>(T, a, h, nc);
-      return hipGetLastError();
-    });
+  if (e == hipSuccess && u_end > h.M) {
+    h.u0 = h.M;
+    k_huge_enc_fwd<<<grid(h.M, u_end), kSK, kHugeLds, s>>>(T, a, h, nc);
+    e = hipGetLastError();
+  }
   return e;
 }
 
@@ -755,12 +750,11 @@ hipError_t launch_reconstruct_huge(const DevTables& T, const ReconstructArgs& a,
   h.pair = pair ? 1u : 0u;
   h.batch = static_cast<uint32_t>(a.batch);
   auto grid = [&](uint32_t u0, uint32_t u1) { return static_cast<uint32_t>(per * (u1 - u0)); };
-  if (e == hipSuccess)
-    e = for_gen_ranges(0, a.n / kSK, [&](auto g, uint32_t u0, uint32_t u1) {
-      h.u0 = u0;
-      k_huge_rec_inv<decltype(g)::value><<<grid(u0, u1), kSK, kHugeLds, s>>>(T, a, h, ns);
-      return hipGetLastError();
-    });
+  if (e == hipSuccess) {
+    h.u0 = 0;
+    k_huge_rec_inv<<<grid(0, a.n / kSK), kSK, kHugeLds, s>>>(T, a, h, ns);
+    e = hipGetLastError();
+  }
   const size_t units = per * 16 * kSK;
   if (e == hipSuccess)
     e = with_m(h.M, [&](auto mc) {
@@ -770,12 +764,11 @@ hipError_t launch_reconstruct_huge(const DevTables& T, const ReconstructArgs& a,
         return hipGetLastError();
       });
     });
-  if (e == hipSuccess)
-    e = for_gen_ranges(0, h.M, [&](auto g, uint32_t u0, uint32_t u1) {
-      h.u0 = u0;
-      k_huge_rec_fwd<decltype(g)::value><<<grid(u0, u1), kSK, kHugeLds, s>>>(T, a, h, ns);
-      return hipGetLastError();
-    });
+  if (e == hipSuccess) {
+    h.u0 = 0;
+    k_huge_rec_fwd<<<grid(0, h.M), kSK, kHugeLds, s>>>(T, a, h, ns);
+    e = hipGetLastError();
+  }
   return e;
 }
 
@@ -785,15 +778,10 @@ hipError_t configure_huge_kernels() {
     const hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kHugeLds));
     if (r != hipSuccess && e == hipSuccess) e = r;
   };
-  for (uint32_t g = 2; g <= 8; ++g)
-    (void)with_sub_gen((256u << g) - 1024u, [&](auto gc) {
-      constexpr int G = decltype(gc)::value;
-      set(reinterpret_cast<const void*>(&k_huge_enc_inv<G>));
-      set(reinterpret_cast<const void*>(&k_huge_enc_fwd<G>));
-      set(reinterpret_cast<const void*>(&k_huge_rec_inv<G>));
-      set(reinterpret_cast<const void*>(&k_huge_rec_fwd<G>));
-      return hipSuccess;
-    });
+  set(reinterpret_cast<const void*>(&k_huge_enc_inv));
+  set(reinterpret_cast<const void*>(&k_huge_enc_fwd));
+  set(reinterpret_cast<const void*>(&k_huge_rec_inv));
+  set(reinterpret_cast<const void*>(&k_huge_rec_fwd));
   return e;
 }
 
