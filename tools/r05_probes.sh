@@ -75,17 +75,11 @@ for r in sorted(rows, key=lambda r: -float(r['TotalDurationNs']))[:14]:
   done
 }
 
-slices() {  # sub-transform path: batch slice size (NP_HUGE_SLICE_MB) against the Infinity Cache
-  for vc in ${VCS:-65536 40000 20000}; do
-    for mb in ${MBS:-2048 512 256 128 64}; do
-      NP_HUGE_SLICE_MB=$mb timeout -k 10 300 python bench.py --no-cpu --steps 3 --warmup 1 --batch 512 --n-wanted $vc --erase $(( (vc - 1) / 3 + 1 )) > gpurun_out/r05/slice_${vc}_$mb.log 2>&1 || exit $?
-      tail -1 gpurun_out/r05/slice_${vc}_$mb.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('vc$vc slice ${mb}MB', d['value'], {k:v['ms'] for k,v in d['kernels'].items()})"
-    done
-  done
-}
+# slices(): the NP_HUGE_SLICE_MB sweep of probe p4 (profiles/r05/huge/slice_sweep.txt);
+# the knob was removed after it, so the function is gone too.
 
-p4() {  # sub-transform path: kernel profile, then the slice sweep
-  hugeprof && MBS="2048 256 128" slices
+p4() {  # sub-transform path: kernel profile (the slice sweep ran here too, with a knob since removed)
+  hugeprof
 }
 
 p6() {  # paired sub-transform decode: huge tests, then 65,536 / 50,000 validators with and without pairing
