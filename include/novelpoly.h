@@ -13,9 +13,12 @@
  *  - plain pointers and sizes only; every buffer is caller-owned;
  *  - host entry points take host memory; `_dev` entry points take device
  *    pointers (hipMalloc'd on the context's device) and a hipStream_t passed
- *    as `void*` (NULL = the context's own stream) and are asynchronous;
- *  - a context is bound to one GPU; calls on one context are serialised on
- *    its stream; distinct contexts may be used from distinct threads;
+ *    as `void*` and are asynchronous on that stream; NULL is HIP's legacy
+ *    null stream (the caller's default stream, e.g. torch's), so work queued
+ *    there before the call is ordered before it;
+ *  - a context is bound to one GPU; host-API calls on one context are
+ *    serialised on its own stream; distinct contexts may be used from
+ *    distinct threads;
  *  - status 0 is success, 1..8 mirror `Error` in src/errors.rs:4-28 in
  *    declaration order, >= 100 are engine failures.
  */
@@ -87,10 +90,25 @@ typedef struct np_ctx np_ctx;
  * tables (inc_gen_field_tables.rs:29-72) and skew factors (inc_afft.rs:386-445). */
 int np_ctx_create(int device, np_ctx** out);
 void np_ctx_destroy(np_ctx* ctx);
+/* Checked builds only (lib/libnovelpoly_hip_chk.so, -DNP_BOUNDS_CHECK=1;
+ * DESIGN.md §6): waits for the device, then returns in out[0] the number of
+ * global accesses since the last call that fell outside the buffers the
+ * kernels' arguments imply (error locator, prefix locator / locator records,
+ * resident reconstruct), and in out[1..7] the first one (buffer kind, kernel
+ * source line, workgroup, thread, byte offset lo/hi, width); clears them.
+ * NP_ERR_INVALID_ARGUMENT in the product build. */
+int np_debug_bounds_check(np_ctx* ctx, uint32_t out[8]);
+
+/* The in-place pin registry of the host batch calls (NP_PAGEABLE=pin):
+ * out[0] = page ranges registered now (0 between calls), out[1] =
+ * hipHostUnregister calls the runtime refused since the process started. */
+void np_pin_registry_stats(size_t out[2]);
+
 /* The context's stream (hipStream_t as void*). */
 void* np_ctx_stream(np_ctx* ctx);
 int np_ctx_device(np_ctx* ctx);
-/* Waits for all work queued on the context's stream. */
+/* Waits for all work queued on the context's stream and on the device's
+ * legacy null stream (the `_dev` calls given a NULL stream). */
 int np_ctx_synchronize(np_ctx* ctx);
 
 /* ---- host-memory API (the crate's surface) -------------------------------- */

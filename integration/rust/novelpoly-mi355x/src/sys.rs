@@ -59,6 +59,8 @@ extern "C" {
 	pub fn np_ctx_stream(ctx: *mut np_ctx) -> *mut c_void;
 	pub fn np_ctx_device(ctx: *mut np_ctx) -> c_int;
 	pub fn np_ctx_synchronize(ctx: *mut np_ctx) -> c_int;
+	pub fn np_debug_bounds_check(ctx: *mut np_ctx, out: *mut u32) -> c_int;
+	pub fn np_pin_registry_stats(out: *mut usize);
 
 	pub fn np_encode(
 		ctx: *mut np_ctx,

@@ -6,6 +6,7 @@
 #include <cstdint>
 
 #include "dev_tables.hpp"
+#include "launchers.hpp"
 
 namespace np {
 
@@ -29,4 +30,143 @@ __device__ __forceinline__ uint16_t be_sym(const uint8_t* p, size_t off, size_t 
   return static_cast<uint16_t>((hi << 8) | lo);
 }
 
+// ------------------------------------------------------- checked builds ----
+// -DNP_BOUNDS_CHECK=1 (`make -C reed-solomon-novelpoly_amd chk` ->
+// lib/libnovelpoly_hip_chk.so; never the product library) checks the global
+// accesses of the kernels in the window of round 5's probe p11 (DESIGN.md §6:
+// k_error_locator, k_prefix_locator / k_locator_records, k_reconstruct_res)
+// against the extents their arguments imply.  Each such kernel arms this
+// translation unit's extent set at entry (bounds_arm: every workgroup writes
+// the same values, computed from its arguments; the checked tests run one
+// launch at a time), and every instrumented access goes through bchk: an
+// address outside its buffer is counted, the first one recorded (kind, line,
+// workgroup, thread, offset, bytes), and redirected to a sink, so that the
+// kernel finishes and the host reads the record (np_debug_bounds_check).
+// Kinds whose extent is empty (not armed, e.g. the shared helpers inside the
+// sub-transform kernels) pass unchecked.
+enum BoundsKind : uint32_t { kBkShards, kBkPresent, kBkLocators, kBkRecords, kBkOut, kBkStatus, kBkZeros, kBkCount };
+struct BoundsSet {
+  uint64_t lo[kBkCount], hi[kBkCount];
+};
+constexpr int kBoundsRecordWords = 8;  // count, kind, line, workgroup, thread, offset lo, offset hi, bytes
+
+}  // namespace np
+
+#ifndef NP_BOUNDS_CHECK
+#define NP_BOUNDS_CHECK 0
+#endif
+
+namespace np {
+namespace {
+
+#if NP_BOUNDS_CHECK
+__device__ BoundsSet g_bounds;
+__device__ uint32_t g_bounds_viol[kBoundsRecordWords];
+__device__ __attribute__((aligned(256))) uint8_t g_bounds_sink[4096];
+
+__device__ __forceinline__ void bounds_arm(const BoundsSet& b) {
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < kBkCount; ++i) {
+      g_bounds.lo[i] = b.lo[i];
+      g_bounds.hi[i] = b.hi[i];
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ bool bounds_in(uint64_t a, uint64_t bytes, uint32_t kind) {
+  const uint64_t lo = g_bounds.lo[kind], hi = g_bounds.hi[kind];
+  return hi == 0 || (a >= lo && a + bytes <= hi);
+}
+
+__device__ __noinline__ void bounds_record(uint64_t a, uint64_t bytes, uint32_t kind, uint32_t line) {
+  const uint32_t c = atomicAdd(&g_bounds_viol[0], 1u);
+  if (c == 0) {
+    const uint64_t off = a - g_bounds.lo[kind];
+    g_bounds_viol[1] = kind;
+    g_bounds_viol[2] = line;
+    g_bounds_viol[3] = blockIdx.x;
+    g_bounds_viol[4] = threadIdx.x;
+    g_bounds_viol[5] = static_cast<uint32_t>(off);
+    g_bounds_viol[6] = static_cast<uint32_t>(off >> 32);
+    g_bounds_viol[7] = static_cast<uint32_t>(bytes);
+  }
+}
+#endif
+
+// p if [p, p + bytes) lies in the armed buffer of `kind` (or `alt`, e.g. the
+// zero page that stands in for absent rows), else the sink (checked builds).
+template <class T>
+__device__ __forceinline__ T* bchk(T* p, uint64_t bytes, uint32_t kind, uint32_t line, uint32_t alt = kBkCount) {
+#if NP_BOUNDS_CHECK
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  if (bytes == 0 || bounds_in(a, bytes, kind) || (alt < kBkCount && bounds_in(a, bytes, alt))) return p;
+  bounds_record(a, bytes, kind, line);
+  return reinterpret_cast<T*>(g_bounds_sink);
+#else
+  (void)bytes, (void)kind, (void)line, (void)alt;
+  return p;
+#endif
+}
+// A table index below `size` (checked builds: counted as a records-kind
+// violation at offset idx and clamped to 0).
+__device__ __forceinline__ uint32_t ichk(uint32_t idx, uint32_t size, uint32_t line) {
+#if NP_BOUNDS_CHECK
+  if (idx < size) return idx;
+  bounds_record(g_bounds.lo[kBkRecords] + idx, size, kBkRecords, line);
+  return 0;
+#else
+  (void)size, (void)line;
+  return idx;
+#endif
+}
+#if NP_BOUNDS_CHECK
+#define NP_BCHK(p, bytes, kind) ::np::bchk((p), (bytes), (kind), __LINE__)
+#define NP_BCHK2(p, bytes, kind, alt) ::np::bchk((p), (bytes), (kind), __LINE__, (alt))
+#define NP_ICHK(i, size) ::np::ichk((i), (size), __LINE__)
+#else  // the product: the expressions themselves (code objects unchanged, tools/isa_same.sh)
+#define NP_BCHK(p, bytes, kind) (p)
+#define NP_BCHK2(p, bytes, kind, alt) (p)
+#define NP_ICHK(i, size) (i)
+#endif
+
+// The extents a ReconstructArgs implies (launchers.hpp), plus the zero page.
+__device__ __forceinline__ BoundsSet bounds_of(const ReconstructArgs& a, const DevTables& T, size_t rec_stride) {
+  BoundsSet b{};
+  auto set = [&](uint32_t k, const void* p, uint64_t bytes) {
+    if (!p || bytes == 0) return;
+    b.lo[k] = reinterpret_cast<uint64_t>(p);
+    b.hi[k] = b.lo[k] + bytes;
+  };
+  const uint64_t n = a.n, nb = a.batch;
+  if (nb) {
+    set(kBkShards, a.shards, (nb - 1) * a.batch_stride + n * a.shard_len);
+    set(kBkPresent, a.present, nb * n);
+    set(kBkLocators, a.locators, nb * n * 2);
+    set(kBkRecords, a.prefix, nb * rec_stride);
+    set(kBkOut, a.out, (nb - 1) * a.out_stride + (a.shard_len / 2) * 2 * static_cast<uint64_t>(a.k));
+#if NP_BOUNDS_CHECK
+    if (b.hi[kBkOut]) b.hi[kBkOut] -= a.chk_shrink_out;
+#endif
+    set(kBkStatus, a.status, nb * 8);
+  }
+  set(kBkZeros, T.zeros, kZeroPageBytes);
+  return b;
+}
+
+// Host side of a translation unit: its first violation record since the last
+// call (out[0] = count), then cleared.  hipErrorNotSupported in the product.
+inline hipError_t bounds_take_tu(uint32_t out[kBoundsRecordWords]) {
+#if NP_BOUNDS_CHECK
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bounds_viol), sizeof(uint32_t) * kBoundsRecordWords);
+  static const uint32_t zero[kBoundsRecordWords] = {};
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_bounds_viol), zero, sizeof zero);
+  return e;
+#else
+  for (int i = 0; i < kBoundsRecordWords; ++i) out[i] = 0;
+  return hipErrorNotSupported;
+#endif
+}
+
+}  // namespace
 }  // namespace np

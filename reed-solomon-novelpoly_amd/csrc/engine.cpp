@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <iterator>
 #include <map>
 #include <cstdio>
@@ -27,10 +28,16 @@ namespace {
 
 thread_local size_t g_detail[3] = {0, 0, 0};
 
+thread_local char g_site_msg[192] = "";
+
+// Every failure sets the detail and clears the call-site text; dev_err writes
+// the text after this for NP_ERR_DEVICE / NP_ERR_ALLOC (a
+// validation error, or a success, never reports an older failure's site).
 int fail(int st, size_t a = 0, size_t b = 0, size_t c = 0) {
   g_detail[0] = a;
   g_detail[1] = b;
   g_detail[2] = c;
+  g_site_msg[0] = '\0';
   return st;
 }
 
@@ -42,7 +49,6 @@ int fail(int st, size_t a = 0, size_t b = 0, size_t c = 0) {
 // (NP_SYNC_EACH=1 below makes the host pipeline synchronise after every step).
 thread_local int g_site_line = 0;
 thread_local const char* g_site_call = nullptr;
-thread_local char g_site_msg[192] = "";
 
 hipError_t at_site(hipError_t e, int line, const char* call) {
   if (e != hipSuccess && !g_site_line) {
@@ -159,13 +165,17 @@ int dev_err(hipError_t e) {
   const char* call = g_site_call;
   g_site_line = 0;
   g_site_call = nullptr;
-  if (e == hipSuccess) return NP_OK;
+  if (e == hipSuccess) {
+    g_site_msg[0] = '\0';
+    return NP_OK;
+  }
+  const int st = fail(e == hipErrorOutOfMemory ? NP_ERR_ALLOC : NP_ERR_DEVICE, static_cast<size_t>(e),
+                      static_cast<size_t>(line));
   if (line)
     std::snprintf(g_site_msg, sizeof g_site_msg, "engine.cpp:%d %s: %s", line, call, hipGetErrorName(e));
   else
     std::snprintf(g_site_msg, sizeof g_site_msg, "(call site not recorded): %s", hipGetErrorName(e));
-  return fail(e == hipErrorOutOfMemory ? NP_ERR_ALLOC : NP_ERR_DEVICE, static_cast<size_t>(e),
-              static_cast<size_t>(line));
+  return st;
 }
 
 template <class T>
@@ -208,18 +218,20 @@ np::EncodeArgs enc_args(const np_code_params* p, const uint8_t* payloads, size_t
 // 256 slots of 9.1 MiB; the sub-transform path: 512 x 1 MiB payloads in one
 // slice at every validator count, 4.5 GiB of slots at 40,000 validators).
 // 8 GiB against 4 measured 4-5 % faster at 20,000 and 40,000 validators
-// (profiles/r05/huge/slices_ab.txt), 2.8 % of the 288 GB; an eighth of the
-// memory free when the context is created, if that is less, but never below
-// kBigScratchMin, the size the path choice (rec_path) assumes.
+// (profiles/r05/huge/slices_ab.txt), 2.8 % of the 288 GB.  The cap follows the
+// device's total memory (a 32nd, 8 GiB on an MI355X), never the memory free at
+// context creation: which kernels run and how a batch is sliced are then the
+// same from run to run.  It is never below kBigScratchMin, the
+// size the path choices (rec_path, launch_encode) assume.
 constexpr size_t kBigScratchMax = size_t(8) << 30;
 constexpr size_t kBigScratchMin = size_t(2) << 30;
 size_t scratch_cap_for(int device) {
-  size_t free_b = 0, total_b = 0;
-  if (hipSetDevice(device) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+  size_t total_b = 0;
+  if (hipSetDevice(device) != hipSuccess || hipDeviceTotalMem(&total_b, device) != hipSuccess) {
     (void)hipGetLastError();
     return kBigScratchMin;
   }
-  return std::min(kBigScratchMax, std::max(kBigScratchMin, free_b / 8));
+  return std::min(kBigScratchMax, std::max(kBigScratchMin, total_b / 32));
 }
 
 // Payloads per slice of the sub-transform path when one payload costs
@@ -287,7 +299,7 @@ hipError_t launch_encode(np_ctx* c, const np::EncodeArgs& a, hipStream_t s) {
   if (np::fast_encode_supported(a.n, a.k)) return HIP(np::launch_encode_fast(c->T, a, s));
   if (np::res_encode_supported(a.n, a.k) && np::res_enabled()) return HIP(np::launch_encode_res(c->T, a, s));
   const size_t huge_per = np::huge_encode_scratch_per_payload(a.shard_len, a.n, a.k);
-  if (np::huge_encode_supported(a.n, a.k) && huge_on(a.k) && huge_per <= c->big_cap) {
+  if (np::huge_encode_supported(a.n, a.k) && huge_on(a.k) && huge_per <= kBigScratchMin) {
     // slices of the batch whose tile slots fit the context scratch
     const size_t per = huge_slice(c, np::huge_encode_scratch(2, a.payload_len, a.n, a.k), 0);
     for (size_t b0 = 0; b0 < a.batch; b0 += per) {
@@ -424,7 +436,13 @@ hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream
   return hipSuccess;
 }
 
-hipStream_t pick(np_ctx* c, void* s) { return s ? static_cast<hipStream_t>(s) : c->stream; }
+// The stream of a `_dev` call: the caller's, where NULL is HIP's legacy null
+// stream (the caller's default stream, e.g. torch's), as in every HIP / CUDA
+// library -- work the caller queued there before the call is ordered before
+// ours (verdict r05: NULL used to mean the context's non-blocking stream,
+// which ran unordered with the caller's default-stream fills and copies).
+// The host calls keep the context's own streams.
+hipStream_t pick(np_ctx*, void* s) { return static_cast<hipStream_t>(s); }
 
 // Host copy with streaming (non-temporal) stores where the destination allows
 // it: the pageable gather and copy-out move tens of MB per call that no CPU
@@ -505,6 +523,25 @@ const char* np_status_message(int st) {
     case NP_ERR_NO_DEVICE: return "no gfx950 device available";
     default: return "unknown status";
   }
+}
+
+int np_debug_bounds_check(np_ctx* c, uint32_t out[8]) {
+  if (!c || !out) return fail(NP_ERR_INVALID_ARGUMENT);
+  (void)hipSetDevice(c->device);
+  for (int i = 0; i < 8; ++i) out[i] = 0;
+  hipError_t e = HIP(hipDeviceSynchronize());
+  if (e != hipSuccess) return dev_err(e);
+  hipError_t (*const take[])(uint32_t*) = {np::bounds_take_generic, np::bounds_take_fast, np::bounds_take_res};
+  for (auto f : take) {
+    uint32_t r[8];
+    e = f(r);
+    if (e == hipErrorNotSupported) return fail(NP_ERR_INVALID_ARGUMENT);  // the product build: no checks
+    if (e != hipSuccess) return dev_err(HIP(e));
+    if (r[0] && !out[0])
+      for (int i = 1; i < 8; ++i) out[i] = r[i];
+    out[0] += r[0];
+  }
+  return NP_OK;
 }
 
 const char* np_version(void) { return "novelpoly-mi355x 0.3.0 (gfx950)"; }
@@ -636,7 +673,9 @@ int np_ctx_device(np_ctx* c) { return c ? c->device : -1; }
 int np_ctx_synchronize(np_ctx* c) {
   if (!c) return fail(NP_ERR_INVALID_ARGUMENT);
   (void)hipSetDevice(c->device);
-  return dev_err(HIP(hipStreamSynchronize(c->stream)));
+  hipError_t e = HIP(hipStreamSynchronize(c->stream));
+  if (e == hipSuccess) e = HIP(hipStreamSynchronize(nullptr));  // the `_dev` calls given a NULL stream
+  return dev_err(e);
 }
 
 // --------------------------------------------------------------- encode ----
@@ -720,6 +759,23 @@ constexpr size_t kPipeSlotBytes = size_t(64) << 20;
 // costs more than copying them.
 constexpr size_t kPinMinBytes = size_t(1) << 20;
 
+// Device address of [p, p + bytes) when the whole range lies in one pinned host
+// allocation mapped into the device address space (hipHostMalloc, torch's
+// pin_memory, hipHostRegister), else nullptr (pageable memory).
+const uint8_t* mapped_host_range(const uint8_t* p, size_t bytes) {
+  if (bytes == 0) return nullptr;
+  hipPointerAttribute_t a0{}, a1{};
+  if (hipPointerGetAttributes(&a0, p) != hipSuccess || hipPointerGetAttributes(&a1, p + bytes - 1) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (a0.type != hipMemoryTypeHost || a1.type != hipMemoryTypeHost || !a0.devicePointer || !a1.devicePointer)
+    return nullptr;
+  const uint8_t* d0 = static_cast<const uint8_t*>(a0.devicePointer);
+  if (static_cast<const uint8_t*>(a1.devicePointer) != d0 + (bytes - 1)) return nullptr;
+  return d0;
+}
+
 // The page ranges this library registered in place, process-wide.
 // hipHostRegister pins whole pages, so the range pinned for one span can share
 // its first and last page with a neighbouring span: the adjacent slice of the
@@ -730,44 +786,84 @@ constexpr size_t kPinMinBytes = size_t(1) << 20;
 // -- after the streams of every call that used it have drained.
 class PinRegistry {
  public:
-  // Registered base of a range holding [p, p + bytes), or 0 (stage instead).
-  uintptr_t acquire(const void* p, size_t bytes) {
+  // The device address of [p, p + bytes) for the length of a call, or nullptr
+  // (stage it).  In this order, under the registry lock: a span inside a range
+  // registered here takes a reference (*base = that range); else memory the
+  // caller pinned itself (mapped_host_range; no reference, the caller owns
+  // it); else, with `may_pin` and at least kPinMinBytes, the span's pages are
+  // registered here (*base = the new range).  One lock over the lookup, the
+  // attribute query and the reference: no other call can unregister a
+  // registry range between this call finding it mapped and taking its
+  // reference (the lookup used to come first, outside the lock).
+  const uint8_t* acquire(const uint8_t* p, size_t bytes, bool may_pin, uintptr_t* base) {
+    *base = 0;
+    if (bytes == 0) return nullptr;
     const uintptr_t a = reinterpret_cast<uintptr_t>(p) & ~uintptr_t(4095);
     const uintptr_t z = (reinterpret_cast<uintptr_t>(p) + bytes + 4095) & ~uintptr_t(4095);
     std::lock_guard<std::mutex> g(mu_);
     auto it = ranges_.upper_bound(a);  // the first range starting above a
+    bool overlap = it != ranges_.end() && it->first < z;
     if (it != ranges_.begin()) {
       auto pv = std::prev(it);
       if (pv->second.end >= z) {
+        const uint8_t* d = mapped_host_range(p, bytes);
+        if (!d) return nullptr;  // (cannot happen while registered; stage)
         ++pv->second.refs;
-        return pv->first;
+        *base = pv->first;
+        return d;
       }
-      if (pv->second.end > a) return 0;
+      overlap = overlap || pv->second.end > a;
     }
-    if (it != ranges_.end() && it->first < z) return 0;
+    if (overlap) return nullptr;  // partly inside a registry range: stage
+    if (const uint8_t* d = mapped_host_range(p, bytes)) return d;  // pinned by the caller
+    if (!may_pin || bytes < kPinMinBytes) return nullptr;
     if (hipHostRegister(reinterpret_cast<void*>(a), z - a, hipHostRegisterMapped | hipHostRegisterPortable) !=
         hipSuccess) {
       (void)hipGetLastError();  // refused (e.g. the caller registered an overlapping range): stage
-      return 0;
+      return nullptr;
+    }
+    const uint8_t* d = mapped_host_range(p, bytes);
+    if (!d) {
+      unregister(a);
+      return nullptr;
     }
     ranges_[a] = Range{z, 1};
-    return a;
+    *base = a;
+    return d;
   }
   void release(uintptr_t base) {
     std::lock_guard<std::mutex> g(mu_);
     auto it = ranges_.find(base);
     if (it == ranges_.end() || --it->second.refs) return;
-    (void)hipHostUnregister(reinterpret_cast<void*>(base));
+    unregister(base);
     ranges_.erase(it);
+  }
+  // Unregistrations the runtime refused (np_pin_registry_stats): a refused one
+  // leaves pages registered that the caller may free and the allocator may
+  // hand out again, so it is counted and reported, never ignored.
+  size_t failed_unregisters() const { return failed_.load(); }
+  size_t live_ranges() {
+    std::lock_guard<std::mutex> g(mu_);
+    return ranges_.size();
   }
 
  private:
+  void unregister(uintptr_t base) {
+    const hipError_t e = hipHostUnregister(reinterpret_cast<void*>(base));
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      if (failed_.fetch_add(1) == 0)
+        std::fprintf(stderr, "novelpoly: hipHostUnregister(%p) failed: %s\n", reinterpret_cast<void*>(base),
+                     hipGetErrorName(e));
+    }
+  }
   struct Range {
     uintptr_t end;
     size_t refs;
   };
   std::mutex mu_;
   std::map<uintptr_t, Range> ranges_;
+  std::atomic<size_t> failed_{0};
 };
 
 PinRegistry& pins() {
@@ -827,23 +923,6 @@ size_t rows_needed(const np_code_params* p, size_t shard_len, const uint8_t* pre
 // memory at the PCIe rate (tools/microbench/h2d_gather.hip).
 constexpr uint32_t kGatherBlocks = 32;
 
-// Device address of [p, p + bytes) when the whole range lies in one pinned host
-// allocation mapped into the device address space (hipHostMalloc, torch's
-// pin_memory, hipHostRegister), else nullptr (pageable memory).
-const uint8_t* mapped_host_range(const uint8_t* p, size_t bytes) {
-  if (bytes == 0) return nullptr;
-  hipPointerAttribute_t a0{}, a1{};
-  if (hipPointerGetAttributes(&a0, p) != hipSuccess || hipPointerGetAttributes(&a1, p + bytes - 1) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  if (a0.type != hipMemoryTypeHost || a1.type != hipMemoryTypeHost || !a0.devicePointer || !a1.devicePointer)
-    return nullptr;
-  const uint8_t* d0 = static_cast<const uint8_t*>(a0.devicePointer);
-  if (static_cast<const uint8_t*>(a1.devicePointer) != d0 + (bytes - 1)) return nullptr;
-  return d0;
-}
-
 // Pageable buffers are staged through pinned memory by host threads
 // (default), or with NP_PAGEABLE=pin pinned in place for the call (read per
 // call).
@@ -858,13 +937,8 @@ bool pageable_pin() {
 // operation on the span (the calls synchronise their streams before return).
 class HostSpan {
  public:
-  HostSpan(const void* p, size_t bytes, bool may_pin) {
-    const uint8_t* b = static_cast<const uint8_t*>(p);
-    dev_ = mapped_host_range(b, bytes);
-    if (dev_ || !may_pin || bytes < kPinMinBytes) return;
-    base_ = pins().acquire(p, bytes);
-    if (base_) dev_ = mapped_host_range(b, bytes);
-  }
+  HostSpan(const void* p, size_t bytes, bool may_pin)
+      : dev_(pins().acquire(static_cast<const uint8_t*>(p), bytes, may_pin, &base_)) {}
   ~HostSpan() {
     if (base_) pins().release(base_);
   }
@@ -874,8 +948,8 @@ class HostSpan {
   bool pinned() const { return dev_ != nullptr; }
 
  private:
-  const uint8_t* dev_ = nullptr;
   uintptr_t base_ = 0;
+  const uint8_t* dev_ = nullptr;
 };
 
 // Per-slot bookkeeping of a staged pipeline: a slot's pinned staging may be
@@ -912,6 +986,12 @@ void copy_blocks(uint8_t* dst, size_t dstride, const uint8_t* src, size_t sstrid
 }  // namespace
 
 extern "C" {
+
+void np_pin_registry_stats(size_t out[2]) {
+  if (!out) return;
+  out[0] = pins().live_ranges();
+  out[1] = pins().failed_unregisters();
+}
 
 int np_encode_batch_host(np_ctx* c, const np_code_params* p, const uint8_t* payloads, size_t len, size_t pstride,
                          size_t batch, uint8_t* shards, size_t bstride) {
@@ -1119,6 +1199,9 @@ int reconstruct_dev2(np_ctx* c, const np_code_params* p, const uint8_t* d_shards
   a.out_stride = out_stride;
   a.status = reinterpret_cast<uint32_t*>(d_status);
   a.trusted = trusted;
+#if NP_BOUNDS_CHECK
+  if (const char* st = std::getenv("NP_BOUNDS_SELFTEST")) a.chk_shrink_out = static_cast<uint32_t>(std::atoi(st));
+#endif
   return dev_err(HIP(launch_reconstruct(c, a, pick(c, stream))));
 }
 
@@ -1351,6 +1434,7 @@ int run_multi(np_ctx* const* ctxs, size_t nctx, size_t batch, F fn) {
     if (!ctxs[i]) return fail(NP_ERR_INVALID_ARGUMENT);
   std::vector<int> st(nctx, NP_OK);
   std::vector<std::array<size_t, 3>> det(nctx);
+  std::vector<std::string> site(nctx);  // the worker's np_last_error_site text (thread-local there)
   std::vector<std::thread> th;
   th.reserve(nctx);
   for (size_t i = 0; i < nctx; ++i) {
@@ -1359,11 +1443,16 @@ int run_multi(np_ctx* const* ctxs, size_t nctx, size_t batch, F fn) {
     th.emplace_back([&, i, b0, cnt] {
       st[i] = cnt ? fn(i, b0, cnt) : NP_OK;
       np_last_error_detail(det[i].data());
+      site[i] = g_site_msg;
     });
   }
   for (auto& t : th) t.join();
   for (size_t i = 0; i < nctx; ++i)
-    if (st[i] != NP_OK) return fail(st[i], det[i][0], det[i][1], det[i][2]);
+    if (st[i] != NP_OK) {
+      const int r = fail(st[i], det[i][0], det[i][1], det[i][2]);
+      std::snprintf(g_site_msg, sizeof g_site_msg, "%s", site[i].c_str());
+      return r;
+    }
   return NP_OK;
 }
 
@@ -1377,7 +1466,7 @@ int np_encode_batch_multi(np_ctx* const* ctxs, size_t nctx, const np_code_params
   if (!d_payloads || !d_shards) return fail(NP_ERR_INVALID_ARGUMENT);
   if (int st = check_params(p)) return st;
   return run_multi(ctxs, nctx, batch, [&](size_t i, size_t, size_t cnt) {
-    int st = np_encode_batch_dev(ctxs[i], p, d_payloads[i], len, pstride, cnt, d_shards[i], bstride, nullptr);
+    int st = np_encode_batch_dev(ctxs[i], p, d_payloads[i], len, pstride, cnt, d_shards[i], bstride, ctxs[i]->stream);
     return st ? st : np_ctx_synchronize(ctxs[i]);
   });
 }
@@ -1390,7 +1479,7 @@ int np_reconstruct_batch_multi(np_ctx* const* ctxs, size_t nctx, const np_code_p
   if (int st = check_params(p)) return st;
   return run_multi(ctxs, nctx, batch, [&](size_t i, size_t, size_t cnt) {
     int st = np_reconstruct_batch_dev3(ctxs[i], p, d_shards[i], shard_len, bstride, d_present[i], nullptr, cnt,
-                                       d_out[i], out_stride, d_status ? d_status[i] : nullptr, nullptr);
+                                       d_out[i], out_stride, d_status ? d_status[i] : nullptr, ctxs[i]->stream);
     return st ? st : np_ctx_synchronize(ctxs[i]);
   });
 }

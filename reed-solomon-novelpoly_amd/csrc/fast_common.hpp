@@ -1221,7 +1221,7 @@ __device__ __forceinline__ void fused_locator(const DevTables& T, const uint8_t*
                                               uint8_t* PR) {
   const uint32_t tid = threadIdx.x;
   for (uint32_t v = tid; v < N; v += NT) {
-    const uint8_t p = pres[v];
+    const uint8_t p = *NP_BCHK(pres + v, 1, kBkPresent);
     PR[v] = p;
     W[v] = p ? 0u : 1u;
   }
@@ -1254,7 +1254,7 @@ __device__ __forceinline__ void fused_locator(const DevTables& T, const uint8_t*
     }
     __syncthreads();
   }
-  for (uint32_t v = tid; v < N; v += NT) E[v] = T.exp[PR[v] ? W[v] : 65535u - W[v]];
+  for (uint32_t v = tid; v < N; v += NT) *NP_BCHK(E + v, 2, kBkRecords) = T.exp[NP_ICHK(PR[v] ? W[v] : 65535u - W[v], 65536u)];
 }
 
 }  // namespace

@@ -1210,8 +1210,8 @@ __device__ __forceinline__ void write_row_pools(const DevTables& T, const uint16
                                                 uint32_t rows, uint8_t* dst) {
   for (uint32_t v = threadIdx.x; v < rows; v += 256) {
     const uint32_t* pools = PR[v] ? T.in_pools : T.out_pools;
-    const uint4* src = reinterpret_cast<const uint4*>(pools + static_cast<size_t>(E[v]) * kPoolWords);
-    uint4* d = reinterpret_cast<uint4*>(dst + static_cast<size_t>(v) * 4 * kPoolWords);
+    const uint4* src = reinterpret_cast<const uint4*>(pools + static_cast<size_t>(NP_ICHK(*NP_BCHK(E + v, 2, kBkRecords), 65536u)) * kPoolWords);
+    uint4* d = NP_BCHK(reinterpret_cast<uint4*>(dst + static_cast<size_t>(v) * 4 * kPoolWords), 4 * kPoolWords, kBkRecords);
     const uint4 a0 = src[0], a1 = src[1], a2 = src[2], a3 = src[3], a4 = src[4];
     d[0] = a0, d[1] = a1, d[2] = a2, d[3] = a3, d[4] = a4;
   }
@@ -1230,7 +1230,7 @@ __device__ __forceinline__ void count_present(const uint8_t* pres, int& have1, i
   have1 = have2 = have = 0;
   for (int r = 0; r < N; r += 256) {
     const int v = static_cast<int>(threadIdx.x) + r;
-    const bool p = v < N && pres[v] != 0;
+    const bool p = v < N && *NP_BCHK(pres + v, 1, kBkPresent) != 0;
     if (r < K) have1 += __syncthreads_count(v < K && p);
     if (r < 2 * K) have2 += __syncthreads_count(v < 2 * K && p);
     have += __syncthreads_count(p);
@@ -1245,7 +1245,7 @@ __device__ __forceinline__ uint32_t segment_occupancy(const uint8_t* pres) {
 #pragma unroll 1
   for (int q = 0; q < N / K; ++q) {
     int any = 0;
-    for (int v = static_cast<int>(threadIdx.x); v < K; v += 256) any |= pres[q * K + v] != 0;
+    for (int v = static_cast<int>(threadIdx.x); v < K; v += 256) any |= *NP_BCHK(pres + (q * K + v), 1, kBkPresent) != 0;
     if (__syncthreads_or(any)) occ |= 1u << q;
   }
   return occ;
@@ -1256,8 +1256,8 @@ __device__ __forceinline__ uint32_t segment_occupancy(const uint8_t* pres) {
 __device__ __forceinline__ bool write_status(const ReconstructArgs& a, uint32_t pb, int have) {
   const bool ok = have >= static_cast<int>(a.k);  // mod.rs:178-180
   if (threadIdx.x == 0 && a.status) {
-    a.status[2 * pb] = ok ? 0u : kStatusNeedMoreShards;
-    a.status[2 * pb + 1] = static_cast<uint32_t>(have);
+    *NP_BCHK(a.status + 2 * pb, 4, kBkStatus) = ok ? 0u : kStatusNeedMoreShards;
+    *NP_BCHK(a.status + 2 * pb + 1, 4, kBkStatus) = static_cast<uint32_t>(have);
   }
   return ok;
 }
@@ -1269,6 +1269,13 @@ __global__ __launch_bounds__(256) void k_prefix_locator(DevTables T, Reconstruct
   __shared__ uint32_t W[N];
   __shared__ uint8_t PR[N];
   const uint32_t pb = blockIdx.x, tid = threadIdx.x;
+#if NP_BOUNDS_CHECK
+  {
+    ReconstructArgs ab = a;
+    ab.prefix = out;
+    bounds_arm(bounds_of(ab, T, prefix_stride_c(N, K)));
+  }
+#endif
   const uint8_t* pres = a.present + static_cast<size_t>(pb) * N;
   uint8_t* rec = out + static_cast<size_t>(pb) * prefix_stride_c(N, K);
   uint16_t* E = reinterpret_cast<uint16_t*>(rec + kPrefixHeader);
@@ -1280,7 +1287,7 @@ __global__ __launch_bounds__(256) void k_prefix_locator(DevTables T, Reconstruct
   // (inc_reconstruct.rs:61-85); the 2K-row prefix only for trusted codewords.
   const int nq = !write_status(a, pb, have) ? 0 : have1 == K ? 1 : (a.trusted && NQ == 4 && have2 >= K) ? 2 : NQ;
   const uint32_t occ = segment_occupancy<K, N>(pres);
-  if (tid == 0) rec[0] = static_cast<uint8_t>(nq), rec[1] = static_cast<uint8_t>(occ);
+  if (tid == 0) *NP_BCHK(rec, 2, kBkRecords) = static_cast<uint8_t>(nq), *NP_BCHK(rec + 1, 1, kBkRecords) = static_cast<uint8_t>(occ);
   if (nq <= 1) return;
   if (NQ == 4 && nq == 2) {
     fused_locator<2 * K, 256>(T, pres, W, E, PR);
@@ -1297,6 +1304,13 @@ template <int K, int NQ>
 __global__ __launch_bounds__(256) void k_locator_records(DevTables T, ReconstructArgs a, uint8_t* out) {
   constexpr int N = NQ * K;
   const uint32_t pb = blockIdx.x, tid = threadIdx.x;
+#if NP_BOUNDS_CHECK
+  {
+    ReconstructArgs ab = a;
+    ab.prefix = out;
+    bounds_arm(bounds_of(ab, T, prefix_stride_c(N, K)));
+  }
+#endif
   const uint16_t* loc = a.locators + static_cast<size_t>(pb) * N;
   uint8_t* rec = out + static_cast<size_t>(pb) * prefix_stride_c(N, K);
   uint16_t* E = reinterpret_cast<uint16_t*>(rec + kPrefixHeader);
@@ -1304,10 +1318,10 @@ __global__ __launch_bounds__(256) void k_locator_records(DevTables T, Reconstruc
   count_present<K, N>(a.present + static_cast<size_t>(pb) * N, have1, have2, have);
   const bool ok = write_status(a, pb, have);
   const uint32_t occ = segment_occupancy<K, N>(a.present + static_cast<size_t>(pb) * N);
-  if (tid == 0) rec[0] = static_cast<uint8_t>(ok ? NQ : 0), rec[1] = static_cast<uint8_t>(occ);
+  if (tid == 0) *NP_BCHK(rec, 2, kBkRecords) = static_cast<uint8_t>(ok ? NQ : 0), *NP_BCHK(rec + 1, 1, kBkRecords) = static_cast<uint8_t>(occ);
   if (!ok) return;
   // mul(x, log m) == x * EXP[m] (inc_log_mul.rs:42-49)
-  for (uint32_t v = tid; v < static_cast<uint32_t>(N); v += 256) E[v] = T.exp[loc[v]];
+  for (uint32_t v = tid; v < static_cast<uint32_t>(N); v += 256) *NP_BCHK(E + v, 2, kBkRecords) = T.exp[*NP_BCHK(loc + v, 2, kBkLocators)];
   write_row_pools(T, E, a.present + static_cast<size_t>(pb) * N, N, rec + prefix_pools_offset(N));
 }
 
@@ -1486,5 +1500,7 @@ hipError_t configure_fast_kernels() {
   set(reinterpret_cast<const void*>(&k_reconstruct_fast<256, 8, 8>), reconstruct_lds_bytes<256, 8>());
   return e;
 }
+
+hipError_t bounds_take_fast(uint32_t out[8]) { return bounds_take_tu(out); }
 
 }  // namespace np

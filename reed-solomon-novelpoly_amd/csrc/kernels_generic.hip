@@ -245,6 +245,16 @@ __global__ __launch_bounds__(1024) void k_error_locator(DevTables T, uint32_t n,
                                                         uint16_t* locators) {
   extern __shared__ uint16_t lw[];
   const size_t b = blockIdx.x;
+#if NP_BOUNDS_CHECK
+  {
+    BoundsSet bs{};
+    bs.lo[kBkPresent] = reinterpret_cast<uint64_t>(present);
+    bs.hi[kBkPresent] = bs.lo[kBkPresent] + static_cast<uint64_t>(gridDim.x) * n;
+    bs.lo[kBkLocators] = reinterpret_cast<uint64_t>(locators);
+    bs.hi[kBkLocators] = bs.lo[kBkLocators] + 2ull * gridDim.x * n;
+    bounds_arm(bs);
+  }
+#endif
   const uint8_t* pres = present + b * n;
   const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
   const uint32_t nr = BLK ? __builtin_amdgcn_readfirstlane(n >> 10) : (n > t ? (n - t + 1023u) >> 10 : 0u);
@@ -263,7 +273,7 @@ __global__ __launch_bounds__(1024) void k_error_locator(DevTables T, uint32_t n,
   uint32_t er[2] = {0u, 0u};  // bit r: row 1024 r + t erased (kept for the output)
 #pragma unroll
   for (int r = 0; r < 64; ++r) {
-    e[r] = in_n(r) ? (pres[t + 1024u * r] == 0) : 0;
+    e[r] = in_n(r) ? (*NP_BCHK(pres + (t + 1024u * r), 1, kBkPresent) == 0) : 0;
     er[r >> 5] |= static_cast<uint32_t>(e[r]) << (r & 31);
     if ((r & 15) == 15) __builtin_amdgcn_sched_barrier(0);  // 16 loads in flight, not 64 addresses live
   }
@@ -317,7 +327,8 @@ __global__ __launch_bounds__(1024) void k_error_locator(DevTables T, uint32_t n,
 #pragma unroll
   for (int r = 0; r < 64; ++r) {
     if (in_n(r))
-      locators[b * n + t + 1024u * r] = static_cast<uint16_t>(((er[r >> 5] >> (r & 31)) & 1u) ? kQ - v[r] : v[r]);
+      *NP_BCHK(locators + (b * n + t + 1024u * r), 2, kBkLocators) =
+          static_cast<uint16_t>(((er[r >> 5] >> (r & 31)) & 1u) ? kQ - v[r] : v[r]);
     if ((r & 15) == 15) __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -515,5 +526,7 @@ hipError_t launch_decode_main(const DevTables& T, uint16_t* codeword, uint32_t u
                                                                                  locator, n, cols, per);
   return hipGetLastError();
 }
+
+hipError_t bounds_take_generic(uint32_t out[8]) { return bounds_take_tu(out); }
 
 }  // namespace np

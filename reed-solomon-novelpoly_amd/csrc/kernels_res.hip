@@ -361,9 +361,12 @@ __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4))) void k_r
     DevTables T, ReconstructArgs a, uint32_t nsyms, uint32_t tiles) {
   // SERVE = 1: copies (nq = 1); 2: 2-segment decodes; 4: 4-segment decodes
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+#if NP_BOUNDS_CHECK
+  bounds_arm(bounds_of(a, T, prefix_stride_c(a.n, a.k)));
+#endif
   const TileRef tr = tile_of(blockIdx.x, tiles, (a.batch & 7u) == 0);
   const uint32_t pb = tr.pb, tl = tr.tl;
-  const uint8_t* rec = a.prefix + static_cast<size_t>(pb) * prefix_stride_c(a.n, a.k);
+  const uint8_t* rec = NP_BCHK(a.prefix + static_cast<size_t>(pb) * prefix_stride_c(a.n, a.k), 2, kBkRecords);
   const uint32_t nq = uniform(rec[0]);
   if (nq != static_cast<uint32_t>(SERVE)) return;
   const uint8_t* pools = rec + prefix_pools_offset(a.n);
@@ -468,5 +471,7 @@ hipError_t configure_res_kernels() {
   const hipError_t f = configure_res_k<512>();
   return e != hipSuccess ? e : f;
 }
+
+hipError_t bounds_take_res(uint32_t out[8]) { return bounds_take_tu(out); }
 
 }  // namespace np

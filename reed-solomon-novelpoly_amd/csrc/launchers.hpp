@@ -43,6 +43,11 @@ struct ReconstructArgs {
   // equals the reference's output only when the received shards form a
   // codeword.  Never set by the crate-equivalent entry points.
   bool trusted;
+#if NP_BOUNDS_CHECK
+  // Checked builds only: bytes taken off the end of the out extent the
+  // kernels check against (NP_BOUNDS_SELFTEST, the checker's own test).
+  uint32_t chk_shrink_out;
+#endif
 };
 
 // Status code of a payload with fewer than k present rows (include/novelpoly.h).
@@ -119,6 +124,13 @@ hipError_t launch_reconstruct_big(const DevTables& T, const ReconstructArgs& a, 
 }  // namespace np
 
 namespace np {
+// Checked builds (device_common.hpp, -DNP_BOUNDS_CHECK=1): the first bounds
+// violation record of each instrumented translation unit since the last call
+// (out[0] = count), then cleared; hipErrorNotSupported in the product build.
+hipError_t bounds_take_generic(uint32_t out[8]);
+hipError_t bounds_take_fast(uint32_t out[8]);
+hipError_t bounds_take_res(uint32_t out[8]);
+
 // Raises the dynamic-LDS limit of the kernels that need > 64 KiB (call once per device).
 hipError_t configure_generic_kernels();
 hipError_t configure_fast_kernels();

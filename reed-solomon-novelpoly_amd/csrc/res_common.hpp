@@ -826,7 +826,7 @@ __device__ __forceinline__ void dma_row_tables(uint8_t* tile, const uint8_t* poo
 #pragma unroll 1
   for (uint32_t pc = w; pc < pieces; pc += nwaves) {
     const uint32_t g = pc / 5, part = pc - 5 * g;
-    const uint8_t* src = src0 + 1280u * g + 256u * part;
+    const uint8_t* src = NP_BCHK(src0 + 1280u * g + 256u * part, 4, kBkRecords);
     const uint32_t dst = uniform(lds0 + kRowGroup * g + 256u * part);
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
@@ -919,7 +919,7 @@ __device__ __forceinline__ FullT row_table_at(const uint8_t* tile, uint32_t addr
 
 // Presence bits of this lane's 16 rows row0 + 64 w + 16 u + i (bit i).
 __device__ __forceinline__ uint32_t lane_rows_present(const uint8_t* pres, uint32_t row0, const Res& r) {
-  const uint8_t* p = pres + row0 + 64u * r.w + 16u * r.u;
+  const uint8_t* p = NP_BCHK(pres + row0 + 64u * r.w + 16u * r.u, 16, kBkPresent);
   uint32_t m = 0;
   if ((reinterpret_cast<uintptr_t>(p) & 3u) == 0) {
 #pragma unroll
@@ -946,6 +946,12 @@ __device__ __forceinline__ void load_lane_rows(uint2 (&raw)[NR], const uint8_t* 
 #pragma unroll
   for (int i = 0; i < NR; ++i) {
     const uint8_t* src = ((pm >> (i0 + i)) & 1u) ? base + static_cast<size_t>(i) * shard_len : zeros;
+#if NP_BOUNDS_CHECK
+    {  // the bytes load4 reads: columns 4 cq .. 4 cq + 3 below ncols
+      const uint32_t nb = full ? 8u : 2u * static_cast<uint32_t>(min(4, max(0, static_cast<int>(ncols) - 4 * static_cast<int>(r.cq))));
+      src = NP_BCHK2(src + 8u * r.cq, nb, kBkShards, kBkZeros) - 8u * r.cq;
+    }
+#endif
     raw[i] = load4(src, r.cq, ncols, full);
   }
 }
@@ -966,7 +972,7 @@ __device__ __forceinline__ void res_copy_out(uint8_t* out_tile, const uint32_t (
   for (int e = 0; e < 4; ++e) {
     const uint32_t c = 4u * r.cq + e;
     if (c >= ncols) break;
-    uint8_t* o = out_tile + static_cast<size_t>(c) * col_bytes + 128u * r.w + 32u * r.u;
+    uint8_t* o = NP_BCHK(out_tile + static_cast<size_t>(c) * col_bytes + 128u * r.w + 32u * r.u, 32, kBkOut);
     if (aligned16) {
       *reinterpret_cast<uint4*>(o) = make_uint4(d[0][e].x, d[0][e].y, d[1][e].x, d[1][e].y);
       *reinterpret_cast<uint4*>(o + 16) = make_uint4(d[2][e].x, d[2][e].y, d[3][e].x, d[3][e].y);

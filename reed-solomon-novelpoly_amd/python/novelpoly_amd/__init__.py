@@ -88,6 +88,8 @@ def lib() -> C.CDLL:
             "np_mul_dev": (C.c_int, [vp, vp, vp, vp, _sz, vp]),
             "np_encode_low_dev": (C.c_int, [vp, vp, _sz, vp, _sz, _sz, vp]),
             "np_decode_main_dev": (C.c_int, [vp, vp, _sz, vp, vp, _sz, _sz, vp]),
+            "np_debug_bounds_check": (C.c_int, [vp, C.POINTER(C.c_uint32)]),
+            "np_pin_registry_stats": (None, [C.POINTER(_sz)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -574,3 +576,29 @@ def decode_main_dev(d_codeword: int, recover_up_to: int, d_present: int, d_locat
 
 def version() -> str:
     return lib().np_version().decode()
+
+
+# ----------------------------------------------------------- diagnostics ----
+BOUNDS_KINDS = ("shards", "present", "locators", "records", "out", "status", "zeros")
+
+
+def debug_bounds_check(ctx: Optional[Context] = None) -> Optional[dict]:
+    """Checked builds (lib/libnovelpoly_hip_chk.so through NP_LIB_PATH): the
+    out-of-extent global accesses of the instrumented kernels since the last
+    call, {count, kind, line, workgroup, thread, offset, bytes} (count 0: none);
+    None with the product library."""
+    ctx = ctx or default_context()
+    r = (C.c_uint32 * 8)()
+    if lib().np_debug_bounds_check(ctx.handle, r) != 0:
+        return None
+    kind = BOUNDS_KINDS[r[1]] if r[0] and r[1] < len(BOUNDS_KINDS) else r[1]
+    return {"count": r[0], "kind": kind, "line": r[2], "workgroup": r[3], "thread": r[4],
+            "offset": r[5] | (r[6] << 32), "bytes": r[7]}
+
+
+def pin_registry_stats() -> dict:
+    """The engine's in-place pin registry: ranges registered now, and
+    hipHostUnregister calls the runtime refused (include/novelpoly.h)."""
+    o = (_sz * 2)()
+    lib().np_pin_registry_stats(o)
+    return {"live_ranges": o[0], "failed_unregisters": o[1]}

@@ -14,6 +14,8 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
+    config.addinivalue_line("markers", "default_stream: runs on torch's default stream (no per-test stream; "
+                            "tests/test_gpu_default_stream.py)")
     config.addinivalue_line("markers", "pin_in_place: NP_PAGEABLE=pin cases, run in a child process "
                             "(test_gpu_pin_isolated.py) so that the rest of the suite never shares a "
                             "process with buffers the engine registered in place")
@@ -78,10 +80,9 @@ def gpu():
 def _own_stream(request):
     """GPU tests run on a non-default torch stream, and the tests hand that
     stream to the library: torch's fills and copies and our kernels are then
-    ordered on one queue.  (A NULL stream means the context's own
-    non-blocking stream, which does not wait for work on torch's default,
-    legacy null stream.)"""
-    if request.node.get_closest_marker("gpu") is None:
+    ordered on one queue.  (A NULL stream is the legacy null stream, torch's
+    default stream: tests marked `default_stream` run there.)"""
+    if request.node.get_closest_marker("gpu") is None or request.node.get_closest_marker("default_stream"):
         yield
         return
     import torch
@@ -90,3 +91,18 @@ def _own_stream(request):
     with torch.cuda.stream(s):
         yield
     torch.cuda.synchronize()
+
+
+@pytest.fixture(autouse=True)
+def _bounds_checked(request):
+    """In the checked-build child of tests/test_gpu_bounds.py (NP_BOUNDS_CHILD,
+    NP_LIB_PATH = lib/libnovelpoly_hip_chk.so): after every GPU test, no global
+    access of the instrumented kernels fell outside its buffer."""
+    yield
+    if not os.environ.get("NP_BOUNDS_CHILD") or request.node.get_closest_marker("gpu") is None:
+        return
+    import novelpoly_amd as npa
+
+    r = npa.debug_bounds_check(npa.default_context(0))
+    assert r is not None, "NP_BOUNDS_CHILD set but the library is not the checked build"
+    assert r["count"] == 0, f"out-of-extent global accesses: {r}"
