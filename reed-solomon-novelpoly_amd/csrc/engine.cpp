@@ -9,6 +9,8 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <iterator>
 #include <map>
 #include <cstdio>
@@ -148,9 +150,10 @@ struct np_ctx {
   bool big_used = false;
   // Host-memory batch pipeline (np_*_batch_host): per slot a stream and
   // device buffers for one sub-batch; created on first use.
-  static constexpr int kPipe = 3;
+  static constexpr int kPipe = 6;  // at most; pipe_slots() are used
   hipStream_t pipe_s[kPipe] = {};
   DevBuf pipe_in[kPipe], pipe_out[kPipe];
+  DevBuf pipe_cin[kPipe];  // packed present rows and their offsets (np_reconstruct_batch_host)
   DevBuf pipe_pres;  // the present mask of a whole host reconstruct call
   // Pageable host reconstruct: pinned staging per slot for the present rows
   // (gathered by host threads) and for the outputs, and the slot's last event.
@@ -468,12 +471,84 @@ void stream_copy(uint8_t* dst, const uint8_t* src, size_t len) {
 void stream_fence() { _mm_sfence(); }
 
 // f(i) for i in [0, count) on up to kHostThreads host threads (the calling
-// thread is one of them): the host side of the pageable reconstruct's gather
-// and copy-out, which move memcpy-sized row pieces.
+// thread is one of them): the host side of the pageable calls' staging, which
+// moves memcpy-sized row pieces.  The workers persist for the process (one
+// pool; a staged call used to start and join 15 threads per step, twice per
+// sub-batch); a caller that finds the pool busy -- another context's call on
+// another thread -- starts threads of its own for that step as before.
 constexpr unsigned kHostThreads = 16;
+
+class HostPool {
+ public:
+  static HostPool& get() {
+    static HostPool* p = new HostPool;  // never destroyed: workers may be waiting at exit
+    return *p;
+  }
+  // false: busy (the caller falls back)
+  template <class F>
+  bool run(size_t count, F& f) {
+    std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
+    if (!busy.owns_lock()) return false;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      job_ = [](void* ctx, size_t i) { (*static_cast<F*>(ctx))(i); };
+      ctx_ = &f;
+      count_ = count;
+      next_.store(0);
+      active_ = workers_.size();
+      ++gen_;
+    }
+    cv_.notify_all();
+    drain(job_, ctx_, count);
+    stream_fence();
+    std::unique_lock<std::mutex> g(mu_);
+    done_cv_.wait(g, [&] { return active_ == 0; });
+    return true;
+  }
+  size_t threads() const { return workers_.size() + 1; }
+
+ private:
+  using Job = void (*)(void*, size_t);
+  HostPool() {
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const unsigned t = std::min(kHostThreads, hw);
+    for (unsigned w = 1; w < t; ++w) workers_.emplace_back([this] { loop(); });
+    for (auto& th : workers_) th.detach();
+  }
+  void drain(Job job, void* ctx, size_t count) {
+    for (size_t i = next_.fetch_add(1); i < count; i = next_.fetch_add(1)) job(ctx, i);
+  }
+  void loop() {
+    size_t seen = 0;
+    for (;;) {
+      Job job;
+      void* ctx;
+      size_t count;
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return gen_ != seen; });
+        seen = gen_;
+        job = job_, ctx = ctx_, count = count_;
+      }
+      drain(job, ctx, count);
+      stream_fence();
+      std::lock_guard<std::mutex> g(mu_);
+      if (--active_ == 0) done_cv_.notify_one();
+    }
+  }
+  std::vector<std::thread> workers_;
+  std::mutex run_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  Job job_ = nullptr;
+  void* ctx_ = nullptr;
+  size_t count_ = 0, active_ = 0, gen_ = 0;
+  std::atomic<size_t> next_{0};
+};
 
 template <class F>
 void parallel_for(size_t count, F f) {
+  if (count == 0) return;
+  if (count > 1 && HostPool::get().threads() > 1 && HostPool::get().run(count, f)) return;
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
   const size_t t = std::min<size_t>({count, kHostThreads, hw});
   if (t <= 1) {
@@ -654,6 +729,7 @@ void np_ctx_destroy(np_ctx* c) {
     if (c->pipe_s[i]) (void)hipStreamSynchronize(c->pipe_s[i]);
     c->pipe_in[i].release();
     c->pipe_out[i].release();
+    c->pipe_cin[i].release();
     c->pipe_hin[i].release();
     c->pipe_hout[i].release();
     if (c->pipe_ev[i]) (void)hipEventDestroy(c->pipe_ev[i]);
@@ -754,7 +830,8 @@ int np_encode_batch_dev(np_ctx* c, const np_code_params* p, const uint8_t* d_pay
 // calls, not traced to any kernel), so pinning in place is opt-in.
 namespace {
 
-constexpr size_t kPipeSlotBytes = size_t(64) << 20;
+constexpr size_t kPipeSlotBytes = size_t(64) << 20;  // encode: payloads + shard rows per sub-batch
+constexpr size_t kPipeMovedBytes = size_t(24) << 20;         // reconstruct: PCIe bytes per sub-batch
 // Pageable spans below this are staged: registering and unregistering them
 // costs more than copying them.
 constexpr size_t kPinMinBytes = size_t(1) << 20;
@@ -871,8 +948,17 @@ PinRegistry& pins() {
   return *r;
 }
 
-hipError_t pipe_init(np_ctx* c) {
-  for (int i = 0; i < np_ctx::kPipe; ++i) {
+// Slots (streams) of the host pipeline: 4 (config-3 / 4 reconstruct from
+// pageable buffers 16.6 / 22.1 GiB/s with 3, 17.7 / 22.8 with 4, no better
+// with 6; profiles/r06/pipe_probe2_cfg{3,4}.txt); NP_PIPE_SLOTS overrides
+// (experiments).
+int pipe_slots() {
+  const char* e = std::getenv("NP_PIPE_SLOTS");
+  return e ? std::min(np_ctx::kPipe, std::max(1, std::atoi(e))) : 4;
+}
+
+hipError_t pipe_init(np_ctx* c, int npipe) {
+  for (int i = 0; i < npipe; ++i) {
     if (!c->pipe_s[i]) {
       hipError_t e = HIP(hipStreamCreateWithFlags(&c->pipe_s[i], hipStreamNonBlocking));
       if (e != hipSuccess) return e;
@@ -887,6 +973,7 @@ hipError_t pipe_init(np_ctx* c) {
 
 hipError_t pipe_sync(np_ctx* c, hipError_t e) {
   for (int i = 0; i < np_ctx::kPipe; ++i) {
+    if (!c->pipe_s[i]) continue;
     const hipError_t r = HIP(hipStreamSynchronize(c->pipe_s[i]));
     if (e == hipSuccess) e = r;
   }
@@ -922,6 +1009,10 @@ size_t rows_needed(const np_code_params* p, size_t shard_len, const uint8_t* pre
 // Workgroups of the present-row gather (launch_copy_rows): 32 read host
 // memory at the PCIe rate (tools/microbench/h2d_gather.hip).
 constexpr uint32_t kGatherBlocks = 32;
+// Pinned callers' present rows: packed by host threads and DMA'd (true) or
+// gathered by k_copy_rows from the caller's memory (false); NP_HOST_ROWS
+// overrides per call.
+constexpr bool kPinnedPack = true;
 
 // Pageable buffers are staged through pinned memory by host threads
 // (default), or with NP_PAGEABLE=pin pinned in place for the call (read per
@@ -955,15 +1046,37 @@ class HostSpan {
 // Per-slot bookkeeping of a staged pipeline: a slot's pinned staging may be
 // refilled once the sub-batch that last used it is done (its event), whose
 // staged outputs are then handed to the caller (copy_out(b0, cnt, slot)).
+// NP_PIPE_STATS=1: the host pipeline's time split (waits for slots, host
+// copies out, packing, the rest) on stderr per call -- the measurements of
+// DESIGN.md §4.7.
+struct PipeStats {
+  bool on = std::getenv("NP_PIPE_STATS") != nullptr;
+  double wait = 0, out = 0, pack = 0;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  static double ms(std::chrono::steady_clock::time_point a) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+  }
+  void report(const char* what, size_t sb, size_t batch) const {
+    if (on)
+      std::fprintf(stderr, "np pipe %s: %.3f ms, %zu sub-batches of %zu: wait %.3f, copy-out %.3f, pack %.3f\n", what,
+                   ms(t0), (batch + sb - 1) / sb, sb, wait, out, pack);
+  }
+};
+
 struct SlotRing {
   np_ctx* c;
+  PipeStats* st = nullptr;
   size_t b0[np_ctx::kPipe] = {}, cnt[np_ctx::kPipe] = {};
   template <class F>
   void drain(int sl, hipError_t& e, F copy_out) {
     if (!cnt[sl]) return;
+    auto t = std::chrono::steady_clock::now();
     const hipError_t r = HIP(hipEventSynchronize(c->pipe_ev[sl]));
+    if (st) st->wait += PipeStats::ms(t);
     if (e == hipSuccess) e = r;
+    t = std::chrono::steady_clock::now();
     if (r == hipSuccess) copy_out(b0[sl], cnt[sl], sl);
+    if (st) st->out += PipeStats::ms(t);
     cnt[sl] = 0;
   }
   hipError_t mark(int sl, hipStream_t s, size_t first, size_t count) {
@@ -1008,9 +1121,10 @@ int np_encode_batch_host(np_ctx* c, const np_code_params* p, const uint8_t* payl
   const bool may_pin = pageable_pin();
   const HostSpan hin(payloads, span_in, may_pin), hout(shards, span_out, may_pin);
   const bool st_in = !hin.pinned(), st_out = !hout.pinned();
-  hipError_t e = pipe_init(c);
+  const int npipe = pipe_slots();
+  hipError_t e = pipe_init(c, npipe);
   const size_t sb = std::min(batch, std::max<size_t>(1, kPipeSlotBytes / (len + row_bytes)));
-  for (int i = 0; e == hipSuccess && i < np_ctx::kPipe; ++i) {
+  for (int i = 0; e == hipSuccess && i < npipe; ++i) {
     e = HIP(c->pipe_in[i].ensure(sb * len));
     if (e == hipSuccess) e = HIP(c->pipe_out[i].ensure(sb * row_bytes));
     if (e == hipSuccess && st_in) e = HIP(c->pipe_hin[i].ensure(sb * len));
@@ -1021,7 +1135,7 @@ int np_encode_batch_host(np_ctx* c, const np_code_params* p, const uint8_t* payl
     if (st_out) copy_blocks(shards + b0 * bstride, bstride, c->pipe_hout[sl].as<uint8_t>(), row_bytes, row_bytes, cnt);
   };
   int slot = 0;
-  for (size_t b0 = 0; e == hipSuccess && b0 < batch; b0 += sb, slot = (slot + 1) % np_ctx::kPipe) {
+  for (size_t b0 = 0; e == hipSuccess && b0 < batch; b0 += sb, slot = (slot + 1) % npipe) {
     const size_t cnt = std::min(sb, batch - b0);
     hipStream_t s = c->pipe_s[slot];
     uint8_t* din = c->pipe_in[slot].as<uint8_t>();
@@ -1047,7 +1161,7 @@ int np_encode_batch_host(np_ctx* c, const np_code_params* p, const uint8_t* payl
   }
   // the pending slots, oldest first: `slot` is the next one the loop would
   // have used, i.e. the one used longest ago
-  for (int i = 0; i < np_ctx::kPipe; ++i) ring.drain((slot + i) % np_ctx::kPipe, e, copy_out);
+  for (int i = 0; i < npipe; ++i) ring.drain((slot + i) % npipe, e, copy_out);
   return dev_err(pipe_sync(c, e));
 }
 
@@ -1075,26 +1189,45 @@ int np_reconstruct_batch_host(np_ctx* c, const np_code_params* p, const uint8_t*
   const bool may_pin = pageable_pin();
   const HostSpan hin(shards, span_in, may_pin), hout(out, span_out, may_pin);
   const bool st_in = !hin.pinned(), st_out = !hout.pinned();
-  // The present rows go by the gather kernel (k_copy_rows: 682 of 1024 rows
-  // cross PCIe at config 3, 1366 of 4096 at config 4) when the rows are 4-byte
-  // aligned in the source (it moves 16- or 4-byte pieces), else the first
-  // `rows` rows of every payload by one 2-D DMA.  The outputs go by DMA either
-  // way (the link shares badly between kernel reads of host
-  // memory and any D2H, but a DMA D2H is the best of it).
-  const bool gather = st_in ? (shard_len & 3) == 0 : ((reinterpret_cast<uintptr_t>(shards) | bstride | shard_len) & 3) == 0;
-  hipError_t e = pipe_init(c);
-  const size_t sb = std::min(batch, std::max<size_t>(1, kPipeSlotBytes / (in_bytes + olen)));
+  // How the present rows (682 of 1024 per payload at config 3, 1366 of 4096
+  // at config 4) reach the device:
+  //  - pack: host threads pack a sub-batch's present rows one after the other
+  //    into the slot's pinned staging, with each row's device offset; one DMA
+  //    moves both, and k_expand_rows puts the rows in place (HBM to HBM).
+  //    Staged (pageable) spans always go this way: the host copy is needed
+  //    anyway, and DMA in both directions shares PCIe better than kernel
+  //    reads of host memory next to a DMA D2H;
+  //  - gather: k_copy_rows reads the present rows straight from the caller's
+  //    pinned rows (4-byte aligned), no host copy;
+  //  - dma2d: the first `rows` rows of every payload by one 2-D DMA (pinned,
+  //    unaligned rows).
+  // Pinned callers: NP_HOST_ROWS=pack / gather picks (read per call; default
+  // below, measured in DESIGN.md §6).
+  enum class Rows { Pack, Gather, Dma2d };
+  const bool aligned = ((reinterpret_cast<uintptr_t>(shards) | bstride | shard_len) & 3) == 0;
+  const char* hr = std::getenv("NP_HOST_ROWS");
+  const bool pinned_pack = hr ? std::strcmp(hr, "pack") == 0 : kPinnedPack;
+  const Rows mode = st_in || pinned_pack ? Rows::Pack : aligned ? Rows::Gather : Rows::Dma2d;
+  const int npipe = pipe_slots();
+  hipError_t e = pipe_init(c, npipe);
+  // Sub-batches of about kPipeMovedBytes of PCIe traffic (the present rows in,
+  // the outputs out): 7 payloads at config 3, 3 at config 4 (the best of
+  // profiles/r06/pipe_probe2_cfg{3,4}.txt); NP_PIPE_SB (payloads) overrides.
+  size_t moved = 0;  // present rows the kernels read, over the whole call
+  for (size_t b = 0; b < batch; ++b)
+    for (size_t v = 0; v < rows; ++v) moved += present[b * n + v] ? 1 : 0;
+  const size_t per = moved * shard_len / batch + olen;
+  size_t sb = std::min(batch, std::max<size_t>(1, (kPipeMovedBytes + per - 1) / per));
+  if (const char* v = std::getenv("NP_PIPE_SB")) sb = std::min(batch, std::max<size_t>(1, std::strtoul(v, nullptr, 10)));
   const size_t slot_in = (sb - 1) * dstride + in_bytes;
-  for (int i = 0; e == hipSuccess && i < np_ctx::kPipe; ++i) {
+  const size_t nblk = (rows + 63) / 64;  // packing tasks per payload: 64 rows each
+  const size_t pack_cap = (sb * rows * 8 + 255) / 256 * 256 + sb * rows * shard_len;  // offsets, then rows
+  for (int i = 0; e == hipSuccess && i < npipe; ++i) {
     e = HIP(c->pipe_in[i].ensure(slot_in));
     if (e == hipSuccess) e = HIP(c->pipe_out[i].ensure(sb * olen));
-    if (e == hipSuccess && st_in) e = HIP(c->pipe_hin[i].ensure(slot_in));
+    if (e == hipSuccess && mode == Rows::Pack) e = HIP(c->pipe_hin[i].ensure(pack_cap));
+    if (e == hipSuccess && mode == Rows::Pack) e = HIP(c->pipe_cin[i].ensure(pack_cap));
     if (e == hipSuccess && st_out) e = HIP(c->pipe_hout[i].ensure(sb * olen));
-  }
-  const uint8_t* hin_dev[np_ctx::kPipe] = {};
-  for (int i = 0; st_in && gather && e == hipSuccess && i < np_ctx::kPipe; ++i) {
-    hin_dev[i] = mapped_host_range(c->pipe_hin[i].as<uint8_t>(), slot_in);
-    if (!hin_dev[i]) e = HIP(hipErrorInvalidValue);  // hipHostMalloc memory is mapped
   }
   // the whole present mask up front, through pinned staging, before any
   // sub-batch reads it
@@ -1105,12 +1238,14 @@ int np_reconstruct_batch_host(np_ctx* c, const np_code_params* p, const uint8_t*
     e = HIP(hipMemcpyAsync(c->pipe_pres.p, c->h_pres.p, batch * n, hipMemcpyHostToDevice, c->pipe_s[0]));
   }
   if (e == hipSuccess) e = HIP(hipStreamSynchronize(c->pipe_s[0]));
-  SlotRing ring{c};
+  PipeStats stats;
+  SlotRing ring{c, &stats};
   auto copy_out = [&](size_t b0, size_t cnt, int sl) {  // staged outputs -> the caller's buffer
     if (st_out) copy_blocks(out + b0 * out_stride, out_stride, c->pipe_hout[sl].as<uint8_t>(), olen, olen, cnt);
   };
+  std::vector<size_t> base;  // packed index of the first present row of each (payload, 64-row block)
   int slot = 0;
-  for (size_t b0 = 0; e == hipSuccess && b0 < batch; b0 += sb, slot = (slot + 1) % np_ctx::kPipe) {
+  for (size_t b0 = 0; e == hipSuccess && b0 < batch; b0 += sb, slot = (slot + 1) % npipe) {
     const size_t cnt = std::min(sb, batch - b0);
     hipStream_t s = c->pipe_s[slot];
     uint8_t* din = c->pipe_in[slot].as<uint8_t>();
@@ -1119,24 +1254,45 @@ int np_reconstruct_batch_host(np_ctx* c, const np_code_params* p, const uint8_t*
     ring.drain(slot, e, copy_out);  // the slot's staging is free again
     if (e != hipSuccess) break;
     const uint8_t* src = shards + b0 * bstride;
-    const uint8_t* src_dev = st_in ? hin_dev[slot] : hin.dev() + b0 * bstride;
-    size_t pitch = bstride;
-    if (st_in) {  // host threads copy the present rows among the first `rows` into the slot's staging
+    if (mode == Rows::Pack) {
+      base.assign(cnt * nblk + 1, 0);
+      for (size_t t = 0; t < cnt * nblk; ++t) {
+        const uint8_t* pr = present + (b0 + t / nblk) * n + 64 * (t % nblk);
+        const size_t m = std::min<size_t>(64, rows - 64 * (t % nblk));
+        size_t have = 0;
+        for (size_t v = 0; v < m; ++v) have += pr[v] ? 1 : 0;
+        base[t + 1] = base[t] + have;
+      }
+      const size_t total = base.back(), list_bytes = (total * 8 + 255) / 256 * 256;
       uint8_t* h = c->pipe_hin[slot].as<uint8_t>();
-      const size_t nrows = cnt * rows;
-      parallel_for((nrows + 63) / 64, [&](size_t i) {  // 64 rows per task
-        for (size_t r = 64 * i; r < std::min(nrows, 64 * i + 64); ++r) {
-          const size_t b = r / rows, v = r % rows;
-          if (present[(b0 + b) * n + v]) stream_copy(h + b * dstride + v * shard_len, src + b * bstride + v * shard_len, shard_len);
+      uint64_t* list = reinterpret_cast<uint64_t*>(h);
+      uint8_t* data = h + list_bytes;
+      const auto tp = std::chrono::steady_clock::now();
+      parallel_for(cnt * nblk, [&](size_t t) {
+        const size_t b = t / nblk, v0 = 64 * (t % nblk), m = std::min<size_t>(64, rows - v0);
+        const uint8_t* pr = present + (b0 + b) * n + v0;
+        size_t j = base[t];
+        for (size_t v = 0; v < m; ++v) {
+          if (!pr[v]) continue;
+          stream_copy(data + j * shard_len, src + b * bstride + (v0 + v) * shard_len, shard_len);
+          list[j++] = b * dstride + (v0 + v) * shard_len;
         }
       });
-      src = h;
-      pitch = dstride;
+      stats.pack += PipeStats::ms(tp);
+      uint8_t* cin = c->pipe_cin[slot].as<uint8_t>();
+      e = HIP(hipMemcpyAsync(cin, h, list_bytes + total * shard_len, hipMemcpyHostToDevice, s));
+      e = after(e, s, __LINE__, "packed rows H2D");
+      if (e == hipSuccess)
+        e = HIP(np::launch_expand_rows(cin + list_bytes, reinterpret_cast<const uint64_t*>(cin), din, shard_len, total, s));
+      e = after(e, s, __LINE__, "packed rows expand");
+    } else if (mode == Rows::Gather) {
+      e = HIP(np::launch_copy_rows(hin.dev() + b0 * bstride, bstride, din, dstride, shard_len, dpres,
+                                   static_cast<uint32_t>(n), static_cast<uint32_t>(rows), cnt, kGatherBlocks, s));
+      e = after(e, s, __LINE__, "present-row gather");
+    } else {
+      e = HIP(hipMemcpy2DAsync(din, dstride, src, bstride, in_bytes, cnt, hipMemcpyHostToDevice, s));
+      e = after(e, s, __LINE__, "shard rows H2D");
     }
-    e = gather ? HIP(np::launch_copy_rows(src_dev, pitch, din, dstride, shard_len, dpres, static_cast<uint32_t>(n),
-                                          static_cast<uint32_t>(rows), cnt, kGatherBlocks, s))
-               : HIP(hipMemcpy2DAsync(din, dstride, src, pitch, in_bytes, cnt, hipMemcpyHostToDevice, s));
-    e = after(e, s, __LINE__, gather ? "present-row gather" : "shard rows H2D");
     if (e == hipSuccess) {
       np::ReconstructArgs a{};
       a.shards = din;
@@ -1157,11 +1313,13 @@ int np_reconstruct_batch_host(np_ctx* c, const np_code_params* p, const uint8_t*
                  : HIP(hipMemcpy2DAsync(out + b0 * out_stride, out_stride, dout, olen, olen, cnt,
                                         hipMemcpyDeviceToHost, s));
     e = after(e, s, __LINE__, "outputs D2H");
-    if (e == hipSuccess && (st_in || st_out)) e = ring.mark(slot, s, b0, cnt);
+    if (e == hipSuccess && (mode == Rows::Pack || st_out)) e = ring.mark(slot, s, b0, cnt);
   }
   // the pending slots, oldest first (a failed call still waits for its streams)
-  for (int i = 0; i < np_ctx::kPipe; ++i) ring.drain((slot + i) % np_ctx::kPipe, e, copy_out);
-  return dev_err(pipe_sync(c, e));
+  for (int i = 0; i < npipe; ++i) ring.drain((slot + i) % npipe, e, copy_out);
+  e = pipe_sync(c, e);
+  stats.report(mode == Rows::Pack ? "reconstruct (pack)" : mode == Rows::Gather ? "reconstruct (gather)" : "reconstruct (2-D DMA)", sb, batch);
+  return dev_err(e);
 }
 
 // ---------------------------------------------------------- reconstruct ----

@@ -109,7 +109,60 @@ __global__ __launch_bounds__(64 * kXferWaves) void k_copy_rows(const uint8_t* __
   }
 }
 
+// np_reconstruct_batch_host's packed present rows (engine.cpp, host-memory
+// pipeline): host threads pack the present rows of a sub-batch one after the
+// other into pinned staging (row j at src + j * row_bytes) with the device
+// offset of each (dst_off[j] = b * dstride + v * row_bytes), one DMA brings
+// both over, and this kernel puts every row in its place of the n-row device
+// layout (HBM to HBM).  One wave per 4 KiB piece of a row.
+__global__ __launch_bounds__(64 * kXferWaves) void k_expand_rows(const uint8_t* __restrict__ src,
+                                                                const uint64_t* __restrict__ dst_off,
+                                                                uint8_t* __restrict__ dst, size_t row_bytes,
+                                                                size_t chunks, size_t total) {
+  const uint32_t lane = threadIdx.x & 63;
+  const size_t waves = static_cast<size_t>(gridDim.x) * kXferWaves;
+  for (size_t u = static_cast<size_t>(blockIdx.x) * kXferWaves + (threadIdx.x >> 6); u < total; u += waves) {
+    const size_t j = u / chunks, ch = u - j * chunks;
+    const size_t off = ch * kXferChunk, len = row_bytes - off < kXferChunk ? row_bytes - off : kXferChunk;
+    const uint8_t* s = src + j * row_bytes + off;
+    uint8_t* d = dst + dst_off[j] + off;
+    const uintptr_t al = reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d) | len;
+    if ((al & 15) == 0) {
+      const uint4* s4 = reinterpret_cast<const uint4*>(s);
+      uint4* d4 = reinterpret_cast<uint4*>(d);
+      const size_t q = len / 16;
+      if (q == 256) {
+        const uint4 x0 = s4[lane], x1 = s4[lane + 64], x2 = s4[lane + 128], x3 = s4[lane + 192];
+        d4[lane] = x0;
+        d4[lane + 64] = x1;
+        d4[lane + 128] = x2;
+        d4[lane + 192] = x3;
+      } else {
+        for (size_t i = lane; i < q; i += 64) d4[i] = s4[i];
+      }
+    } else if ((al & 3) == 0) {
+      const uint32_t* s1 = reinterpret_cast<const uint32_t*>(s);
+      uint32_t* d1 = reinterpret_cast<uint32_t*>(d);
+      for (size_t i = lane; i < len / 4; i += 64) d1[i] = s1[i];
+    } else {  // rows are whole symbols: 2-byte pieces
+      const uint16_t* s1 = reinterpret_cast<const uint16_t*>(s);
+      uint16_t* d1 = reinterpret_cast<uint16_t*>(d);
+      for (size_t i = lane; i < len / 2; i += 64) d1[i] = s1[i];
+    }
+  }
+}
+
 }  // namespace
+
+hipError_t launch_expand_rows(const uint8_t* src, const uint64_t* dst_off, uint8_t* dst, size_t row_bytes,
+                              size_t nrows, hipStream_t s) {
+  const size_t chunks = (row_bytes + kXferChunk - 1) / kXferChunk, total = nrows * chunks;
+  if (total == 0) return hipSuccess;
+  if (row_bytes & 1) return hipErrorInvalidValue;
+  const size_t grid = std::min<size_t>((total + kXferWaves - 1) / kXferWaves, 4096);
+  k_expand_rows<<<static_cast<uint32_t>(grid), 64 * kXferWaves, 0, s>>>(src, dst_off, dst, row_bytes, chunks, total);
+  return hipGetLastError();
+}
 
 hipError_t launch_systematic(const uint8_t* shards, size_t shard_len, size_t bstride, uint32_t k, size_t batch,
                              uint8_t* out, size_t ostride, hipStream_t s) {

@@ -82,6 +82,12 @@ hipError_t launch_copy_rows(const uint8_t* src, size_t sstride, uint8_t* dst, si
                             const uint8_t* present, uint32_t n, uint32_t rows, size_t count, uint32_t blocks,
                             hipStream_t s);
 
+// dst + dst_off[j] = row j of src (row_bytes each, rows packed one after the
+// other), for j < nrows: the packed present rows of a staged host reconstruct
+// put in their n-row device layout.  row_bytes even.
+hipError_t launch_expand_rows(const uint8_t* src, const uint64_t* dst_off, uint8_t* dst, size_t row_bytes,
+                              size_t nrows, hipStream_t s);
+
 // ---- fast path (kernels_fast.hip) ----
 // Returns true if a specialised kernel serves (n, k).
 bool fast_encode_supported(uint32_t n, uint32_t k);

@@ -170,3 +170,49 @@ def test_multi_empty_batch_ok(gpu):
     npa.encode_batch_dev(p, ptr, 16, 16, 0, ptr, bstride, ctx=gpu)
     npa.encode_batch_multi(ctxs, p, [ptr, ptr], 16, 16, 0, [ptr, ptr], bstride)
     npa.encode_batch_host_multi(ctxs, p, ptr, 16, 16, 0, ptr, bstride)
+
+
+@pytest.mark.pin_in_place
+def test_pin_registry_two_threads_share_pages(gpu, oracle, monkeypatch):
+    """two host calls at once, on two contexts from two threads,
+    with NP_PAGEABLE=pin, on adjacent slices of one pageable buffer whose
+    spans share a page.  Whichever call registers the shared range first, the
+    other finds its span inside a registry range (or partly overlapping one)
+    and takes a reference (or stages) under the registry's lock
+    (engine.cpp PinRegistry::acquire), so no range is unregistered under the
+    other call's DMA or gather.  Afterwards no range stays registered and no
+    unregistration was refused; every payload against the oracle."""
+    import threading
+
+    monkeypatch.setenv("NP_PAGEABLE", "pin")
+    ctxs = [npa.Context(0), npa.Context(0)]
+    p = npa.CodeParams.derive_parameters(1024, 342)
+    n, k = p.n(), p.k()
+    plen, per = 128 * 1024 + 5, 3  # shard_len 514: spans of 1.5 MiB per call
+    sl = p.make_encoder(gpu).shard_len(plen)
+    bstride, olen = n * sl + 100, (sl // 2) * 2 * k
+    batch = 2 * per
+    pay = np.stack([np.frombuffer(synth.payload(970 + b, plen), np.uint8) for b in range(batch)])
+    sh = np.zeros((batch, bstride), np.uint8)
+    npa.encode_batch_host(p, pay.ctypes.data, plen, plen, batch, sh.ctypes.data, bstride, ctx=ctxs[0])
+    pres = np.stack([synth.present_mask(970 + b, n, 342) for b in range(batch)])
+    outs = [np.zeros((per, olen), np.uint8) for _ in range(2)]
+    errors = []
+
+    def worker(i):
+        try:
+            for _ in range(12):
+                npa.reconstruct_batch_host(p, sh.ctypes.data + i * per * bstride, sl, bstride,
+                                           pres[i * per:].ctypes.data, per, outs[i].ctypes.data, olen, ctx=ctxs[i])
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
+    assert npa.pin_registry_stats() == {"live_ranges": 0, "failed_unregisters": 0}
+    for b in range(batch):
+        assert outs[b // per][b % per, :plen].tobytes() == pay[b].tobytes(), b

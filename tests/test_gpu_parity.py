@@ -748,8 +748,8 @@ def _host_array(shape, fill, pinned, offset=0):
 
 
 @pytest.mark.parametrize("pinned,mode", [pytest.param(False, "pin", marks=pytest.mark.pin_in_place), (False, "stage"),
-                                        (True, "stage")],
-                         ids=["pageable-pin", "pageable", "pinned"])
+                                        (True, "stage"), (True, "gather")],
+                         ids=["pageable-pin", "pageable", "pinned", "pinned-gather"])
 @pytest.mark.parametrize("nw,kw,plen,batch,offset", [(1024, 342, 512 * 256, 9, 0), (256, 86, 128 * 99 + 1, 7, 0),
                                                      (300, 100, 5000, 3, 2), (4096, 1366, 2048 * 40, 2, 0),
                                                      (1024, 342, 512 * 256, 3, 6)])
@@ -760,7 +760,13 @@ def test_host_batch_pipeline(gpu, oracle, nw, kw, plen, batch, offset, pinned, m
     gathered over PCIe by a kernel) and garbage in the absent rows included.
     Pageable buffers go through host-thread staging (the default) or, with
     NP_PAGEABLE=pin, pinned in place for the call (engine.cpp reads the
-    variable per call; those cases run in a child process)."""
+    variable per call; those cases run in a child process).  Pinned present
+    rows are packed by host threads and DMA'd (the default), or with
+    NP_HOST_ROWS=gather read by the k_copy_rows kernel (4-byte aligned rows;
+    the unaligned start takes the 2-D DMA)."""
+    if mode == "gather":
+        monkeypatch.setenv("NP_HOST_ROWS", "gather")
+        mode = "stage"
     monkeypatch.setenv("NP_PAGEABLE", mode)
     p = npa.CodeParams.derive_parameters(nw, kw)
     n, k = p.n(), p.k()

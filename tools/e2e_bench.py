@@ -65,6 +65,17 @@ def rec():
 h_out.zero_()
 t_rec = timed(rec)
 ok = torch.equal(h_out[:, :plen], h_pay)
+# pinned buffers, present rows packed by host threads and DMA'd (NP_HOST_ROWS=pack)
+# instead of gathered by the k_copy_rows kernel
+os.environ["NP_HOST_ROWS"] = "pack"
+h_out.zero_()
+t_rec_pack = timed(rec)
+ok = ok and torch.equal(h_out[:, :plen], h_pay)
+os.environ["NP_HOST_ROWS"] = "gather"
+h_out.zero_()
+t_rec_gather = timed(rec)
+ok = ok and torch.equal(h_out[:, :plen], h_pay)
+del os.environ["NP_HOST_ROWS"]
 # bytes crossing PCIe: encode P in + n*sl out; reconstruct the rows the engine
 # reads (engine.cpp rows_needed: the k systematic rows when every payload of the
 # batch has them all, else all n rows), of those only the present ones on the
@@ -137,6 +148,9 @@ res = {
                     # the two directions one after the other: kernel reads of host memory and a
                     # concurrent D2H share the link badly (tools/microbench/h2d_gather.hip)
                     "pcie_serial_bound_GiB_s": round(B * plen / (B * rows * sl / (bw_h2d * 1e9) + B * olen / (bw_d2h * 1e9)) / 2**30, 2)},
+    "reconstruct_pinned_pack": {"GiB_s": round(B * plen / t_rec_pack / 2**30, 2), "ms": round(t_rec_pack * 1e3, 2)},
+    "reconstruct_pinned_gather": {"GiB_s": round(B * plen / t_rec_gather / 2**30, 2),
+                                  "ms": round(t_rec_gather * 1e3, 2)},
     "encode_pageable_pinned_in_place": {"GiB_s": round(B * plen / t_enc_pg / 2**30, 2), "ms": round(t_enc_pg * 1e3, 2)},
     "reconstruct_pageable_pinned_in_place": {"GiB_s": round(B * plen / t_pg / 2**30, 2), "ms": round(t_pg * 1e3, 2),
                                              "rows_copied": rows},
