@@ -86,9 +86,9 @@ def aggregate_gib_s(world: int, per_rank: int, payload_len: int, elapsed: float,
     return world * per_rank * payload_len / (elapsed / steps) / 2**30
 
 
-# Profile tags, newest first: round 5's closing profiles (r05: configs 3, 4
+# Profile tags, newest first: round 6's closing profiles (r06: configs 3, 4
 # and 2), then round 4's (r04g: configs 3 and 4; r04: config 2).
-ROUND_TAGS = ("r05", "r04g", "r04")
+ROUND_TAGS = ("r06", "r05", "r04g", "r04")
 
 
 def load_traffic(config: int):

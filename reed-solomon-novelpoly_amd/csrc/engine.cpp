@@ -1202,12 +1202,10 @@ int np_reconstruct_batch_host(np_ctx* c, const np_code_params* p, const uint8_t*
   //  - dma2d: the first `rows` rows of every payload by one 2-D DMA (pinned,
   //    unaligned rows).
   // Pinned callers: NP_HOST_ROWS=pack / gather picks (read per call; default
-  // below, measured in DESIGN.md §6).
+  // below, measured in DESIGN.md §4.7).
   enum class Rows { Pack, Gather, Dma2d };
   const bool aligned = ((reinterpret_cast<uintptr_t>(shards) | bstride | shard_len) & 3) == 0;
   const char* hr = std::getenv("NP_HOST_ROWS");
-  const bool pinned_pack = hr ? std::strcmp(hr, "pack") == 0 : kPinnedPack;
-  const Rows mode = st_in || pinned_pack ? Rows::Pack : aligned ? Rows::Gather : Rows::Dma2d;
   const int npipe = pipe_slots();
   hipError_t e = pipe_init(c, npipe);
   // Sub-batches of about kPipeMovedBytes of PCIe traffic (the present rows in,
@@ -1219,6 +1217,11 @@ int np_reconstruct_batch_host(np_ctx* c, const np_code_params* p, const uint8_t*
   const size_t per = moved * shard_len / batch + olen;
   size_t sb = std::min(batch, std::max<size_t>(1, (kPipeMovedBytes + per - 1) / per));
   if (const char* v = std::getenv("NP_PIPE_SB")) sb = std::min(batch, std::max<size_t>(1, std::strtoul(v, nullptr, 10)));
+  // Pinned callers: packed when the call pipelines several sub-batches; a call
+  // of one sub-batch has nothing to overlap the packing with, so its aligned
+  // rows go by the gather (one payload at config 3: 0.20 ms against 0.29).
+  const bool pinned_pack = hr ? std::strcmp(hr, "pack") == 0 : kPinnedPack && (batch > sb || !aligned);
+  const Rows mode = st_in || pinned_pack ? Rows::Pack : aligned ? Rows::Gather : Rows::Dma2d;
   const size_t slot_in = (sb - 1) * dstride + in_bytes;
   const size_t nblk = (rows + 63) / 64;  // packing tasks per payload: 64 rows each
   const size_t pack_cap = (sb * rows * 8 + 255) / 256 * 256 + sb * rows * shard_len;  // offsets, then rows

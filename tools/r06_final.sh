@@ -1,14 +1,14 @@
 #!/bin/bash
-# Round-5 closing run on the GPU box: the GPU test suite, the records
+# Round-6 closing run on the GPU box: the GPU test suite, the records
 # (tools/records.sh: BASELINE lines with CPU baselines, config-1 CPU record,
 # shapes), the config-3 kernel trace and PMC passes (tools/profile_round.sh),
 # and the PCIe-inclusive rates (tools/e2e_bench.py).  Usage:
-#   bash tools/r05_final.sh [RECORDS_TAG [PROFILE_TAG [PART]]]   (defaults r05f, r05,
+#   bash tools/r06_final.sh [RECORDS_TAG [PROFILE_TAG [PART]]]   (defaults r06f, r06,
 #   all; PART a = tests and records, b = profiles and PCIe rates)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-RT=${1:-r05f}
-PT=${2:-r05}
+RT=${1:-r06f}
+PT=${2:-r06}
 PART=${3:-ab}
 D=gpurun_out/$RT
 mkdir -p $D
