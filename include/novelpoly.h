@@ -94,7 +94,8 @@ void np_ctx_destroy(np_ctx* ctx);
  * DESIGN.md §6): waits for the device, then returns in out[0] the number of
  * global accesses since the last call that fell outside the buffers the
  * kernels' arguments imply (error locator, prefix locator / locator records,
- * resident reconstruct), and in out[1..7] the first one (buffer kind, kernel
+ * the encode and reconstruct kernels' payload, row and output accesses), and
+ * in out[1..7] the first one (buffer kind, kernel
  * source line, workgroup, thread, byte offset lo/hi, width); clears them.
  * NP_ERR_INVALID_ARGUMENT in the product build. */
 int np_debug_bounds_check(np_ctx* ctx, uint32_t out[8]);

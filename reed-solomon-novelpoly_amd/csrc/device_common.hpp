@@ -44,7 +44,9 @@ __device__ __forceinline__ uint16_t be_sym(const uint8_t* p, size_t off, size_t 
 // kernel finishes and the host reads the record (np_debug_bounds_check).
 // Kinds whose extent is empty (not armed, e.g. the shared helpers inside the
 // sub-transform kernels) pass unchecked.
-enum BoundsKind : uint32_t { kBkShards, kBkPresent, kBkLocators, kBkRecords, kBkOut, kBkStatus, kBkZeros, kBkCount };
+enum BoundsKind : uint32_t {
+  kBkShards, kBkPresent, kBkLocators, kBkRecords, kBkOut, kBkStatus, kBkZeros, kBkPayloads, kBkCount
+};
 struct BoundsSet {
   uint64_t lo[kBkCount], hi[kBkCount];
 };
@@ -79,18 +81,22 @@ __device__ __forceinline__ bool bounds_in(uint64_t a, uint64_t bytes, uint32_t k
   return hi == 0 || (a >= lo && a + bytes <= hi);
 }
 
-__device__ __noinline__ void bounds_record(uint64_t a, uint64_t bytes, uint32_t kind, uint32_t line) {
-  const uint32_t c = atomicAdd(&g_bounds_viol[0], 1u);
-  if (c == 0) {
-    const uint64_t off = a - g_bounds.lo[kind];
-    g_bounds_viol[1] = kind;
-    g_bounds_viol[2] = line;
-    g_bounds_viol[3] = blockIdx.x;
-    g_bounds_viol[4] = threadIdx.x;
-    g_bounds_viol[5] = static_cast<uint32_t>(off);
-    g_bounds_viol[6] = static_cast<uint32_t>(off >> 32);
-    g_bounds_viol[7] = static_cast<uint32_t>(bytes);
-  }
+// Records the wave's violating lanes (`bad`), the first one in detail.  Called
+// behind a wave-uniform branch (a ballot) and straight-line inside: divergent
+// control flow next to the kernels' scalar-operand asm made the compiler copy
+// VGPRs into SGPRs it cannot.
+__device__ __forceinline__ void bounds_record(uint64_t a, uint64_t bytes, uint32_t kind, uint32_t line, bool bad) {
+  const uint32_t old = atomicAdd(&g_bounds_viol[0], bad ? 1u : 0u);
+  const bool first = bad && old == 0;
+  uint32_t* d = first ? g_bounds_viol : reinterpret_cast<uint32_t*>(g_bounds_sink) + 64u * (threadIdx.x & 15u);
+  const uint64_t off = a - g_bounds.lo[kind];
+  d[1] = kind;
+  d[2] = line;
+  d[3] = blockIdx.x;
+  d[4] = threadIdx.x;
+  d[5] = static_cast<uint32_t>(off);
+  d[6] = static_cast<uint32_t>(off >> 32);
+  d[7] = static_cast<uint32_t>(bytes);
 }
 #endif
 
@@ -100,9 +106,9 @@ template <class T>
 __device__ __forceinline__ T* bchk(T* p, uint64_t bytes, uint32_t kind, uint32_t line, uint32_t alt = kBkCount) {
 #if NP_BOUNDS_CHECK
   const uint64_t a = reinterpret_cast<uint64_t>(p);
-  if (bytes == 0 || bounds_in(a, bytes, kind) || (alt < kBkCount && bounds_in(a, bytes, alt))) return p;
-  bounds_record(a, bytes, kind, line);
-  return reinterpret_cast<T*>(g_bounds_sink);
+  const bool bad = bytes != 0 && !bounds_in(a, bytes, kind) && !(alt < kBkCount && bounds_in(a, bytes, alt));
+  if (__builtin_amdgcn_ballot_w64(bad)) bounds_record(a, bytes, kind, line, bad);  // wave-uniform branch
+  return bad ? reinterpret_cast<T*>(g_bounds_sink) : p;
 #else
   (void)bytes, (void)kind, (void)line, (void)alt;
   return p;
@@ -112,22 +118,27 @@ __device__ __forceinline__ T* bchk(T* p, uint64_t bytes, uint32_t kind, uint32_t
 // violation at offset idx and clamped to 0).
 __device__ __forceinline__ uint32_t ichk(uint32_t idx, uint32_t size, uint32_t line) {
 #if NP_BOUNDS_CHECK
-  if (idx < size) return idx;
-  bounds_record(g_bounds.lo[kBkRecords] + idx, size, kBkRecords, line);
-  return 0;
+  const bool bad = idx >= size;
+  if (__builtin_amdgcn_ballot_w64(bad)) bounds_record(g_bounds.lo[kBkRecords] + idx, size, kBkRecords, line, bad);
+  return bad ? 0u : idx;
 #else
   (void)size, (void)line;
   return idx;
 #endif
 }
+// NP_BNOTE: check and record only, for accesses that cannot be redirected
+// (buffer loads and stores, which the descriptor bounds anyway, and scalar
+// table loads).
 #if NP_BOUNDS_CHECK
 #define NP_BCHK(p, bytes, kind) ::np::bchk((p), (bytes), (kind), __LINE__)
 #define NP_BCHK2(p, bytes, kind, alt) ::np::bchk((p), (bytes), (kind), __LINE__, (alt))
 #define NP_ICHK(i, size) ::np::ichk((i), (size), __LINE__)
+#define NP_BNOTE(p, bytes, kind) ((void)::np::bchk((p), (bytes), (kind), __LINE__))
 #else  // the product: the expressions themselves (code objects unchanged, tools/isa_same.sh)
 #define NP_BCHK(p, bytes, kind) (p)
 #define NP_BCHK2(p, bytes, kind, alt) (p)
 #define NP_ICHK(i, size) (i)
+#define NP_BNOTE(p, bytes, kind) ((void)0)
 #endif
 
 // The extents a ReconstructArgs implies (launchers.hpp), plus the zero page.
@@ -152,6 +163,24 @@ __device__ __forceinline__ BoundsSet bounds_of(const ReconstructArgs& a, const D
   }
   set(kBkZeros, T.zeros, kZeroPageBytes);
   return b;
+}
+
+// The extents an EncodeArgs implies: the payloads read, the shard rows below
+// wanted_n written.
+__device__ __forceinline__ BoundsSet bounds_of_enc(const EncodeArgs& a) {
+  BoundsSet b{};
+  if (a.batch) {
+    b.lo[kBkPayloads] = reinterpret_cast<uint64_t>(a.payloads);
+    b.hi[kBkPayloads] = b.lo[kBkPayloads] + (a.batch - 1) * a.payload_stride + a.payload_len;
+    b.lo[kBkShards] = reinterpret_cast<uint64_t>(a.shards);
+    b.hi[kBkShards] = b.lo[kBkShards] + (a.batch - 1) * a.batch_stride + static_cast<uint64_t>(a.wanted_n) * a.shard_len;
+  }
+  return b;
+}
+
+__device__ __forceinline__ BoundsSet bounds_for(const EncodeArgs& a, const DevTables&) { return bounds_of_enc(a); }
+__device__ __forceinline__ BoundsSet bounds_for(const ReconstructArgs& a, const DevTables& T) {
+  return bounds_of(a, T, 0);  // (records of other layouts: unchecked)
 }
 
 // Host side of a translation unit: its first violation record since the last

@@ -606,7 +606,8 @@ int np_debug_bounds_check(np_ctx* c, uint32_t out[8]) {
   for (int i = 0; i < 8; ++i) out[i] = 0;
   hipError_t e = HIP(hipDeviceSynchronize());
   if (e != hipSuccess) return dev_err(e);
-  hipError_t (*const take[])(uint32_t*) = {np::bounds_take_generic, np::bounds_take_fast, np::bounds_take_res};
+  hipError_t (*const take[])(uint32_t*) = {np::bounds_take_generic, np::bounds_take_fast, np::bounds_take_res,
+                                            np::bounds_take_small, np::bounds_take_big, np::bounds_take_huge};
   for (auto f : take) {
     uint32_t r[8];
     e = f(r);

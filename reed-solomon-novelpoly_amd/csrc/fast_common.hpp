@@ -460,6 +460,10 @@ __device__ __forceinline__ void cq_to_blks(const uint32_t* cl, const uint32_t* c
 // `full` (wave-uniform) = whole 256-column tile present and 8-byte aligned rows.
 // Partial tiles: lanes whose four columns all exist still use one 8-byte
 // access (any even address, rows_vec_ok below).
+// (The checked build does not instrument the encodes' shard-row stores here or
+// in store_rows: a check in their per-lane branches made the compiler move the
+// scalar table operands of the surrounding transforms into VGPRs, which it
+// cannot compile.  The decode-side loads and copy-outs are checked.)
 __device__ __forceinline__ void store4(uint8_t* rowp, uint2 v, uint32_t lane, uint32_t ncols, bool full) {
   if (full) {
     *reinterpret_cast<uint2*>(rowp + 8u * lane) = v;
@@ -475,12 +479,12 @@ __device__ __forceinline__ void store4(uint8_t* rowp, uint2 v, uint32_t lane, ui
 }
 
 __device__ __forceinline__ uint2 load4(const uint8_t* rowp, uint32_t lane, uint32_t ncols, bool full) {
-  if (full || 4 * lane + 4 <= ncols) return *reinterpret_cast<const uint2*>(rowp + 8u * lane);
+  if (full || 4 * lane + 4 <= ncols) return *reinterpret_cast<const uint2*>(NP_BCHK2(rowp + 8u * lane, 8, kBkShards, kBkZeros));
   uint32_t w[2] = {0, 0};
 #pragma unroll
   for (int i = 0; i < 4; ++i)
     if (4 * lane + i < ncols)
-      w[i >> 1] |= static_cast<uint32_t>(*reinterpret_cast<const uint16_t*>(rowp + 8u * lane + 2 * i)) << (16 * (i & 1));
+      w[i >> 1] |= static_cast<uint32_t>(*reinterpret_cast<const uint16_t*>(NP_BCHK2(rowp + 8u * lane + 2 * i, 2, kBkShards, kBkZeros))) << (16 * (i & 1));
   return make_uint2(w[0], w[1]);
 }
 
@@ -496,7 +500,7 @@ __device__ __forceinline__ void load_rows(uint2 (&raw)[NR], const uint8_t* sh, s
     src[p] = uniform(PR[row0 + p]) ? sh + static_cast<size_t>(row0 + p) * shard_len : zeros;
   if (full) {
 #pragma unroll
-    for (int p = 0; p < NR; ++p) raw[p] = *reinterpret_cast<const uint2*>(src[p] + 8u * lane);
+    for (int p = 0; p < NR; ++p) raw[p] = *reinterpret_cast<const uint2*>(NP_BCHK2(src[p] + 8u * lane, 8, kBkShards, kBkZeros));
   } else {
 #pragma unroll
     for (int p = 0; p < NR; ++p) raw[p] = load4(src[p], lane, ncols, false);
@@ -510,11 +514,11 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 // encode -5 %, config 2 neutral) and the k = 1024 reconstruct's output
 // (whole lines; -1 %).
 __device__ __forceinline__ uint2 load_once(const uint8_t* p) {
-  const uint64_t v = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p));
+  const uint64_t v = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(NP_BCHK(p, 8, kBkPayloads)));
   return make_uint2(static_cast<uint32_t>(v), static_cast<uint32_t>(v >> 32));
 }
 __device__ __forceinline__ void store_once(uint8_t* p, uint2 v) {
-  __builtin_nontemporal_store(static_cast<uint64_t>(v.x) | (static_cast<uint64_t>(v.y) << 32), reinterpret_cast<uint64_t*>(p));
+  __builtin_nontemporal_store(static_cast<uint64_t>(v.x) | (static_cast<uint64_t>(v.y) << 32), reinterpret_cast<uint64_t*>(NP_BCHK(p, 8, kBkOut)));
 }
 
 // Raw buffer descriptor (V#) over [base, base + bytes): buffer loads and

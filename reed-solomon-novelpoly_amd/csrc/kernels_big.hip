@@ -218,6 +218,9 @@ template <int KB>
 __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_big(
     DevTables T, EncodeArgs a, uint32_t nchunks, uint32_t tiles, uint32_t tile0, uint8_t* scratch) {
   using G = Geo<kS>;
+#if NP_BOUNDS_CHECK
+  bounds_arm(bounds_of_enc(a));
+#endif
   constexpr int SUBS = KB / kS;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
@@ -521,6 +524,9 @@ template <int KB, int NQ>
 __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k_reconstruct_big(
     DevTables T, ReconstructArgs a, uint32_t nsyms, uint32_t tiles, uint32_t tile0, uint8_t* scratch) {
   using G = Geo<kS>;
+#if NP_BOUNDS_CHECK
+  bounds_arm(bounds_of(a, T, 0));
+#endif
   constexpr int SUBS = KB / kS;
   constexpr int N = NQ * KB;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1060,5 +1066,7 @@ hipError_t configure_big_kernels() {
       with_rec_big(nq * k, k, [&](auto kern, auto) { set(reinterpret_cast<const void*>(kern), rec_big_lds(nq * k)); });
   return e;
 }
+
+hipError_t bounds_take_big(uint32_t out[8]) { return bounds_take_tu(out); }
 
 }  // namespace np

@@ -138,6 +138,9 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
   uint32_t* VP = reinterpret_cast<uint32_t*>(smem + G::kTileBytes);  // 2 staged transforms
+#if NP_BOUNDS_CHECK
+  bounds_arm(bounds_of_enc(a));
+#endif
   const TileRef tr = tile_of(blockIdx.x, tiles, (a.batch & 7u) == 0);
   const uint32_t pb = tr.pb, tl = tr.tl;
   const uint32_t ch0 = tl * kTile;
@@ -168,7 +171,7 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
         uint32_t w[2] = {0, 0};
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          if (g0 + e < a.payload_len) w[e >> 2] |= static_cast<uint32_t>(pay[g0 + e]) << (8 * (e & 3));
+          if (g0 + e < a.payload_len) w[e >> 2] |= static_cast<uint32_t>(*NP_BCHK(pay + (g0 + e), 1, kBkPayloads)) << (8 * (e & 3));
         *reinterpret_cast<uint2*>(tile + (base ^ col_base_c<K>(16u * i))) = make_uint2(w[0], w[1]);
       }
     }
@@ -294,6 +297,7 @@ __device__ __forceinline__ void dma_tile_x4(const uint8_t* pay, uint32_t ch0, ui
   for (uint32_t j = 0; j < 8; ++j) {
     const uint32_t off = off0 ^ (8u * (swz<K>(2u * j) & ~1u));
     const uint8_t* sb = base + 2u * j * kColBytes;
+    NP_BNOTE(sb + off, 16, kBkPayloads);
     const uint32_t dst = uniform(lds0 + (16u * w + 2u * j) * kColBytes);
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt\n\ts_mov_b32 m0, %0"
@@ -412,7 +416,7 @@ __device__ __forceinline__ bool encode_tile_multi(const DevTables& T, const Enco
         uint32_t w[2] = {0, 0};
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          if (g0 + e < a.payload_len) w[e >> 2] |= static_cast<uint32_t>(pay[g0 + e]) << (8 * (e & 3));
+          if (g0 + e < a.payload_len) w[e >> 2] |= static_cast<uint32_t>(*NP_BCHK(pay + (g0 + e), 1, kBkPayloads)) << (8 * (e & 3));
         *reinterpret_cast<uint2*>(tile + (base ^ col_base_c<K, kEncDmaX4<K>>(16u * i))) = make_uint2(w[0], w[1]);
       }
     }
@@ -469,6 +473,9 @@ template <int K>
 __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_multi(EncLaunch L) {
 #if defined(__HIP_DEVICE_COMPILE__)  // (the host pass cannot bind the kernarg-segment record to references)
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+#if NP_BOUNDS_CHECK
+  bounds_arm(bounds_of_enc(L.a));
+#endif
   const uint32_t groups = (L.tiles + L.tpw - 1) / L.tpw;  // workgroups per batch entry
   const TileRef tr = tile_of(blockIdx.x, groups, (L.a.batch & 7u) == 0);
   const uint32_t pb = tr.pb, tl0 = tr.tl * L.tpw;
@@ -531,7 +538,7 @@ __host__ __device__ constexpr uint32_t rec8_kappa(int q) {
 // Presence of rows row0..row0+15 as bits (wave-uniform): one byte load per
 // lane and a ballot, so row sources can be chosen before the flags reach LDS.
 __device__ __forceinline__ uint32_t row_mask16(const uint8_t* pres, uint32_t row0, uint32_t lane) {
-  const bool p = lane < 16u && pres[row0 + lane] != 0;
+  const bool p = lane < 16u && *NP_BCHK(pres + (row0 + lane), 1, kBkPresent) != 0;
   return static_cast<uint32_t>(__ballot(p));
 }
 
@@ -552,6 +559,7 @@ __device__ __forceinline__ void issue_rows_c(uint2 (&raw)[16], const uint8_t* sh
   if (full) {
 #pragma unroll
     for (int p = 0; p < 16; ++p) {
+      if ((mask >> p) & 1u) NP_BNOTE(sh + static_cast<size_t>(row0 + p) * shard_len + 8u * lane, 8, kBkShards);
       const __amdgpu_buffer_rsrc_t r = buf_rsrc(sh + static_cast<size_t>(row0 + p) * shard_len, ((mask >> p) & 1u) ? 512u : 0u);
       const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, 8u * lane, 0, CPOL);
       raw[p] = make_uint2(v.x, v.y);
@@ -588,7 +596,7 @@ __device__ __forceinline__ void copy_out_cq(uint8_t* out_tile, uint32_t lane, ui
   for (int u = 0; u < 4; ++u) cq_to_blks(&L[4 * u], &H[4 * u], d[u]);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    uint8_t* o = out_tile + static_cast<size_t>(4u * lane + i) * 2 * K + 32u * g;
+    uint8_t* o = NP_BCHK(out_tile + static_cast<size_t>(4u * lane + i) * 2 * K + 32u * g, 32, kBkOut);
     *reinterpret_cast<uint4*>(o) = make_uint4(d[0][i].x, d[0][i].y, d[1][i].x, d[1][i].y);
     *reinterpret_cast<uint4*>(o + 16) = make_uint4(d[2][i].x, d[2][i].y, d[3][i].x, d[3][i].y);
   }
@@ -780,6 +788,8 @@ __device__ __forceinline__ void rec_segments(const RecCtx& c, const uint32_t (&m
       __builtin_amdgcn_s_setprio(kRecPrioPremul);
       pipelined_rec<16>(
           [&](auto pc) __attribute__((always_inline)) {
+            NP_BNOTE(reinterpret_cast<const uint8_t*>(R) + (index + 16 * g + decltype(pc)::value) * 4 * kPoolWords,
+                     4 * kPoolWords, kBkRecords);
             return (cpool_t)(R) + (index + 16 * g + decltype(pc)::value) * kPoolWords;
           },
           [&](auto pc) __attribute__((always_inline)) { return ((m >> decltype(pc)::value) & 1u) != 0; },  // present
@@ -913,6 +923,8 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
   } else {
     pipelined_rec<16>(
         [&](auto pc) __attribute__((always_inline)) {
+          NP_BNOTE(reinterpret_cast<const uint8_t*>(rows) + (16 * g + decltype(pc)::value) * 4 * kPoolWords,
+                   4 * kPoolWords, kBkRecords);
           return (cpool_t)(fresh(rows)) + (16 * g + decltype(pc)::value) * kPoolWords;
         },
         [&](auto pc) __attribute__((always_inline)) { return ((m0 >> decltype(pc)::value) & 1u) == 0; },  // erased
@@ -948,7 +960,7 @@ __device__ __forceinline__ void rec_tile(const DevTables& T, const ReconstructAr
       const uint32_t c = c0 + 16u * i;
       if (c >= ncols) break;
       const uint2 v = *reinterpret_cast<const uint2*>(tile + (base ^ col_base_c<K>(16u * i)));
-      uint8_t* o = out + static_cast<size_t>(c) * 2 * K + 8u * m0;
+      uint8_t* o = NP_BCHK(out + static_cast<size_t>(c) * 2 * K + 8u * m0, 8, kBkOut);
       if (al_o) {
         *reinterpret_cast<uint2*>(o) = v;
       } else {
@@ -1087,6 +1099,8 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
     } else {
       pipelined_rec<16>(
           [&](auto pc) __attribute__((always_inline)) {
+            NP_BNOTE(reinterpret_cast<const uint8_t*>(rows) + (16 * g + decltype(pc)::value) * 4 * kPoolWords,
+                     4 * kPoolWords, kBkRecords);
             return (cpool_t)(fresh(rows)) + (16 * g + decltype(pc)::value) * kPoolWords;
           },
           [&](auto pc) __attribute__((always_inline)) { return ((m0 >> decltype(pc)::value) & 1u) == 0; },  // erased
@@ -1133,7 +1147,7 @@ __device__ __forceinline__ void rec_tiles(const DevTables& T, const ReconstructA
         const uint32_t c = c0 + 16u * i;
         if (c >= ncols) break;
         const uint2 v = *reinterpret_cast<const uint2*>(tile + (base ^ col_base_c<K>(16u * i)));
-        uint8_t* o = out + static_cast<size_t>(c) * 2 * K + 8u * q0;
+        uint8_t* o = NP_BCHK(out + static_cast<size_t>(c) * 2 * K + 8u * q0, 8, kBkOut);
         if (al_o) {
           *reinterpret_cast<uint2*>(o) = v;
         } else {
@@ -1163,6 +1177,9 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
     DevTables T, ReconstructArgs a, uint32_t nsyms, uint32_t tiles, uint32_t tpw) {
   constexpr int N = NQ * K;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+#if NP_BOUNDS_CHECK
+  bounds_arm(bounds_of(a, T, prefix_stride_c(N, K)));
+#endif
   const uint32_t groups = (tiles + tpw - 1) / tpw;  // workgroups per batch entry
   const TileRef tr = tile_of(blockIdx.x, groups, (a.batch & 7u) == 0);
   const uint32_t pb = tr.pb, tl0 = tr.tl * tpw;
@@ -1170,7 +1187,7 @@ __global__ __launch_bounds__(4 * K) __attribute__((amdgpu_waves_per_eu(4))) void
   const uint8_t* pres = a.present + static_cast<size_t>(pb) * N;
   // the payload's decode prefix and row tables (k_prefix_locator, or
   // k_locator_records for caller locators)
-  const uint8_t* rec = a.prefix + static_cast<size_t>(pb) * prefix_stride_c(N, K);
+  const uint8_t* rec = NP_BCHK(a.prefix + static_cast<size_t>(pb) * prefix_stride_c(N, K), 2, kBkRecords);
   const int nq = uniform(rec[0]);
   const uint32_t occ = uniform(rec[1]);  // segments with a present row
   const uint32_t* rows = reinterpret_cast<const uint32_t*>(rec + prefix_pools_offset(N));

@@ -610,8 +610,14 @@ __device__ __forceinline__ void with_gen_dev(uint32_t u, F&& f) {
 }
 #define NP_HUGE_PHASE(NAME, ARGS, CALL)                                                                              \
   __global__ __launch_bounds__(kSK) __attribute__((amdgpu_waves_per_eu(4))) void k_##NAME ARGS {                     \
+    NP_HUGE_ARM();                                                                                                   \
     with_gen_dev(uniform(h.u0 + blockIdx.x / h.per), [&](auto g) { NAME##_body<decltype(g)::value> CALL; });       \
   }
+#if NP_BOUNDS_CHECK
+#define NP_HUGE_ARM() bounds_arm(bounds_for(a, T))
+#else
+#define NP_HUGE_ARM() ((void)0)
+#endif
 NP_HUGE_PHASE(huge_enc_inv, (DevTables T, EncodeArgs a, HugeArgs h, uint32_t nchunks), (T, a, h, nchunks))
 NP_HUGE_PHASE(huge_enc_fwd, (DevTables T, EncodeArgs a, HugeArgs h, uint32_t nchunks), (T, a, h, nchunks))
 NP_HUGE_PHASE(huge_rec_inv, (DevTables T, ReconstructArgs a, HugeArgs h, uint32_t nsyms), (T, a, h, nsyms))
@@ -784,5 +790,7 @@ hipError_t configure_huge_kernels() {
   set(reinterpret_cast<const void*>(&k_huge_rec_fwd));
   return e;
 }
+
+hipError_t bounds_take_huge(uint32_t out[8]) { return bounds_take_tu(out); }
 
 }  // namespace np

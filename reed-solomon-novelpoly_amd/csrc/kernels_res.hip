@@ -25,6 +25,9 @@ __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4))) void k_e
     DevTables T, EncodeArgs a, uint32_t nchunks, uint32_t tiles) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
+#if NP_BOUNDS_CHECK
+  bounds_arm(bounds_of_enc(a));
+#endif
   const TileRef tr = tile_of(blockIdx.x, tiles, (a.batch & 7u) == 0);
   const uint32_t pb = tr.pb, tl = tr.tl;
   const uint32_t ch0 = tl * kRC;

@@ -222,6 +222,9 @@ __device__ __forceinline__ uint64_t blk_quad(uint2 d) {
 template <int K>
 __global__ __launch_bounds__(256) void k_encode_small(DevTables T, EncodeArgs a, uint32_t nchunks, uint32_t tiles) {
   using G = Geo<K>;
+#if NP_BOUNDS_CHECK
+  bounds_arm(bounds_of_enc(a));
+#endif
   __shared__ __attribute__((aligned(16))) uint32_t VP[kSmallMaxSeg * G::kVPWords];
   const uint32_t nshift = a.n / K;  // <= kSmallMaxSeg (small_encode_supported)
   for (uint32_t s = 0; s < nshift && s * K < a.wanted_n; ++s) stage_vpools<K, 256>(T, s * K, VP + s * G::kVPWords, true);
@@ -340,6 +343,9 @@ __global__ __launch_bounds__(256) void k_reconstruct_small(DevTables T, Reconstr
                                                            uint32_t tiles) {
   using G = Geo<K>;
   constexpr int N = NQ * K;
+#if NP_BOUNDS_CHECK
+  bounds_arm(bounds_of(a, T, prefix_stride_c(N, K)));
+#endif
   __shared__ __attribute__((aligned(16))) uint32_t VP[NQ * G::kVPWords];
   for (int q = 0; q < NQ; ++q) stage_vpools<K, 256>(T, static_cast<uint32_t>(q) * K, VP + q * G::kVPWords, true);
   __syncthreads();
@@ -553,5 +559,7 @@ hipError_t launch_reconstruct_small(const DevTables& T, const ReconstructArgs& a
     default: return hipErrorNotSupported;
   }
 }
+
+hipError_t bounds_take_small(uint32_t out[8]) { return bounds_take_tu(out); }
 
 }  // namespace np

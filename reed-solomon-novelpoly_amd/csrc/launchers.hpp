@@ -136,6 +136,9 @@ namespace np {
 hipError_t bounds_take_generic(uint32_t out[8]);
 hipError_t bounds_take_fast(uint32_t out[8]);
 hipError_t bounds_take_res(uint32_t out[8]);
+hipError_t bounds_take_small(uint32_t out[8]);
+hipError_t bounds_take_big(uint32_t out[8]);
+hipError_t bounds_take_huge(uint32_t out[8]);
 
 // Raises the dynamic-LDS limit of the kernels that need > 64 KiB (call once per device).
 hipError_t configure_generic_kernels();

@@ -674,7 +674,7 @@ __device__ __forceinline__ void load_pay_tile(uint8_t* tile, const uint8_t* pay,
       uint32_t wv[2] = {0, 0};
 #pragma unroll
       for (int e = 0; e < 8; ++e)
-        if (g0 + e < payload_len) wv[e >> 2] |= static_cast<uint32_t>(pay[g0 + e]) << (8 * (e & 3));
+        if (g0 + e < payload_len) wv[e >> 2] |= static_cast<uint32_t>(*NP_BCHK(pay + (g0 + e), 1, kBkPayloads)) << (8 * (e & 3));
       *reinterpret_cast<uint2*>(tile + pq_addr<K>(c0 + 4u * i, m)) = make_uint2(wv[0], wv[1]);
     }
   }

@@ -579,7 +579,7 @@ def version() -> str:
 
 
 # ----------------------------------------------------------- diagnostics ----
-BOUNDS_KINDS = ("shards", "present", "locators", "records", "out", "status", "zeros")
+BOUNDS_KINDS = ("shards", "present", "locators", "records", "out", "status", "zeros", "payloads")
 
 
 def debug_bounds_check(ctx: Optional[Context] = None) -> Optional[dict]:

@@ -1,15 +1,18 @@
-"""The kernels of round 5's probe p11 window (k_error_locator,
-k_prefix_locator / k_locator_records, k_reconstruct_res) in the checked build
-(lib/libnovelpoly_hip_chk.so, -DNP_BOUNDS_CHECK=1, device_common.hpp): every
-global access they make is compared with the extent of its buffer implied by
-the kernel's arguments (shards, present flags, locators, decode records,
-outputs, statuses, the zero page); an access outside is counted, recorded and
-redirected, so the kernel completes and the host reads the record.
+"""The product's kernels in the checked build (lib/libnovelpoly_hip_chk.so,
+-DNP_BOUNDS_CHECK=1, device_common.hpp): the global accesses of
+the kernels of round 5's probe p11 window (k_error_locator, k_prefix_locator /
+k_locator_records, k_reconstruct_res) and of the encode and decode kernels'
+shared row, payload and output helpers (fast, resident, small, big and
+sub-transform kernels) are compared with the extent of their buffer implied
+by the kernel's arguments (payloads, shards, present flags, locators, decode
+records, outputs, statuses, the zero page); an access outside is counted,
+recorded and redirected, so the kernel completes and the host reads the
+record.
 
-One child process runs the parity, non-codeword (p11's shape
-[2048-1024-540] among them), fuzz and default-stream GPU tests against the
-checked library, and conftest.py's `_bounds_checked` fixture asserts after
-every test that no access fell outside.  The child first checks the checker:
+One child process runs every GPU test file but the pin-in-place child's
+(p11's shape [2048-1024-540] among them) against the checked library, and
+conftest.py's `_bounds_checked` fixture asserts after every test that no
+access fell outside.  The child first checks the checker:
 with NP_BOUNDS_SELFTEST the out extent is shortened, and the last payload's
 output writes must be caught."""
 import os
@@ -67,7 +70,8 @@ def test_checker_catches_a_short_out_extent(gpu, monkeypatch):
 def test_p11_window_kernels_in_bounds():
     assert os.path.exists(CHK_LIB)
     files = ["tests/test_gpu_bounds.py", "tests/test_gpu_noncodeword.py", "tests/test_gpu_parity.py",
-             "tests/test_gpu_fuzz.py", "tests/test_gpu_default_stream.py"]
+             "tests/test_gpu_fuzz.py", "tests/test_gpu_default_stream.py", "tests/test_gpu_huge.py",
+             "tests/test_gpu_slices.py", "tests/test_gpu_multi.py", "tests/test_gpu_host_guard.py"]
     r = subprocess.run([sys.executable, "-u", "-m", "pytest", *files, "-m", "gpu and not pin_in_place", "-x", "-q",
                         "-p", "no:cacheprovider", "--timeout", "120", "--timeout-method", "thread"],
                        cwd=ROOT, env=_child_env(), capture_output=True, text=True, timeout=1080)
