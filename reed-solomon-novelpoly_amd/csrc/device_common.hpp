@@ -42,8 +42,12 @@ __device__ __forceinline__ uint16_t be_sym(const uint8_t* p, size_t off, size_t 
 // address outside its buffer is counted, the first one recorded (kind, line,
 // workgroup, thread, offset, bytes), and redirected to a sink, so that the
 // kernel finishes and the host reads the record (np_debug_bounds_check).
-// Kinds whose extent is empty (not armed, e.g. the shared helpers inside the
-// sub-transform kernels) pass unchecked.
+// The record is one per code object and device, so checked runs launch one
+// kernel at a time (tests/test_gpu_bounds.py: one pipeline stream, no
+// concurrent contexts).  Kinds whose extent is empty pass unchecked.  Every kernel of an instrumented
+// translation unit arms (or clears) the set at entry, so that no kernel is
+// checked against the extents of an earlier launch (round 6: k_big_records
+// was, and flagged its own present flags against another launch's batch).
 enum BoundsKind : uint32_t {
   kBkShards, kBkPresent, kBkLocators, kBkRecords, kBkOut, kBkStatus, kBkZeros, kBkPayloads, kBkCount
 };

@@ -850,6 +850,9 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
 // the record (big_rows_global) instead of through LDS.
 template <int K, int N>
 __global__ __launch_bounds__(256) void k_big_records(DevTables T, ReconstructArgs a, uint8_t* out) {
+#if NP_BOUNDS_CHECK
+  bounds_arm(bounds_of(a, T, 0));  // (E and PR may live in LDS here: records unchecked)
+#endif
   constexpr bool RG = big_rows_global(N);
   __shared__ uint32_t W[N];
   __shared__ __attribute__((aligned(16))) uint16_t El[RG ? 8 : N];

@@ -232,6 +232,9 @@ __device__ __forceinline__ void huge_enc_inv_body(
 template <int M>
 __global__ __launch_bounds__(256) void k_huge_enc_top(DevTables T, HugeArgs h, uint32_t nshift, uint32_t wanted_n,
                                                       size_t units) {
+#if NP_BOUNDS_CHECK
+  bounds_arm(BoundsSet{});  // every kernel of an instrumented unit arms its extents (none here)
+#endif
   const size_t gid = static_cast<size_t>(blockIdx.x) * 256u + threadIdx.x;
   if (gid >= units) return;
   uint8_t* base = h.scr + (gid >> 14) * h.slots * kSlotBytes + (gid & 16383u) * 8u;
@@ -294,6 +297,9 @@ __device__ __forceinline__ void huge_enc_fwd_body(
 // each; n is a multiple of 1024), then one block sum.
 // Iteration i covers block i (rows 1024 i .. + 1023): its occupancy bit.
 __global__ __launch_bounds__(256) void k_huge_records(ReconstructArgs a, uint8_t* mode, uint64_t* occ) {
+#if NP_BOUNDS_CHECK
+  bounds_arm(BoundsSet{});
+#endif
   __shared__ int part[2][4];
   const uint32_t pb = blockIdx.x;
   const uint8_t* pres = a.present + static_cast<size_t>(pb) * a.n;
@@ -433,6 +439,9 @@ __host__ __device__ constexpr uint32_t huge_kappa(int q) {
 
 template <int M, int NQ>
 __global__ __launch_bounds__(256) void k_huge_rec_top(DevTables T, HugeArgs h, size_t units) {
+#if NP_BOUNDS_CHECK
+  bounds_arm(BoundsSet{});
+#endif
   const size_t gid = static_cast<size_t>(blockIdx.x) * 256u + threadIdx.x;
   if (gid >= units) return;
   const size_t pt = gid >> 14;  // tile of the slice

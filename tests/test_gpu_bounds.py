@@ -9,8 +9,9 @@ records, outputs, statuses, the zero page); an access outside is counted,
 recorded and redirected, so the kernel completes and the host reads the
 record.
 
-One child process runs every GPU test file but the pin-in-place child's
-(p11's shape [2048-1024-540] among them) against the checked library, and
+One child process runs every GPU test file but the pin-in-place child's and
+the multi-context one (p11's shape [2048-1024-540] among them) against the
+checked library, one launch at a time, and
 conftest.py's `_bounds_checked` fixture asserts after every test that no
 access fell outside.  The child first checks the checker:
 with NP_BOUNDS_SELFTEST the out extent is shortened, and the last payload's
@@ -28,7 +29,11 @@ CHK_LIB = os.path.join(ROOT, "reed-solomon-novelpoly_amd", "lib", "libnovelpoly_
 
 
 def _child_env():
-    return dict(os.environ, NP_LIB_PATH=CHK_LIB, NP_BOUNDS_CHILD="1")
+    # The checked kernels keep their extents in one record per code object and
+    # device, so the child runs one launch at a time: the host pipeline on one
+    # stream (NP_PIPE_SLOTS=1), and no multi-context file (test_gpu_multi.py
+    # runs contexts from several threads at once).
+    return dict(os.environ, NP_LIB_PATH=CHK_LIB, NP_BOUNDS_CHILD="1", NP_PIPE_SLOTS="1")
 
 
 def test_checked_library_built():
@@ -71,7 +76,7 @@ def test_p11_window_kernels_in_bounds():
     assert os.path.exists(CHK_LIB)
     files = ["tests/test_gpu_bounds.py", "tests/test_gpu_noncodeword.py", "tests/test_gpu_parity.py",
              "tests/test_gpu_fuzz.py", "tests/test_gpu_default_stream.py", "tests/test_gpu_huge.py",
-             "tests/test_gpu_slices.py", "tests/test_gpu_multi.py", "tests/test_gpu_host_guard.py"]
+             "tests/test_gpu_slices.py", "tests/test_gpu_host_guard.py"]
     r = subprocess.run([sys.executable, "-u", "-m", "pytest", *files, "-m", "gpu and not pin_in_place", "-x", "-q",
                         "-p", "no:cacheprovider", "--timeout", "120", "--timeout-method", "thread"],
                        cwd=ROOT, env=_child_env(), capture_output=True, text=True, timeout=1080)
