@@ -40,6 +40,15 @@ def test_checked_library_built():
     assert os.path.exists(CHK_LIB), "run `make -C reed-solomon-novelpoly_amd chk` (__graft_entry__.build does)"
 
 
+@pytest.mark.skipif(bool(os.environ.get("NP_BOUNDS_CHILD")), reason="the product library's answer")
+def test_product_library_has_no_checks(gpu):
+    """The product library reports that it is not a checked build (its code
+    objects carry no checks: the macros are the plain expressions)."""
+    import novelpoly_amd as npa
+
+    assert npa.debug_bounds_check(gpu) is None
+
+
 @pytest.mark.skipif(not os.environ.get("NP_BOUNDS_CHILD"), reason="runs in the checked child process")
 def test_checker_catches_a_short_out_extent(gpu, monkeypatch):
     """NP_BOUNDS_SELFTEST=64: the kernels see an out extent 64 bytes short, so
