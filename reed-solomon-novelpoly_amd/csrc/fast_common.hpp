@@ -1220,6 +1220,103 @@ __device__ __forceinline__ void hi_read_q(const uint8_t* tile, uint32_t w, uint3
 // is all a multiplier needs (EXP[65535] == EXP[0]).  Leaves E[v] = EXP[loc] for
 // present rows and EXP[65535 - loc] for erased rows (the postmultiplier,
 // inc_reconstruct.rs:108-112), and PR[v] = present flag.  W: N dwords of scratch.
+// Walsh-Hadamard transform of W[0, N) in LDS, two levels per pass (each
+// thread takes groups of 4 elements: levels b and b + 1 in registers), so a
+// size-1024 transform has 5 barriers instead of 10.  MOD = false: exact in
+// int32 (the 0/1 erasure vector, |x| <= N); MOD = true: mod 65535 with
+// canonical residues in [0, 65534], so the level order does not matter (only
+// the residue enters a multiplier: EXP[65535] == EXP[0]).
+template <bool MOD>
+__device__ __forceinline__ void wht_bfly(uint32_t& x, uint32_t& y) {
+  if constexpr (MOD) {
+    uint32_t s = x + y, d = x + 65535u - y;
+    s -= s >= 65535u ? 65535u : 0u;
+    d -= d >= 65535u ? 65535u : 0u;
+    x = s;
+    y = d;
+  } else {
+    const int32_t a = static_cast<int32_t>(x), b = static_cast<int32_t>(y);
+    x = static_cast<uint32_t>(a + b);
+    y = static_cast<uint32_t>(a - b);
+  }
+}
+template <int N, int NT, bool MOD>
+__device__ __forceinline__ void lds_wht(uint32_t* W) {
+  const uint32_t tid = threadIdx.x;
+  int b = 0;
+#pragma unroll 1
+  for (; (2 << b) < N; b += 2) {  // levels b, b + 1 (both below log2 N)
+    const uint32_t h = 1u << b;
+    for (uint32_t q = tid; q < N / 4; q += NT) {
+      const uint32_t i = ((q & ~(h - 1u)) << 2) | (q & (h - 1u));
+      uint32_t x0 = W[i], x1 = W[i + h], x2 = W[i + 2 * h], x3 = W[i + 3 * h];
+      wht_bfly<MOD>(x0, x1);
+      wht_bfly<MOD>(x2, x3);
+      wht_bfly<MOD>(x0, x2);
+      wht_bfly<MOD>(x1, x3);
+      W[i] = x0, W[i + h] = x1, W[i + 2 * h] = x2, W[i + 3 * h] = x3;
+    }
+    __syncthreads();
+  }
+  if ((1 << b) < N) {  // log2 N odd: the last level alone
+    const uint32_t h = 1u << b;
+    for (uint32_t q = tid; q < N / 2; q += NT) {
+      const uint32_t i = ((q & ~(h - 1u)) << 1) | (q & (h - 1u));
+      uint32_t x = W[i], y = W[i + h];
+      wht_bfly<MOD>(x, y);
+      W[i] = x, W[i + h] = y;
+    }
+    __syncthreads();
+  }
+}
+
+// The locator from the erasure indicator W[v] = (row v absent) and PR[v] (the
+// present flag), both in LDS and synchronised: see fused_locator.
+template <int N, int NT>
+__device__ __forceinline__ void fused_locator_core(const DevTables& T, uint32_t* W, uint16_t* E, const uint8_t* PR) {
+  const uint32_t tid = threadIdx.x;
+  lds_wht<N, NT, false>(W);  // integer WHT of the 0/1 erasure vector
+  const uint16_t* F = T.lw_fold + N;
+  for (uint32_t v = tid; v < N; v += NT) {
+    const int32_t x = static_cast<int32_t>(W[v]);  // |x| <= N
+    const uint32_t m = x < 0 ? static_cast<uint32_t>(x + 65535) : static_cast<uint32_t>(x);
+    W[v] = (m * static_cast<uint32_t>(F[v])) % 65535u;
+  }
+  __syncthreads();
+  lds_wht<N, NT, true>(W);  // WHT mod 65535
+  for (uint32_t v = tid; v < N; v += NT) *NP_BCHK(E + v, 2, kBkRecords) = T.exp[NP_ICHK(PR[v] ? W[v] : 65535u - W[v], 65536u)];
+}
+
+// The same, leaving each row's multiplier table (80 bytes: in_pools of
+// EXP[loc] for a present row, out_pools of EXP[65535 - loc] for an erased one)
+// at dst + 80 v instead of the u16 multipliers: the table loads follow the
+// multiplier in registers (k_prefix_locator's records; write_row_pools'
+// layout).
+template <int N, int NT>
+__device__ __forceinline__ void fused_locator_pools(const DevTables& T, uint32_t* W, const uint8_t* PR, uint8_t* dst) {
+  const uint32_t tid = threadIdx.x;
+  lds_wht<N, NT, false>(W);
+  const uint16_t* F = T.lw_fold + N;
+  for (uint32_t v = tid; v < N; v += NT) {
+    const int32_t x = static_cast<int32_t>(W[v]);
+    const uint32_t m = x < 0 ? static_cast<uint32_t>(x + 65535) : static_cast<uint32_t>(x);
+    W[v] = (m * static_cast<uint32_t>(F[v])) % 65535u;
+  }
+  __syncthreads();
+  lds_wht<N, NT, true>(W);
+  // (the row's table follows its multiplier in registers; batching four rows'
+  // table loads ahead of their stores measured 98 us per launch against 55.5,
+  // config 3)
+  for (uint32_t v = tid; v < N; v += NT) {
+    const bool p = PR[v] != 0;
+    const uint32_t e = T.exp[NP_ICHK(p ? W[v] : 65535u - W[v], 65536u)];
+    const uint4* src = reinterpret_cast<const uint4*>((p ? T.in_pools : T.out_pools) + static_cast<size_t>(e) * kPoolWords);
+    uint4* d = NP_BCHK(reinterpret_cast<uint4*>(dst + static_cast<size_t>(v) * 4 * kPoolWords), 4 * kPoolWords, kBkRecords);
+    const uint4 a0 = src[0], a1 = src[1], a2 = src[2], a3 = src[3], a4 = src[4];
+    d[0] = a0, d[1] = a1, d[2] = a2, d[3] = a3, d[4] = a4;
+  }
+}
+
 template <int N, int NT>
 __device__ __forceinline__ void fused_locator(const DevTables& T, const uint8_t* pres, uint32_t* W, uint16_t* E,
                                               uint8_t* PR) {
@@ -1230,35 +1327,7 @@ __device__ __forceinline__ void fused_locator(const DevTables& T, const uint8_t*
     W[v] = p ? 0u : 1u;
   }
   __syncthreads();
-  for (uint32_t h = 1; h < N; h <<= 1) {  // integer WHT of the 0/1 erasure vector
-    for (uint32_t b = tid; b < N / 2; b += NT) {
-      const uint32_t i = ((b & ~(h - 1u)) << 1) | (b & (h - 1u)), j = i + h;  // h is a power of 2
-      const int32_t x = static_cast<int32_t>(W[i]), y = static_cast<int32_t>(W[j]);
-      W[i] = static_cast<uint32_t>(x + y);
-      W[j] = static_cast<uint32_t>(x - y);
-    }
-    __syncthreads();
-  }
-  const uint16_t* F = T.lw_fold + N;
-  for (uint32_t v = tid; v < N; v += NT) {
-    const int32_t x = static_cast<int32_t>(W[v]);  // |x| <= N
-    const uint32_t m = x < 0 ? static_cast<uint32_t>(x + 65535) : static_cast<uint32_t>(x);
-    W[v] = (m * static_cast<uint32_t>(F[v])) % 65535u;
-  }
-  __syncthreads();
-  for (uint32_t h = 1; h < N; h <<= 1) {  // WHT mod 65535
-    for (uint32_t b = tid; b < N / 2; b += NT) {
-      const uint32_t i = ((b & ~(h - 1u)) << 1) | (b & (h - 1u)), j = i + h;  // h is a power of 2
-      const uint32_t x = W[i], y = W[j];
-      uint32_t s = x + y, d = x + 65535u - y;
-      s -= s >= 65535u ? 65535u : 0u;
-      d -= d >= 65535u ? 65535u : 0u;
-      W[i] = s;
-      W[j] = d;
-    }
-    __syncthreads();
-  }
-  for (uint32_t v = tid; v < N; v += NT) *NP_BCHK(E + v, 2, kBkRecords) = T.exp[NP_ICHK(PR[v] ? W[v] : 65535u - W[v], 65536u)];
+  fused_locator_core<N, NT>(T, W, E, PR);
 }
 
 }  // namespace

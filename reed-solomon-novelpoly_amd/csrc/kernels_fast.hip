@@ -1238,9 +1238,11 @@ __device__ __forceinline__ void write_row_pools(const DevTables& T, const uint16
 // One workgroup per payload: the decode prefix (rec_tile) and the erasure
 // locator folded to it (fused_locator, SURVEY F8: eval_error_polynomial
 // inc_reconstruct.rs:90-113 over [0, NQ' * K)), as row multipliers EXP[loc]
-// (present) / EXP[-loc] (erased).  Record: byte 0 = NQ' in {1, 2, NQ}, u16
-// multipliers from kPrefixHeader.  Computed once per payload instead of once
-// per column tile.
+// (present) / EXP[-loc] (erased).  Record: byte 0 = NQ' in {1, 2, NQ}, byte 1
+// the segment occupancy, the rows' 80-byte multiplier tables from
+// prefix_pools_offset (k_locator_records also leaves the u16 multipliers at
+// kPrefixHeader; the decodes read only the tables).  Computed once per payload
+// instead of once per column tile.
 // Present rows of payload pb in [0, K), [0, 2K) and [0, N) (256 threads).
 template <int K, int N>
 __device__ __forceinline__ void count_present(const uint8_t* pres, int& have1, int& have2, int& have) {
@@ -1295,23 +1297,46 @@ __global__ __launch_bounds__(256) void k_prefix_locator(DevTables T, Reconstruct
 #endif
   const uint8_t* pres = a.present + static_cast<size_t>(pb) * N;
   uint8_t* rec = out + static_cast<size_t>(pb) * prefix_stride_c(N, K);
-  uint16_t* E = reinterpret_cast<uint16_t*>(rec + kPrefixHeader);
-  int have1, have2, have;  // present rows in [0, K), [0, 2K), [0, N)
-  count_present<K, N>(pres, have1, have2, have);
+  // One pass over the present flags: PR, the erasure indicator W for the
+  // locator, the present rows in [0, K), [0, 2K), [0, N) and the segments
+  // holding one (was count_present + segment_occupancy + the locator's own
+  // load: 17 barriers fewer).
+  __shared__ uint32_t acc[4];  // have1, have2, have, occupancy
+  if (tid < 4) acc[tid] = 0;
+  __syncthreads();
+  {
+    uint32_t c1 = 0, c2 = 0, c = 0, occ = 0;
+    for (uint32_t v = tid; v < static_cast<uint32_t>(N); v += 256) {
+      const uint8_t p = *NP_BCHK(pres + v, 1, kBkPresent);
+      PR[v] = p;
+      W[v] = p ? 0u : 1u;
+      const uint32_t on = p ? 1u : 0u;
+      c += on;
+      c1 += v < static_cast<uint32_t>(K) ? on : 0u;
+      c2 += v < 2u * K ? on : 0u;
+      occ |= on << (v / K);
+    }
+    atomicAdd(&acc[0], c1);
+    atomicAdd(&acc[1], c2);
+    atomicAdd(&acc[2], c);
+    atomicOr(&acc[3], occ);
+  }
+  __syncthreads();
+  const int have1 = static_cast<int>(acc[0]), have2 = static_cast<int>(acc[1]), have = static_cast<int>(acc[2]);
   // All K systematic rows present: the output is those rows (the reference
   // copies received rows < k, inc_reconstruct.rs:46-50), exact for any input.
   // Otherwise the full decode from every present row, as the reference
   // (inc_reconstruct.rs:61-85); the 2K-row prefix only for trusted codewords.
   const int nq = !write_status(a, pb, have) ? 0 : have1 == K ? 1 : (a.trusted && NQ == 4 && have2 >= K) ? 2 : NQ;
-  const uint32_t occ = segment_occupancy<K, N>(pres);
-  if (tid == 0) *NP_BCHK(rec, 2, kBkRecords) = static_cast<uint8_t>(nq), *NP_BCHK(rec + 1, 1, kBkRecords) = static_cast<uint8_t>(occ);
+  if (tid == 0) *NP_BCHK(rec, 2, kBkRecords) = static_cast<uint8_t>(nq), *NP_BCHK(rec + 1, 1, kBkRecords) = static_cast<uint8_t>(acc[3]);
   if (nq <= 1) return;
+  // the row tables straight from the multipliers (the decodes read only the
+  // tables, not the u16 multipliers)
   if (NQ == 4 && nq == 2) {
-    fused_locator<2 * K, 256>(T, pres, W, E, PR);
+    fused_locator_pools<2 * K, 256>(T, W, PR, rec + prefix_pools_offset(N));  // the first 2K entries of W and PR
   } else {
-    fused_locator<N, 256>(T, pres, W, E, PR);
+    fused_locator_pools<N, 256>(T, W, PR, rec + prefix_pools_offset(N));
   }
-  write_row_pools(T, E, PR, static_cast<uint32_t>(nq) * K, rec + prefix_pools_offset(N));
 }
 
 // The record for caller locators (log form, all n rows: the full decode,
