@@ -194,4 +194,15 @@ p1() {  # the host-pipeline fix: whole suite, smoke, bench, e2e
   suite p1 && bench p1 && e2e p1
 }
 
+
+tpw() {  # tiles per workgroup of the config-3 encode / decode (NP_ENC_TPW, NP_REC_TPW), two passes
+  for pass in 1 2; do
+    for v in default 4 8 16 32; do
+      if [ $v = default ]; then env=""; else env="NP_ENC_TPW=$v NP_REC_TPW=$v"; fi
+      env $env timeout -k 10 200 python bench.py --no-cpu --steps 10 --warmup 3 > gpurun_out/$R/tpw_${v}_$pass.log 2>&1 || exit $?
+      tail -1 gpurun_out/$R/tpw_${v}_$pass.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('tpw $v pass $pass', d['value'], {k:v['ms'] for k,v in d['kernels'].items()})"
+    done
+  done
+}
+
 "$@"
