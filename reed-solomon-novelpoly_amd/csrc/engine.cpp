@@ -353,7 +353,7 @@ constexpr size_t kStatusBytes = 2 * sizeof(uint32_t);  // per payload (launchers
 hipError_t launch_reconstruct(np_ctx* c, const np::ReconstructArgs& a, hipStream_t s) {
   const size_t own_status = a.status ? 0 : kStatusBytes;  // scratch bytes per payload for the status
   const RecPath path = rec_path(a.n, a.k, a.shard_len);
-  const bool res = !np::fast_reconstruct_supported(a.n, a.k);
+  const bool res = !np::fast_reconstruct_supported(a.n, a.k) || np::res256_reconstruct(a.n, a.k);
   if (path == RecPath::FastRes) {
     // per-payload decode rows + row multipliers and their tables (from the
     // caller's locators when given) and the status, then the decode

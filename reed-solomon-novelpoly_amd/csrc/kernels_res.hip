@@ -125,6 +125,13 @@ constexpr bool kRecDeltaST = !(K == 1024 && NQ == 8);
 // decode 4.37 / 4.38 ms with, 4.37 / 4.36 without (noise, profiles/r04_ab.txt);
 // kept, it leaves the step start to the row loads.
 
+// K = 256 (the decode A/B of DESIGN.md §8, NP_REC_RES256): 8 levels, CQ 0-3
+// and HA 4-7, so there are no HD levels.  Each x_q stays in HA, and so does d
+// (the folds are elementwise); only D(x0) goes through HD (its position bits
+// 2-3 are in lanes there), and back.  One exchange per segment instead of two.
+template <int K>
+constexpr bool kResNoHD = (K == 256);
+
 template <int NQ>
 __host__ __device__ constexpr int res_seg(int step) {  // segments 2, 3, 1, 0 (NQ = 4); 1, 0 (NQ = 2); 7..0 (NQ = 8)
   return NQ == 8 ? 7 - step : NQ == 4 ? (step == 0 ? 2 : step == 1 ? 3 : 3 - step) : 1 - step;
@@ -201,6 +208,38 @@ __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructAr
   rh_read<kHA>(tile, fresh_v(rr.hab), XL, XH);
   rstamp(dbg, s0 + 3);
   const uint32_t* vs = DL + kDeltaWords + q * RStage<K>::kWords;
+  if constexpr (kResNoHD<K>) {
+    // K = 256: HA holds every level above 3, x_q stays there and d with it
+    if constexpr (STEP + 1 < NQ) {
+      __syncthreads();  // every wave has read the tile: the next step's tables may land in it
+      dma_row_tables(tile, pools, static_cast<uint32_t>(res_seg<NQ>(STEP + 1)) * K, K, rr.w, rr.l, K / 64);
+    }
+    ha_levels_st<K, true, res_gen<K>(I), kResPrioDec>(T, I, rr, XL, XH, vs);
+    rstamp(dbg, s0 + 4);
+    if constexpr (q == 0) {
+      // D(x0) needs position bits 2-3 in one wave: through HD and back
+      __syncthreads();  // every wave has read its HA items
+      rh_write<kHA>(tile, fresh_v(rr.hab), XL, XH);
+      __syncthreads();
+      rh_read<kHD>(tile, fresh_v(rr.hdb), XL, XH);
+      uint32_t YL[16], YH[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        YL[j] = (NQ == 2 || NQ == 8) ? XL[j] : 0u;  // d = D(x0) ^ x0 ^ ..
+        YH[j] = (NQ == 2 || NQ == 8) ? XH[j] : 0u;
+      }
+      add_derivative_hd<K>(YL, XL, rr.l);
+      add_derivative_hd<K>(YH, XH, rr.l);
+      __syncthreads();
+      rh_write<kHD>(tile, fresh_v(rr.hdb), YL, YH);
+      __syncthreads();
+      rh_read<kHA>(tile, fresh_v(rr.hab), YL, YH);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) AL[j] ^= YL[j], AH[j] ^= YH[j];
+      rstamp(dbg, s0 + 7);
+      return true;
+    }
+  } else {
   ha_levels_st<K, true, res_gen<K>(I), kResPrioDec>(T, I, rr, XL, XH, vs);
   rstamp(dbg, s0 + 4);
   __syncthreads();
@@ -214,6 +253,7 @@ __device__ __forceinline__ bool res_step(const DevTables& T, const ReconstructAr
   rstamp(dbg, s0 + 5);
   hd_levels_st<K, true, kResPrioDec>(T, I, XL, XH, vs);
   rstamp(dbg, s0 + 6);
+  }
   }
   // fold x_q into d (kernels_fast.hip rec_segments)
   if constexpr (NQ == 8 && q != 0 && rec8_kappa_res(q) != 1u) {  // d ^= kappa_q x_q, kappa_q in GF(16)
@@ -287,7 +327,7 @@ __device__ __forceinline__ void res_decode_tile(const DevTables& T, const Recons
     return;
   constexpr uint32_t kHD = RGeo<K>::kHD, lpc = RGeo<K>::kLPC;
   const Res r = res_coords<K>();
-  if constexpr ((kExp & 8192) != 0) {  // experiment (tools/res_debug_rec.py): d in natural blocks, tower coordinates
+  if constexpr ((kExp & 8192) != 0 && !kResNoHD<K>) {  // experiment (tools/res_debug_rec.py): d in natural blocks, tower coordinates
     const uint32_t c = (64u / lpc) * r.w + r.l / lpc;
 #pragma unroll
     for (int j = 0; j < 16; ++j)
@@ -297,12 +337,14 @@ __device__ __forceinline__ void res_decode_tile(const DevTables& T, const Recons
     return;
   }
   // ---- out = FFT(K, 0)(d), first k rows (inc_reconstruct.rs:80)
-  hd_levels_st<K, false, kResPrioDec>(T, 0, AL, AH, VS);
-  rstamp(dbg, 40);
-  __syncthreads();  // the last step's HD read is done
-  rh_write<kHD>(tile, fresh_v(r.hdb), AL, AH);
-  __syncthreads();
-  rh_read<kHA>(tile, fresh_v(r.hab), AL, AH);
+  if constexpr (!kResNoHD<K>) {  // (K = 256: d is in HA already)
+    hd_levels_st<K, false, kResPrioDec>(T, 0, AL, AH, VS);
+    rstamp(dbg, 40);
+    __syncthreads();  // the last step's HD read is done
+    rh_write<kHD>(tile, fresh_v(r.hdb), AL, AH);
+    __syncthreads();
+    rh_read<kHA>(tile, fresh_v(r.hab), AL, AH);
+  }
   rstamp(dbg, 41);
   ha_levels_st<K, false, 0, kResPrioDec>(T, 0, r, AL, AH, VS);
   rstamp(dbg, 42);
@@ -415,6 +457,7 @@ constexpr uint32_t res_lds(uint32_t nblk) {
 }
 static_assert(res_lds<1024>(8) <= 160u * 1024u, "k = 1024: one workgroup per CU");
 static_assert(res_lds<512>(8) <= 80u * 1024u, "k = 512: two workgroups per CU");
+static_assert(res_lds<256>(4) <= 40u * 1024u, "k = 256, n = 4k: four workgroups per CU");
 
 template <int K>
 hipError_t launch_reconstruct_res_k(const DevTables& T, const ReconstructArgs& a, hipStream_t s) {
@@ -449,9 +492,12 @@ hipError_t launch_encode_res_k(const DevTables& T, const EncodeArgs& a, hipStrea
 template <int K>
 hipError_t configure_res_k() {
   hipError_t e = hipSuccess;
-  for (const void* f : {reinterpret_cast<const void*>(&k_encode_res<K>), reinterpret_cast<const void*>(&k_reconstruct_res<K, 2>),
+  const void* enc = nullptr;  // (no K = 256 encode: the fast one serves it)
+  if constexpr (K != 256) enc = reinterpret_cast<const void*>(&k_encode_res<K>);
+  for (const void* f : {enc, reinterpret_cast<const void*>(&k_reconstruct_res<K, 2>),
                         reinterpret_cast<const void*>(&k_reconstruct_res<K, 4>),
                         reinterpret_cast<const void*>(&k_reconstruct_res<K, 8>)}) {
+    if (!f) continue;
     const hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(res_lds<K>(8)));
     if (r != hipSuccess && e == hipSuccess) e = r;
   }
@@ -460,8 +506,18 @@ hipError_t configure_res_k() {
 }  // namespace
 
 hipError_t launch_reconstruct_res(const DevTables& T, const ReconstructArgs& a, hipStream_t s) {
+  if (a.k == 256 && (a.n == 512 || a.n == 1024 || a.n == 2048)) return launch_reconstruct_res_k<256>(T, a, s);
   if (!res_reconstruct_supported(a.n, a.k)) return hipErrorInvalidValue;
   return a.k == 512 ? launch_reconstruct_res_k<512>(T, a, s) : launch_reconstruct_res_k<1024>(T, a, s);
+}
+
+// The k = 256 decode in the resident geometry instead of k_reconstruct_fast
+// (the A/B of four 64-column workgroups per CU against one
+// 256-column workgroup).  Experiment knob, read per call.
+bool res256_reconstruct(uint32_t n, uint32_t k) {
+  if (k != 256 || (n != 512 && n != 1024 && n != 2048)) return false;
+  const char* e = std::getenv("NP_REC_RES256");
+  return e && e[0] == '1';
 }
 
 hipError_t launch_encode_res(const DevTables& T, const EncodeArgs& a, hipStream_t s) {
@@ -472,7 +528,8 @@ hipError_t launch_encode_res(const DevTables& T, const EncodeArgs& a, hipStream_
 hipError_t configure_res_kernels() {
   const hipError_t e = configure_res_k<1024>();
   const hipError_t f = configure_res_k<512>();
-  return e != hipSuccess ? e : f;
+  const hipError_t g = configure_res_k<256>();
+  return e != hipSuccess ? e : f != hipSuccess ? f : g;
 }
 
 hipError_t bounds_take_res(uint32_t out[8]) { return bounds_take_tu(out); }

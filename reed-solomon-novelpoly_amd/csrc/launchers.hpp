@@ -154,6 +154,9 @@ bool res_encode_supported(uint32_t n, uint32_t k);
 bool res_reconstruct_supported(uint32_t n, uint32_t k);
 hipError_t launch_encode_res(const DevTables& T, const EncodeArgs& a, hipStream_t s);
 hipError_t launch_reconstruct_res(const DevTables& T, const ReconstructArgs& a, hipStream_t s);
+// NP_REC_RES256=1: k = 256 (n = 2k, 4k, 8k) decodes on the resident kernels
+// (a 64-column tile, four workgroups per CU) instead of the fast ones.
+bool res256_reconstruct(uint32_t n, uint32_t k);
 hipError_t configure_res_kernels();
 
 // ---- k = 2048 .. 16384 (kernels_huge.hip): M = k / 1024 resident size-1024

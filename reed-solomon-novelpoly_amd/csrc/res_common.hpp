@@ -66,13 +66,13 @@ constexpr int kRC = 64;  // columns per tile
 // Geometry of the size-K kernels (K = 512, 1024): K threads, K / 64 waves.
 template <int K>
 struct RGeo {
-  static_assert(K == 512 || K == 1024, "resident kernels: k = 512 or 1024");
+  static_assert(K == 256 || K == 512 || K == 1024, "resident kernels: k = 256 (decode A/B), 512 or 1024");
   static constexpr int kThreads = K;
   static constexpr uint32_t kTileBytes = kRC * 2 * K;  // 128 / 64 KiB
   static constexpr uint32_t kColBytes = 2 * K;
   static constexpr uint32_t kLPC = K / 64;  // HD: lanes per column
   static constexpr uint32_t kHD = 8 * kLPC;  // HD: item j at hdb ^ kHD j
-  static constexpr int kLogK = K == 1024 ? 10 : 9;
+  static constexpr int kLogK = K == 1024 ? 10 : K == 512 ? 9 : 8;
 };
 
 // ------------------------------------------------------------- LDS tile ----
@@ -87,15 +87,20 @@ struct RGeo {
 //      5; writes: rank {v2..v5} mod 16 = 4).
 // K = 512 (HD: 8 blocks of columns c .. c + 3): c0 -> 28, c1 -> 14, c2 -> 1,
 // c3 -> 25, c4 -> 20, c5 -> 27, found and checked over every sweep of both
-// sizes (and the payload tile's writes) by tools/res_swizzle.py.
+// sizes (and the payload tile's writes) by tools/res_swizzle.py.  K = 256 (the
+// decode A/B of DESIGN.md §8; HD: 4 blocks of columns c .. c + 7): c0 -> 24,
+// c1 -> 4, c2 -> 14, c3 -> 5, c4 -> 17, c5 -> 23, by the same search.
 template <int K>
 __host__ __device__ constexpr uint32_t rsw(uint32_t c) {
   if constexpr (K == 1024)
     return ((c & 1u) ? 24u : 0u) ^ ((c & 2u) ? 4u : 0u) ^ ((c & 4u) ? 1u : 0u) ^ ((c & 8u) ? 2u : 0u) ^
            ((c & 16u) ? 20u : 0u) ^ ((c & 32u) ? 8u : 0u);
-  else
+  else if constexpr (K == 512)
     return ((c & 1u) ? 28u : 0u) ^ ((c & 2u) ? 14u : 0u) ^ ((c & 4u) ? 1u : 0u) ^ ((c & 8u) ? 25u : 0u) ^
            ((c & 16u) ? 20u : 0u) ^ ((c & 32u) ? 27u : 0u);
+  else
+    return ((c & 1u) ? 24u : 0u) ^ ((c & 2u) ? 4u : 0u) ^ ((c & 4u) ? 14u : 0u) ^ ((c & 8u) ? 5u : 0u) ^
+           ((c & 16u) ? 17u : 0u) ^ ((c & 32u) ? 23u : 0u);
 }
 template <int K>
 __host__ __device__ constexpr uint32_t pq_addr(uint32_t c, uint32_t m) {
@@ -624,7 +629,8 @@ __device__ __forceinline__ void hd_levels_st(const DevTables& T, uint32_t I, uin
 // closed form SURVEY F7: D(x)[p] = x[p] ^ XOR over single bits l not in p of
 // x[p | l]): bits 0-1 inside the quad, bits 2-5 (K = 512: 2-4) in the lanes
 // of a DPP row (l & 15: quad_perm for bits 2-3, row_shl 4 / 8 for bits 4-5),
-// the rest (6-9; K = 512: 5-8) in the registers.
+// the rest (6-9; K = 512: 5-8) in the registers.  K = 256: bits 2-3 in the
+// lanes (quad_perm), 4-7 in the registers.
 template <int K>
 __device__ __forceinline__ void add_derivative_hd(uint32_t (&A)[16], uint32_t (&X)[16], uint32_t lane) {
   const uint32_t r = lane & 15u;
@@ -636,7 +642,8 @@ __device__ __forceinline__ void add_derivative_hd(uint32_t (&A)[16], uint32_t (&
     uint32_t v = xor3(x, vperm(x, x, 0x0C030301u), vperm(x, x, 0x0C0C0C02u));
     v ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0xB1, 0xF, 0xF, false)) & m0;
     v ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0x4E, 0xF, 0xF, false)) & m1;
-    v ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0x104, 0xF, 0xF, false)) & m2;
+    if constexpr (RGeo<K>::kLPC >= 8)
+      v ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0x104, 0xF, 0xF, false)) & m2;
     if constexpr (RGeo<K>::kLPC == 16)
       v ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0x108, 0xF, 0xF, false)) & m3;
 #pragma unroll
@@ -791,6 +798,7 @@ constexpr uint32_t kRowGroup = 16 * kRowSlot + 16;
 __host__ __device__ constexpr uint32_t row_slot(uint32_t r) { return kRowGroup * (r >> 4) + kRowSlot * (r & 15u); }
 static_assert(row_slot(1023) + kRowSlot <= RGeo<1024>::kTileBytes, "row tables fit the tile");
 static_assert(row_slot(511) + kRowSlot <= RGeo<512>::kTileBytes, "row tables fit the tile");
+static_assert(row_slot(255) + kRowSlot <= RGeo<256>::kTileBytes, "row tables fit the tile");
 
 // Thread t stages the table of row row0 + t (zeros for an absent row, so that
 // its premultiplied zero row stays zero without a select).

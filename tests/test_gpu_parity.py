@@ -866,3 +866,49 @@ def test_explicit_wide_codes(gpu, oracle, nw, kw, plen, erase):
     st, want = oracle.reconstruct(recv, n, k)
     assert st == 0 and got == want
     assert got[:plen] == pl
+
+
+@pytest.mark.parametrize("nw,kw,plen,batch", [(1024, 342, 512 * 771 - 5, 6), (1024, 342, 512 * 64, 4),
+                                              (512, 256, 512 * 771 - 5, 4), (1200, 400, 512 * 131 + 9, 5),
+                                              (2048, 256, 512 * 200, 4)])
+def test_reconstruct_res256(gpu, oracle, monkeypatch, nw, kw, plen, batch):
+    """k = 256 on the resident kernels (NP_REC_RES256=1, kernels_res.hip
+    kResNoHD: a 64-column tile, four workgroups per CU -- the decode A/B of
+    DESIGN.md §8) against the oracle: n = 2k, 4k and 8k (wanted_n < n: empty
+    segments), every prefix mode, 771 columns = 12 full tiles and one of 3."""
+    import torch
+
+    monkeypatch.setenv("NP_REC_RES256", "1")
+    p = npa.CodeParams.derive_parameters(nw, kw)
+    n, k = p.n(), p.k()
+    assert k == 256
+    rng = np.random.default_rng(nw + plen)
+    sl = p.make_encoder(gpu).shard_len(plen)
+    pls = np.stack([np.frombuffer(synth.payload(7300 + b, plen), dtype=np.uint8) for b in range(batch)])
+    dp = dev(pls)
+    ds = torch.empty((batch, n, sl), dtype=torch.uint8, device="cuda")
+    npa.encode_batch_dev(p, dp.data_ptr(), plen, plen, batch, ds.data_ptr(), n * sl, ctx=gpu, stream=stream())
+    wn = p.wanted_n
+    pats = [pt for pt in _prefix_patterns(n, k, rng) if pt[:wn].sum() >= k]
+    for _ in range(2):  # random erasures inside wanted_n
+        pt = np.zeros(n, np.uint8)
+        pt[rng.choice(wn, k + int(rng.integers(0, wn - k + 1)), replace=False)] = 1
+        pats.append(pt)
+    pres = np.stack([pats[b % len(pats)] for b in range(batch)])
+    pres[:, wn:] = 0  # rows >= wanted_n are never produced
+    for b in range(batch):
+        if pres[b].sum() < k:
+            pres[b, rng.choice(np.flatnonzero(pres[b, :wn] == 0), k - int(pres[b].sum()), replace=False)] = 1
+    dpres = dev(pres)
+    olen = (sl // 2) * 2 * k
+    out = torch.empty((batch, olen), dtype=torch.uint8, device="cuda")
+    npa.reconstruct_batch_dev2(p, ds.data_ptr(), sl, n * sl, dpres.data_ptr(), 0, batch, out.data_ptr(), olen,
+                               ctx=gpu, stream=stream())
+    o = host(out)
+    hs = host(ds)
+    for b in range(batch):
+        recv = [hs[b, i].tobytes() if pres[b, i] else None for i in range(n)]
+        st, want = oracle.reconstruct(recv, n, k)
+        assert st == 0
+        assert o[b].tobytes() == want, b
+        assert want[:plen] == pls[b].tobytes()

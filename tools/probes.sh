@@ -205,4 +205,35 @@ tpw() {  # tiles per workgroup of the config-3 encode / decode (NP_ENC_TPW, NP_R
   done
 }
 
+res256() {  # the k = 256 decode on the resident kernels (NP_REC_RES256) against the fast one: parity, A/B, kernel trace
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "res256" --timeout 120 --timeout-method thread \
+    > gpurun_out/$R/pytest_res256_$1.log 2>&1 || { tail -30 gpurun_out/$R/pytest_res256_$1.log; exit 1; }
+  tail -1 gpurun_out/$R/pytest_res256_$1.log
+  for pass in 1 2; do
+    for v in 0 1; do
+      NP_REC_RES256=$v timeout -k 10 200 python bench.py --no-cpu --steps 10 --warmup 3 > gpurun_out/$R/res256_${v}_$pass.log 2>&1 || exit $?
+      tail -1 gpurun_out/$R/res256_${v}_$pass.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('res256=$v pass $pass', d['value'], {k:v['ms'] for k,v in d['kernels'].items()})"
+    done
+  done
+  export NP_REC_RES256=1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/$R/prof_res256_$1 -o run -- python bench.py --no-cpu --steps 10 --warmup 3 \
+    > gpurun_out/$R/prof_res256_$1.log 2>&1 || exit $?
+  f=$(find gpurun_out/$R/prof_res256_$1 -name '*kernel_stats.csv' | head -1); head -8 "$f" | cut -c1-160
+}
+
+res256prof() {  # wave stamps of the k = 256 resident decode (NP_EXP=192 build), then its PMC passes (tools/profile_round.sh)
+  CFG=3 BATCH=1024 NP_REC_RES256=1 NP_LIB_PATH=$PWD/tools/exp/lib_st192.so timeout -k 10 300 python tools/res_stamps.py \
+    > gpurun_out/$R/res256_wave_stamps.txt 2>&1 || { tail -20 gpurun_out/$R/res256_wave_stamps.txt; exit 1; }
+  cat gpurun_out/$R/res256_wave_stamps.txt
+  NP_REC_RES256=1 timeout -k 10 900 bash tools/profile_round.sh r06_res256 3 > gpurun_out/$R/prof_res256.log 2>&1 || { tail -20 gpurun_out/$R/prof_res256.log; exit 1; }
+  f=$(find gpurun_out/prof_r06_res256/stats -name '*kernel_stats.csv' | head -1); head -6 "$f" | cut -c1-160
+}
+
+stampsab() {  # wave stamps of both config-3 decodes on one box: fast (tools/wave_stamps.py) and k = 256 resident (tools/res_stamps.py)
+  NP_LIB_PATH=$PWD/tools/exp/lib_st192.so timeout -k 10 300 python tools/wave_stamps.py > gpurun_out/$R/decode_wave_stamps.txt 2>&1 || exit $?
+  CFG=3 BATCH=1024 NP_REC_RES256=1 NP_LIB_PATH=$PWD/tools/exp/lib_st192.so timeout -k 10 300 python tools/res_stamps.py \
+    > gpurun_out/$R/res256_wave_stamps.txt 2>&1 || exit $?
+  head -8 gpurun_out/$R/decode_wave_stamps.txt; head -8 gpurun_out/$R/res256_wave_stamps.txt
+}
+
 "$@"

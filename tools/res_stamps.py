@@ -3,7 +3,10 @@
 build (kernels_res.hip `rstamp`: lane 0 of every wave writes s_memtime at each
 phase boundary into the output-stride padding).  For every phase: mean
 duration over waves and tiles, the slowest wave's, and its share of the tile.
-GPU box: NP_LIB_PATH=$PWD/tools/exp/lib_st192.so python tools/res_stamps.py"""
+GPU box: NP_LIB_PATH=$PWD/tools/exp/lib_st192.so python tools/res_stamps.py
+CFG=3 with NP_REC_RES256=1: the k = 256 decode on the resident kernels
+(k_reconstruct_res<256, 4>, 4 waves per tile; no HD levels, so the HD
+phases read 0 and the last step's fold holds D(x0)'s two exchanges)."""
 import os
 import sys
 
@@ -15,9 +18,10 @@ sys.path.insert(0, os.path.join(ROOT, "reed-solomon-novelpoly_amd", "python"))
 import novelpoly_amd as npa  # noqa: E402
 from novelpoly_amd import synth  # noqa: E402
 
-cfg = synth.CONFIGS[4]
+cfg = synth.CONFIGS[int(os.environ.get("CFG", "4"))]
 p = npa.CodeParams.derive_parameters(cfg["n_wanted"], cfg["k_wanted"])
 n, k, plen, b = p.n(), p.k(), cfg["payload"], int(os.environ.get("BATCH", "256"))
+nw = k // 64  # waves per tile
 ctx = npa.Context(0)
 torch.cuda.set_stream(torch.cuda.Stream())
 s = torch.cuda.current_stream().cuda_stream
@@ -43,7 +47,7 @@ for it in range(3):
     e1.record()
     torch.cuda.synchronize()
 print(f"reconstruct {e0.elapsed_time(e1):.3f} ms (stamped build)")
-st = out[:, out_len:].cpu().numpy().view(np.uint64).reshape(b * tiles, 16, 64).astype(np.int64)
+st = out[:, out_len:].cpu().numpy().view(np.uint64).reshape(b * tiles, 16, 64)[:, :nw].astype(np.int64)
 st = st[(st[:, :, 0] != 0).all(axis=1)]
 names = {0: "start", 1: "stage CQ delta + HA/HD tables", 40: "FFT hd levels", 41: "sync+HD write+sync+HA read",
          42: "FFT ha levels", 43: "sync+HA write+sync+CQ read", 44: "FFT cq levels",

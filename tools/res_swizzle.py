@@ -54,7 +54,7 @@ def conflicts(K, f):
     return bad
 
 
-PRODUCT = {1024: [24, 4, 1, 2, 20, 8], 512: [28, 14, 1, 25, 20, 27]}  # kernels_res rsw<K>
+PRODUCT = {1024: [24, 4, 1, 2, 20, 8], 512: [28, 14, 1, 25, 20, 27], 256: [24, 4, 14, 5, 17, 23]}  # kernels_res rsw<K>
 
 
 # The encode's quad items (res_common.hpp Qi): column quad cq at position p,
@@ -100,7 +100,7 @@ def search(K, tries=200000, seed=1):
 
 
 if __name__ == "__main__":
-    for K in [int(a) for a in sys.argv[1:]] or [1024, 512]:
+    for K in [int(a) for a in sys.argv[1:]] or [1024, 512, 256]:
         rows = PRODUCT.get(K)
         if rows is not None:
             print(K, rows, "conflicting wave-instruction groups:", conflicts(K, rsw_of(rows)))
