@@ -1281,9 +1281,18 @@ __device__ __forceinline__ bool write_status(const ReconstructArgs& a, uint32_t 
   return ok;
 }
 
+// Threads of k_prefix_locator for n = N rows: 512 from N = 512 on, so that
+// each thread's chain of dependent loads (flag, multiplier, its 80-byte
+// table) runs N / 512 times.  Config 3 (N = 1024), with the counters summed
+// per wave before the LDS atomics: 256 threads 51.0 / 50.6 us per launch,
+// 512 49.8 / 50.0, 1024 54.5 / 54.6 (two workgroups per CU instead of four;
+// profiles/r06/prefix_threads.txt); 55.4 before the wave sums.
+template <int N>
+constexpr int kPrefixThreads = N >= 512 ? 512 : 256;
+
 // NQ' = 0 marks a payload with fewer than K present rows: no decode.
-template <int K, int NQ>
-__global__ __launch_bounds__(256) void k_prefix_locator(DevTables T, ReconstructArgs a, uint8_t* out) {
+template <int K, int NQ, int NT = kPrefixThreads<NQ * K>>
+__global__ __launch_bounds__(NT) void k_prefix_locator(DevTables T, ReconstructArgs a, uint8_t* out) {
   constexpr int N = NQ * K;
   __shared__ uint32_t W[N];
   __shared__ uint8_t PR[N];
@@ -1306,7 +1315,7 @@ __global__ __launch_bounds__(256) void k_prefix_locator(DevTables T, Reconstruct
   __syncthreads();
   {
     uint32_t c1 = 0, c2 = 0, c = 0, occ = 0;
-    for (uint32_t v = tid; v < static_cast<uint32_t>(N); v += 256) {
+    for (uint32_t v = tid; v < static_cast<uint32_t>(N); v += NT) {
       const uint8_t p = *NP_BCHK(pres + v, 1, kBkPresent);
       PR[v] = p;
       W[v] = p ? 0u : 1u;
@@ -1316,10 +1325,19 @@ __global__ __launch_bounds__(256) void k_prefix_locator(DevTables T, Reconstruct
       c2 += v < 2u * K ? on : 0u;
       occ |= on << (v / K);
     }
-    atomicAdd(&acc[0], c1);
-    atomicAdd(&acc[1], c2);
-    atomicAdd(&acc[2], c);
-    atomicOr(&acc[3], occ);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {  // wave sums first: one LDS atomic per wave and counter
+      c1 += __shfl_xor(c1, o);
+      c2 += __shfl_xor(c2, o);
+      c += __shfl_xor(c, o);
+      occ |= __shfl_xor(occ, o);
+    }
+    if ((tid & 63u) == 0) {
+      atomicAdd(&acc[0], c1);
+      atomicAdd(&acc[1], c2);
+      atomicAdd(&acc[2], c);
+      atomicOr(&acc[3], occ);
+    }
   }
   __syncthreads();
   const int have1 = static_cast<int>(acc[0]), have2 = static_cast<int>(acc[1]), have = static_cast<int>(acc[2]);
@@ -1333,9 +1351,9 @@ __global__ __launch_bounds__(256) void k_prefix_locator(DevTables T, Reconstruct
   // the row tables straight from the multipliers (the decodes read only the
   // tables, not the u16 multipliers)
   if (NQ == 4 && nq == 2) {
-    fused_locator_pools<2 * K, 256>(T, W, PR, rec + prefix_pools_offset(N));  // the first 2K entries of W and PR
+    fused_locator_pools<2 * K, NT>(T, W, PR, rec + prefix_pools_offset(N));  // the first 2K entries of W and PR
   } else {
-    fused_locator_pools<N, 256>(T, W, PR, rec + prefix_pools_offset(N));
+    fused_locator_pools<N, NT>(T, W, PR, rec + prefix_pools_offset(N));
   }
 }
 
@@ -1425,7 +1443,7 @@ hipError_t launch_prefix_k(const DevTables& T, const ReconstructArgs& a, uint8_t
   if (a.locators)
     k_locator_records<K, NQ><<<static_cast<uint32_t>(a.batch), 256, 0, s>>>(T, a, out);
   else
-    k_prefix_locator<K, NQ><<<static_cast<uint32_t>(a.batch), 256, 0, s>>>(T, a, out);
+    k_prefix_locator<K, NQ><<<static_cast<uint32_t>(a.batch), kPrefixThreads<NQ * K>, 0, s>>>(T, a, out);
   return hipGetLastError();
 }
 

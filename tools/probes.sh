@@ -236,4 +236,19 @@ stampsab() {  # wave stamps of both config-3 decodes on one box: fast (tools/wav
   head -8 gpurun_out/$R/decode_wave_stamps.txt; head -8 gpurun_out/$R/res256_wave_stamps.txt
 }
 
+prefixnt() {  # thread count of k_prefix_locator (NP_PREFIX_NT): parity files, then kernel traces of the config-3 bench per count
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fuzz.py tests/test_gpu_noncodeword.py -m gpu -x -q --timeout 120 --timeout-method thread \
+    > gpurun_out/$R/pytest_prefixnt_$1.log 2>&1 || { tail -30 gpurun_out/$R/pytest_prefixnt_$1.log; exit 1; }
+  tail -1 gpurun_out/$R/pytest_prefixnt_$1.log
+  export TMPDIR=/tmp
+  for pass in 1 2; do
+    for v in 256 512 1024; do
+      NP_PREFIX_NT=$v timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/$R/prof_pnt_${v}_$pass --output-format csv -- python3 bench.py --no-cpu --steps 10 --warmup 3 \
+        > gpurun_out/$R/pnt_${v}_$pass.log 2>&1 || exit $?
+      f=$(find gpurun_out/$R/prof_pnt_${v}_$pass -name '*kernel_stats.csv' | head -1)
+      echo "nt $v pass $pass: $(grep prefix_locator "$f" | awk -F'",' '{print $2}' | cut -d, -f3) ns; bench $(tail -1 gpurun_out/$R/pnt_${v}_$pass.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['kernels']['reconstruct']['ms'])")"
+    done
+  done
+}
+
 "$@"
