@@ -251,4 +251,17 @@ prefixnt() {  # thread count of k_prefix_locator (NP_PREFIX_NT): parity files, t
   done
 }
 
+pntall() {  # k_prefix_locator thread count per n (experiment library tools/exp/lib_pnt.so, NP_PREFIX_NT): kernel-trace averages
+  export TMPDIR=/tmp
+  for shape in "cfg2:--config 2" "vc300:--n-wanted 300 --batch 1024 --erase 100" "cfg3:--config 3" "cfg4:--config 4"; do
+    name=${shape%%:*}; args=${shape#*:}
+    for v in 64 128 256 512; do
+      NP_PREFIX_NT=$v NP_LIB_PATH=$PWD/tools/exp/lib_pnt.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/$R/prof_pa_${name}_$v --output-format csv -- python3 bench.py --no-cpu --steps 5 --warmup 2 $args \
+        > gpurun_out/$R/pa_${name}_$v.log 2>&1 || exit $?
+      f=$(find gpurun_out/$R/prof_pa_${name}_$v -name '*kernel_stats.csv' | head -1)
+      echo "$name nt $v: $(grep prefix_locator "$f" | awk -F'",' '{print $2}' | cut -d, -f3) ns"
+    done
+  done
+}
+
 "$@"
