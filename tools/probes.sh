@@ -236,7 +236,7 @@ stampsab() {  # wave stamps of both config-3 decodes on one box: fast (tools/wav
   head -8 gpurun_out/$R/decode_wave_stamps.txt; head -8 gpurun_out/$R/res256_wave_stamps.txt
 }
 
-prefixnt() {  # thread count of k_prefix_locator (NP_PREFIX_NT): parity files, then kernel traces of the config-3 bench per count
+prefixnt() {  # thread count of k_prefix_locator (NP_PREFIX_NT, a knob of the build this ran on, removed since): parity files, then kernel traces of the config-3 bench per count
   timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fuzz.py tests/test_gpu_noncodeword.py -m gpu -x -q --timeout 120 --timeout-method thread \
     > gpurun_out/$R/pytest_prefixnt_$1.log 2>&1 || { tail -30 gpurun_out/$R/pytest_prefixnt_$1.log; exit 1; }
   tail -1 gpurun_out/$R/pytest_prefixnt_$1.log
@@ -251,7 +251,7 @@ prefixnt() {  # thread count of k_prefix_locator (NP_PREFIX_NT): parity files, t
   done
 }
 
-pntall() {  # k_prefix_locator thread count per n (experiment library tools/exp/lib_pnt.so, NP_PREFIX_NT): kernel-trace averages
+pntall() {  # k_prefix_locator thread count per n (experiment library tools/exp/lib_pnt.so built with an NP_PREFIX_NT knob, not in the product): kernel-trace averages
   export TMPDIR=/tmp
   for shape in "cfg2:--config 2" "vc300:--n-wanted 300 --batch 1024 --erase 100" "cfg3:--config 3" "cfg4:--config 4"; do
     name=${shape%%:*}; args=${shape#*:}
